@@ -1,0 +1,7 @@
+"""gymnasium.utils.seeding.np_random semantics: Generator(PCG64(SeedSequence(seed)))."""
+import numpy as np
+
+
+def np_random(seed=None):
+    seed_seq = np.random.SeedSequence(seed)
+    return np.random.Generator(np.random.PCG64(seed_seq)), seed_seq.entropy

@@ -1,0 +1,2 @@
+"""empty stand-in (fixture generation only)"""
+options = {}
