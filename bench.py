@@ -1,0 +1,200 @@
+#!/usr/bin/env python3
+"""Headline benchmark: env-steps/s of batched FourRooms 11x11 Hansen-4 (BASELINE.json configs[1]).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--envs B] [--mode numpy|philox] [--strong]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+Workload (per GPU): `MultistoryFourRoomsEnv(B, grid_z=1, obs_type="hansen")` (FR_MAP, cardinal,
+p_fail 1/3, goal (0,7,9), T=500), reset(seed=rank's SeedSequence(0).spawn), random int32 actions in
+[0,4) from a pre-generated device buffer. A "step" = one batched env.step over all B envs, with the
+reference's RNG reproduced bit-exactly (rng_mode=numpy, the parity-tested mode) — reset draws,
+autoreset and obs included. Envs are independent shards: each rank owns its own B envs (weak
+scaling, no data-path collective); RCCL only reduces the timing max and the episode metrics.
+
+Prints ONE JSON line (rank 0) with value = total env-steps / max-over-ranks wall time, the live
+roofline of the step kernel (HIP-event kernel time on its stream) and the CPU baseline (the numpy
+oracle, i.e. the reference's algorithm, timed on this host for a bounded sample).
+"""
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "gym-po-taxi_amd"))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec); 6.29 TB/s measured float4 copy
+# Algorithmic bytes per env-step of the numpy-mode step kernel:
+#   read  action int32 (4) + state agent|elapsed uint32 (4)
+#   write state (4) + obs int32 (4) + reward f32 (4) + terminated u8 (1) + truncated u8 (1)
+BYTES_PER_ENV_STEP = 22
+
+
+def lib_hash():
+    p = os.path.join(ROOT, "gym-po-taxi_amd", "gym_po_amd", "libgympo_amd.so")
+    with open(p, "rb") as f:
+        return hashlib.sha1(f.read()).hexdigest()[:12]
+
+
+def cpu_baseline(target_s=12.0):
+    """The numpy oracle (the reference's algorithm restated, fixture-pinned) on one host core."""
+    import numpy as np
+    from oracle.gridworld import FourRoomsOracle
+    B = 1 << 18
+    ora = FourRoomsOracle(B, 1, obs_type="hansen")
+    ora.reset_seed(0)
+    acts = np.random.default_rng(1).integers(0, 4, (8, B))
+    ora.step_seeded(acts[0])  # warm
+    t0 = time.perf_counter()
+    n = 0
+    while True:
+        ora.step_seeded(acts[n % 8])
+        n += 1
+        dt = time.perf_counter() - t0
+        if dt >= target_s or n >= 400:
+            break
+    return {"value": B * n / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"oracle.gridworld.FourRoomsOracle (numpy, reference-pinned), 2^18 envs x {n} steps, "
+                      f"1 process ({dt:.1f} s)"}
+
+
+def load_pmc(cfg_key):
+    """HBM traffic per launch from profiles/pmc_*.json, only if collected for this exact build."""
+    import glob
+    best = None
+    for fn in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json"))):
+        try:
+            d = json.load(open(fn))
+        except Exception:  # noqa: BLE001
+            continue
+        if d.get("lib_hash") == lib_hash() and d.get("config") == cfg_key:
+            best = d
+    return best
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--envs", type=int, default=1 << 20, help="envs per GPU (weak scaling)")
+    ap.add_argument("--strong", action="store_true", help="split --envs across GPUs instead")
+    ap.add_argument("--mode", default="numpy", choices=["numpy", "philox"])
+    ap.add_argument("--chunk", type=int, default=64, help="steps per gp_rollout call")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if world > 1 else 0)
+    torch.cuda.set_device(dev)
+
+    from gym_po_amd import MultistoryFourRoomsEnv
+    B = args.envs // world if args.strong else args.envs
+    env = MultistoryFourRoomsEnv(B, grid_z=1, obs_type="hansen", device=dev, rng_mode=args.mode)
+    if world == 1:
+        env.reset(seed=0)
+    else:  # shard g: SeedSequence(0, spawn_key=(g,))
+        env.seed(0, spawn_key=(rank,))
+        env.reset()
+    C = max(1, min(args.chunk, args.steps))
+    g = torch.Generator(device=dev)
+    g.manual_seed(1 + rank)
+    acts = torch.randint(0, 4, (C, B), device=dev, dtype=torch.int32, generator=g)
+    out = env._alloc_outputs(C)
+
+    def run(n):
+        done = 0
+        while done < n:
+            k = min(C, n - done)
+            if k == C:
+                env.rollout(acts, out=out)
+            else:
+                env.rollout(acts[:k], out=tuple(o[:k] for o in out))
+            done += k
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    run(args.warmup)
+    torch.cuda.synchronize(dev)
+    barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    run(args.steps)
+    torch.cuda.synchronize(dev)
+    barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    tmax = float(t.item())
+
+    # live roofline: HIP events bracketing every step-kernel launch on its stream
+    env.set_profiling(True)
+    prof_steps = min(max(args.steps // 2, 50), 2000)
+    run(prof_steps)
+    kms, nk = env.profile_read()
+    env.set_profiling(False)
+    kavg_ms = kms / max(nk, 1)
+    achieved = BYTES_PER_ENV_STEP * B / (kavg_ms * 1e-3) / 1e9
+
+    m = env.metrics()
+    mt = torch.tensor([m["episodes"], m["return_sum"], m["length_sum"], m["env_steps"]], dtype=torch.float64,
+                      device=dev)
+    if world > 1:
+        dist.all_reduce(mt)  # RCCL: the only collective (episode statistics)
+
+    total_steps = B * args.steps * world
+    cfg_key = f"fourrooms_hansen4_B{B}_{args.mode}"
+    pmc = load_pmc(cfg_key)
+    traffic = pmc["hbm_bytes_per_launch"] if pmc else None
+    line = {
+        "metric": "env steps/sec (whole node), FourRooms 11x11 Hansen-4 at 1M envs, 1/2/4/8 GPUs",
+        "value": total_steps / tmax,
+        "unit": "env-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": tmax / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong" if args.strong else "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic (uniform random actions, seeded); reference RNG stream reproduced bit-exactly",
+        "config": {"workload": "configs[1]: FourRooms 11x11 (FR_MAP) Hansen-4 obs, "
+                               f"{B} envs per GPU, MultistoryFourRoomsEnv(grid_z=1, obs_type='hansen')",
+                   "envs_per_gpu": B, "global_envs": B * world, "rng_mode": args.mode,
+                   "parallelism": f"independent env shards x{world}", "steps_per_launch_call": C},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "grid_step_numpy<GP_OBS_HANSEN>" if args.mode == "numpy" else
+                               "grid_rollout_counter<GP_OBS_HANSEN,false>",
+                     "kernel_avg_us": kavg_ms * 1e3, "bytes_per_env_step": BYTES_PER_ENV_STEP,
+                     "kernel_launches_timed": nk},
+        "episodes": {"count": mt[0].item(), "mean_return": mt[1].item() / max(mt[0].item(), 1),
+                     "mean_length": mt[2].item() / max(mt[0].item(), 1)},
+        "lib_hash": lib_hash(),
+    }
+    if rank == 0:
+        line["cpu_baseline"] = None if args.no_cpu_baseline else cpu_baseline()
+        print(json.dumps(line), flush=True)
+    env.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,51 @@
+"""Build libgympo_amd.so (HIP for gfx950) in-tree: gym_po_amd/libgympo_amd.so.
+
+    python gym-po-taxi_amd/build.py [--debug]
+
+hipcc cross-compiles without a GPU. Sources: csrc/*.hip (+ the C ABI header in include/).
+Rebuilds only when a source is newer than the library.
+"""
+import glob
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+OUT = os.path.join(HERE, "gym_po_amd", "libgympo_amd.so")
+ARCH = os.environ.get("GP_OFFLOAD_ARCH", "gfx950")
+
+
+def sources():
+    return sorted(glob.glob(os.path.join(HERE, "csrc", "*.hip")))
+
+
+def deps():
+    return sources() + glob.glob(os.path.join(HERE, "csrc", "*.h")) + [os.path.join(ROOT, "include", "gym_po_amd.h")]
+
+
+def up_to_date():
+    if not os.path.exists(OUT):
+        return False
+    t = os.path.getmtime(OUT)
+    return all(os.path.getmtime(d) <= t for d in deps())
+
+
+def build(force=False, debug=False, verbose=True):
+    if not force and up_to_date():
+        return OUT
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-shared", "-O3",
+           "-Wno-unused-result", "-I", os.path.join(ROOT, "include"), "-o", OUT + ".tmp"] + sources()
+    if debug:
+        cmd[cmd.index("-O3")] = "-O1"
+        cmd.append("-g")
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(OUT + ".tmp", OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv, debug="--debug" in sys.argv)

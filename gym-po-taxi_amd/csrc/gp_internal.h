@@ -1,0 +1,109 @@
+// gp_internal.h — handle layout shared by the per-kind backends (not part of the C ABI).
+#pragma once
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/gym_po_amd.h"
+#include "gp_common.h"
+
+// numpy Generator(PCG64) state as the host sees it.
+struct RngHost {
+  u128 state = 0, inc = 1;
+  uint32_t has_u32 = 0, uinteger = 0;
+};
+
+// SeedSequence(entropy, spawn_key).generate_state(n, uint64) — numpy bit_generator.pyx restated.
+std::vector<uint64_t> seed_sequence_u64(const std::vector<uint32_t>& entropy, const std::vector<uint32_t>& spawn_key,
+                                        int n_words64);
+RngHost pcg64_from_seed(const std::vector<uint32_t>& entropy, const std::vector<uint32_t>& spawn_key);
+// P(argmax = k) for Multinomial(n, uniform over m) counts, ties -> first (taxi reset law).
+std::vector<double> argmax_multinomial_distribution(int m, int n);
+// Radix-64 jump tables (JT_LEVELS x 64) for increment `inc`.
+std::vector<PcgJump> build_jump_tables(u128 inc);
+
+// Per-kind backend interface; gp_env owns one.
+// hipEvent pairs around the step-kernel launches (gp_set_profiling / gp_profile_read).
+struct KernelTimer {
+  bool on = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+  size_t used = 0;
+  double acc_ms = 0;
+  int64_t acc_n = 0;
+  void begin(hipStream_t s);
+  void end(hipStream_t s);
+  int read(double* ms, int64_t* n);
+  ~KernelTimer();
+};
+
+struct EnvBackend {
+  KernelTimer timer;
+  int64_t B = 0;
+  int device = 0;
+  int rng_mode = GP_RNG_NUMPY;
+  int obs_dtype = GP_DTYPE_I32;
+  int obs_width = 1;
+  bool has_reset = false;
+  RngHost rng;                 // host copy of the numpy-mode RNG state (authoritative until uploaded)
+  uint32_t philox_key[2] = {0, 0};
+  virtual ~EnvBackend() {}
+  virtual int seed(const RngHost& r, const uint32_t key[2]) = 0;
+  virtual int set_rng_state(const RngHost& r) = 0;
+  virtual int get_rng_state(RngHost* r) = 0;
+  virtual int reset(void* obs, hipStream_t s) = 0;
+  virtual int step(const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc, hipStream_t s) = 0;
+  virtual int rollout(int K, const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc, hipStream_t s);
+  virtual int get_state(void* a, void* b, void* c, void* d, hipStream_t s) = 0;
+  virtual int set_state(const void* a, const void* b, const void* c, const void* d, hipStream_t s) = 0;
+  virtual int set_replay(const void* u, const void* i0, const void* i1, const void* f0, const void* f1) {
+    gp_set_error("replay mode not supported by this env kind");
+    return GP_E_UNSUPPORTED;
+  }
+  virtual int valid_cells(int which, int32_t* out, int cap) const { return 0; }
+  virtual int metrics(double out[4]) = 0;
+  virtual int reset_distribution(double* out, int cap) const {
+    gp_set_error("no reset distribution for this env kind");
+    return GP_E_UNSUPPORTED;
+  }
+  size_t obs_elem_size() const { return obs_dtype == GP_DTYPE_U8 ? 1 : 4; }
+  virtual size_t rollout_action_bytes_per_env() const { return 4; }
+};
+
+std::unique_ptr<EnvBackend> make_grid_backend(const gp_grid_config* cfg, int64_t B, int device, int rng_mode, int* err);
+std::unique_ptr<EnvBackend> make_taxi_backend(const gp_taxi_config* cfg, int64_t B, int device, int rng_mode, int* err);
+std::unique_ptr<EnvBackend> make_crooms_backend(const gp_crooms_config* cfg, int64_t B, int device, int rng_mode,
+                                                int* err);
+std::unique_ptr<EnvBackend> make_anttag_backend(const gp_anttag_config* cfg, int64_t B, int device, int rng_mode,
+                                                int* err);
+
+// Small device-buffer owner.
+struct DevBuf {
+  void* p = nullptr;
+  size_t n = 0;
+  DevBuf() {}
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  int alloc(size_t bytes) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = bytes;
+    if (bytes == 0) return GP_OK;
+    GP_HIP_CHECK(hipMalloc(&p, bytes));
+    GP_HIP_CHECK(hipMemset(p, 0, bytes));
+    return GP_OK;
+  }
+  template <class T>
+  int upload(const std::vector<T>& v) {
+    int e = alloc(v.size() * sizeof(T) + 16);
+    if (e) return e;
+    if (!v.empty()) GP_HIP_CHECK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    return GP_OK;
+  }
+  template <class T>
+  T* as() const {
+    return (T*)p;
+  }
+};

@@ -1,0 +1,1419 @@
+// grid.hip — GP_KIND_GRID: batched Multistory FourRooms (msrooms.py) and ROOMS (rooms.py).
+//
+// One env per lane-slot, 4 consecutive envs per thread (16-B vector loads/stores), 256 threads
+// per block (1024 envs per block). State in HBM is one uint32 per env (agent cell | elapsed<<16)
+// plus a uint16 goal cell when goals are random. Static tables (move table with the stair
+// transit folded in, Hansen bases, obs windows, valid-cell lists) are built on the host once.
+//
+// RNG modes
+//   GP_RNG_NUMPY  seed-identical to the reference's numpy Generator(PCG64):
+//     step(): random(B) -> each env jumps the PCG64 state to its own stream position (radix-64
+//     jump tables), the action-failure compare is done on integers (k > floor(cumsum*2^53));
+//     resets: choice(valid, b) over the resetting envs in ascending order = Lemire-32 draws on
+//     the buffered 32-bit halves. The resetting envs' ranks come from a single-pass
+//     decoupled-lookback scan (ticket-ordered blocks, agent-scope status words). Lemire
+//     rejections (p ~ 1e-8 per draw) are detected per word position in the same pass and take
+//     an exact block-serial slow path. The last block publishes the next PCG64 state.
+//   GP_RNG_PHILOX counter-based Philox4x32-10 keyed by (seed, env, global step): no scan, so K
+//     steps fuse into one launch with the env state in registers (gp_rollout).
+//   GP_RNG_REPLAY pre-decided per-env draws (parity harness for the Philox path).
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <cmath>
+
+#include "gp_internal.h"
+
+namespace {
+
+constexpr int TPB = 256;
+constexpr int EPT = 4;
+constexpr int EPB = TPB * EPT;
+constexpr uint32_t SPIN_LIMIT = 1u << 24;
+
+struct alignas(16) GridCtl {
+  uint64_t s_hi, s_lo, inc_hi, inc_lo;  // PCG64 state at step start, increment
+  uint32_t has_u32, uinteger;           // numpy's buffered 32-bit half
+  uint32_t ticket[2];                   // dynamic block tickets of the two lookback passes
+  uint32_t b_total, w_after1;           // resets this step / absolute word index after call 1
+  uint32_t pad[2];
+};
+
+struct alignas(64) GridCtlBlock {
+  GridCtl rec[2];
+  uint32_t parity;     // which rec is current
+  uint32_t err;        // bit0: lookback spin timeout
+  uint64_t step;       // philox global step counter
+  uint32_t done;       // philox done counter
+  uint32_t pad;
+  double return_sum;   // metrics
+  unsigned long long episodes, length_sum, env_steps;
+};
+
+struct GridDev {
+  int32_t B, nblk;
+  int32_t nact, ncells;
+  int32_t obs_kind, obs_dirs, obs_goal, obs_n, obs_width, ndim;
+  int32_t fixed_goal, fixed_agent;  // -1 random
+  int32_t goal_gz, goal_gy, goal_gx; // coordinates of the fixed goal (may be off-grid)
+  int32_t n_goal_valid, n_agent_valid;
+  uint32_t thr_goal, thr_agent;
+  int32_t time_limit;
+  float r_step, r_wall, r_goal;
+  int32_t goal_code;
+  const uint16_t* move;
+  const uint64_t* thr;
+  const uint16_t* goal_valid;
+  const uint16_t* agent_valid;
+  const uint32_t* hbase;
+  const int32_t* doff;
+  const uint8_t* hvec;
+  const int32_t* t1;
+  const int32_t* t2;
+  const int16_t* coords;
+  const uint8_t* window;
+  const PcgJump* jt;
+  uint32_t* ae;
+  uint16_t* goal;
+  GridCtlBlock* ctl;
+  uint64_t* status;  // [2 parities][2 sets][nblk]
+  // philox / replay
+  uint32_t key0, key1;
+  const uint64_t* rp_u;
+  const int32_t* rp_goal;
+  const int32_t* rp_agent;
+};
+
+// ------------------------------------------------------------------ vector I/O helpers ----
+__device__ __forceinline__ bool full_aligned(const void* p, int env0, int B, int esz) {
+  return env0 + 3 < B && ((((uintptr_t)p) + (size_t)env0 * esz) & (size_t)(4 * esz - 1)) == 0;
+}
+template <class T>
+__device__ __forceinline__ void load4(const T* __restrict__ p, int env0, int B, T (&v)[4]) {
+  if (full_aligned(p, env0, B, sizeof(T))) {
+    if constexpr (sizeof(T) == 4) {
+      uint4 q = *reinterpret_cast<const uint4*>(p + env0);
+      v[0] = __builtin_bit_cast(T, q.x); v[1] = __builtin_bit_cast(T, q.y);
+      v[2] = __builtin_bit_cast(T, q.z); v[3] = __builtin_bit_cast(T, q.w);
+    } else if constexpr (sizeof(T) == 2) {
+      uint2 q = *reinterpret_cast<const uint2*>(p + env0);
+      v[0] = (T)(q.x & 0xFFFF); v[1] = (T)(q.x >> 16); v[2] = (T)(q.y & 0xFFFF); v[3] = (T)(q.y >> 16);
+    } else {
+      uint32_t q = *reinterpret_cast<const uint32_t*>(p + env0);
+      v[0] = (T)(q & 0xFF); v[1] = (T)((q >> 8) & 0xFF); v[2] = (T)((q >> 16) & 0xFF); v[3] = (T)(q >> 24);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = (env0 + i < B) ? p[env0 + i] : (T)0;
+  }
+}
+template <class T>
+__device__ __forceinline__ void store4(T* __restrict__ p, int env0, int B, const T (&v)[4]) {
+  if (full_aligned(p, env0, B, sizeof(T))) {
+    if constexpr (sizeof(T) == 4) {
+      uint4 q;
+      q.x = __builtin_bit_cast(uint32_t, v[0]); q.y = __builtin_bit_cast(uint32_t, v[1]);
+      q.z = __builtin_bit_cast(uint32_t, v[2]); q.w = __builtin_bit_cast(uint32_t, v[3]);
+      *reinterpret_cast<uint4*>(p + env0) = q;
+    } else if constexpr (sizeof(T) == 2) {
+      uint2 q;
+      q.x = (uint32_t)(uint16_t)v[0] | ((uint32_t)(uint16_t)v[1] << 16);
+      q.y = (uint32_t)(uint16_t)v[2] | ((uint32_t)(uint16_t)v[3] << 16);
+      *reinterpret_cast<uint2*>(p + env0) = q;
+    } else {
+      uint32_t q = (uint32_t)(uint8_t)v[0] | ((uint32_t)(uint8_t)v[1] << 8) | ((uint32_t)(uint8_t)v[2] << 16) |
+                   ((uint32_t)(uint8_t)v[3] << 24);
+      *reinterpret_cast<uint32_t*>(p + env0) = q;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (env0 + i < B) p[env0 + i] = v[i];
+  }
+}
+
+// ------------------------------------------------------------------ observation builders ----
+// GP_OBS_HANSEN:     hbase[agent] * goal_mult (msrooms.py:162-189 ternary / observations.py:44-71 binary)
+// GP_OBS_HANSEN_VEC: hvec[agent][i], goal -> goal_code    (msrooms.py:131-159 / observations.py:106-131)
+// GP_OBS_TABLE:      t1[agent] + t2[goal]                 (mdp / room scalars: rooms.py:23-48, msrooms.py:217-235)
+// GP_OBS_COORDS:     (z,)y,x of agent (+ goal)            (vector mdp: rooms.py:31-37, msrooms.py:218-224)
+// GP_OBS_WINDOW:     n x n window, goal -> 2              (observations.py:74-103)
+template <int OK>
+__device__ __forceinline__ void write_obs(const GridDev& p, int env, int agent, int goal, void* __restrict__ obs) {
+  const bool gvalid = (unsigned)goal < (unsigned)p.ncells;
+  if constexpr (OK == GP_OBS_HANSEN) {
+    int mult = 1;
+    if (gvalid) {
+      int diff = goal - agent;
+      for (int i = p.obs_dirs - 1; i >= 0; --i)
+        if (diff == p.doff[i]) mult = i + 1;
+    }
+    ((int32_t*)obs)[env] = (int32_t)p.hbase[agent] * mult;
+  } else if constexpr (OK == GP_OBS_HANSEN_VEC) {
+    uint8_t* o = (uint8_t*)obs + (size_t)env * p.obs_width;
+    int diff = goal - agent;
+    for (int i = 0; i < p.obs_dirs; ++i) {
+      uint8_t v = p.hvec[agent * p.obs_dirs + i];
+      if (p.obs_goal && gvalid && diff == p.doff[i]) v = (uint8_t)p.goal_code;
+      o[i] = v;
+    }
+  } else if constexpr (OK == GP_OBS_TABLE) {
+    int32_t v = p.t1[agent];
+    if (p.t2) v += p.t2[goal];
+    ((int32_t*)obs)[env] = v;
+  } else if constexpr (OK == GP_OBS_COORDS) {
+    int32_t* o = (int32_t*)obs + (size_t)env * p.obs_width;
+    const int16_t* ca = p.coords + agent * 3;
+    int k = 0;
+    if (p.ndim == 3) o[k++] = ca[0];
+    o[k++] = ca[1];
+    o[k++] = ca[2];
+    if (p.obs_goal) {
+      int gz, gy, gx;
+      if (gvalid) {
+        const int16_t* cg = p.coords + goal * 3;
+        gz = cg[0]; gy = cg[1]; gx = cg[2];
+      } else {
+        gz = p.goal_gz; gy = p.goal_gy; gx = p.goal_gx;
+      }
+      if (p.ndim == 3) o[k++] = gz;
+      o[k++] = gy;
+      o[k++] = gx;
+    }
+  } else {  // GP_OBS_WINDOW
+    const int n = p.obs_n, nn = n * n, h = n / 2;
+    uint8_t* o = (uint8_t*)obs + (size_t)env * nn;
+    const uint8_t* w = p.window + (size_t)agent * nn;
+    for (int k = 0; k < nn; ++k) o[k] = w[k];
+    if (gvalid) {
+      const int16_t* ca = p.coords + agent * 3;
+      const int16_t* cg = p.coords + goal * 3;
+      int dy = cg[1] - ca[1], dx = cg[2] - ca[2];
+      if (cg[0] == ca[0] && dy >= -h && dy <= n - 1 - h && dx >= -h && dx <= n - 1 - h) o[(dy + h) * n + (dx + h)] = 2;
+    }
+  }
+}
+
+template <int OK>
+__device__ __forceinline__ void write_obs4(const GridDev& p, int env0, const int (&agent)[4], const int (&goal)[4],
+                                           void* __restrict__ obs) {
+  if constexpr (OK == GP_OBS_HANSEN || OK == GP_OBS_TABLE) {
+    int32_t v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int a = agent[i], g = goal[i];
+      if constexpr (OK == GP_OBS_HANSEN) {
+        int mult = 1;
+        if ((unsigned)g < (unsigned)p.ncells) {
+          int diff = g - a;
+          for (int d = p.obs_dirs - 1; d >= 0; --d)
+            if (diff == p.doff[d]) mult = d + 1;
+        }
+        v[i] = (int32_t)p.hbase[a] * mult;
+      } else {
+        v[i] = p.t1[a] + (p.t2 ? p.t2[g] : 0);
+      }
+    }
+    store4<int32_t>((int32_t*)obs, env0, p.B, v);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (env0 + i < p.B) write_obs<OK>(p, env0 + i, agent[i], goal[i], obs);
+  }
+}
+
+// ------------------------------------------------------------------ numpy word stream ----
+// Absolute 32-bit word index w (counted from the first word after the step's random(B)) ->
+// the u64 draw index and half, honouring numpy's buffered half (has_uint32 at step start).
+struct Stream {
+  u128 s0, inc;
+  uint32_t h0, u0;
+  uint32_t U0;  // u64 draws consumed before the word stream starts (B for step, 0 for reset)
+};
+
+__device__ __forceinline__ uint32_t word_at(const GridDev& p, const Stream& st, uint32_t w) {
+  if (st.h0 && w == 0) return st.u0;
+  uint32_t ww = w - st.h0;
+  uint32_t q = ww >> 1;
+  uint64_t x = pcg_output(pcg_jump(p.jt, st.s0, st.U0 + q + 1));
+  return (ww & 1) ? (uint32_t)(x >> 32) : (uint32_t)x;
+}
+
+// The 4 consecutive words w0..w0+3.
+__device__ __forceinline__ void words4(const GridDev& p, const Stream& st, uint32_t w0, uint32_t (&out)[4]) {
+  uint32_t k = 0;
+  uint32_t w = w0;
+  if (st.h0 && w == 0) {
+    out[0] = st.u0;
+    k = 1;
+    w = 1;
+  }
+  uint32_t ww = w - st.h0;
+  uint32_t q = ww >> 1;
+  u128 s = pcg_jump(p.jt, st.s0, st.U0 + q + 1);
+  uint64_t x = pcg_output(s);
+  uint32_t half = ww & 1;
+  for (; k < 4; ++k) {
+    out[k] = half ? (uint32_t)(x >> 32) : (uint32_t)x;
+    if (half) {
+      s = pcg_step(s, st.inc);
+      x = pcg_output(s);
+    }
+    half ^= 1;
+  }
+}
+
+// ------------------------------------------------------------------ block scan + lookback ----
+struct ScanShared {
+  uint32_t wsum[TPB / 64];
+  uint32_t wrej[TPB / 64];
+  uint32_t excl, exrej, total, blkrej;
+  uint32_t ticket;
+  uint32_t pos[EPB];  // slow path: absolute word positions of this block's accepted draws
+};
+
+__device__ __forceinline__ uint64_t ld_status(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_status(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Exclusive block prefix of c (reset count per thread) and OR of r (rejection seen); then the
+// decoupled lookback over predecessor blocks (ticket order). Leaves results in sh.
+__device__ void scan_and_lookback(const GridDev& p, uint64_t* __restrict__ status, int blk, uint32_t c, uint32_t r,
+                                  uint32_t& excl_thread, ScanShared& sh) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  uint32_t x = c;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  const bool wr = __any((int)r);
+  if (lane == 63) {
+    sh.wsum[wid] = x;
+    sh.wrej[wid] = wr ? 1u : 0u;
+  }
+  __syncthreads();
+  uint32_t woff = 0, tot = 0, brej = 0;
+#pragma unroll
+  for (int w = 0; w < TPB / 64; ++w) {
+    if (w < wid) woff += sh.wsum[w];
+    tot += sh.wsum[w];
+    brej |= sh.wrej[w];
+  }
+  excl_thread = x - c + woff;
+  if (wid == 0) {
+    uint32_t excl = 0, exrej = 0;
+    if (blk == 0) {
+      if (lane == 0) st_status(&status[0], st_pack(ST_FLAG_P, brej, tot));
+    } else {
+      if (lane == 0) st_status(&status[blk], st_pack(ST_FLAG_A, brej, tot));
+      int base = blk - 1;
+      while (true) {
+        const int idx = base - lane;
+        uint64_t s = idx >= 0 ? ld_status(&status[idx]) : st_pack(ST_FLAG_P, 0, 0);
+        uint32_t spins = 0;
+        while (__any(st_flag(s) == ST_FLAG_X)) {
+          if (st_flag(s) == ST_FLAG_X) s = ld_status(&status[idx]);
+          if (++spins > SPIN_LIMIT) {
+            if (lane == 0) atomicOr(&p.ctl->err, 1u);
+            s = st_pack(ST_FLAG_P, 0, 0);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        const unsigned long long pm = __ballot(st_flag(s) == ST_FLAG_P);
+        const int first = pm ? __builtin_ctzll(pm) : 64;
+        uint32_t v = lane <= first ? st_count(s) : 0u;
+        uint32_t rj = lane <= first ? st_rej(s) : 0u;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+          v += __shfl_xor(v, d, 64);
+          rj |= __shfl_xor(rj, d, 64);
+        }
+        excl += v;
+        exrej |= rj;
+        if (pm) break;
+        base -= 64;
+      }
+      if (lane == 0) st_status(&status[blk], st_pack(ST_FLAG_P, exrej | brej, excl + tot));
+    }
+    if (lane == 0) {
+      sh.excl = excl;
+      sh.exrej = exrej;
+      sh.total = tot;
+      sh.blkrej = brej;
+    }
+  }
+  __syncthreads();
+}
+
+// Slow path (a Lemire rejection somewhere before this block's draws): wave 0 walks the word
+// stream from `wbase`, recording the absolute positions of the accepted draws with rank in
+// [jlo, jhi) into sh.pos. Returns (to wave 0) the position after the last recorded draw.
+__device__ uint32_t scan_accepted(const GridDev& p, const Stream& st, uint32_t wbase, uint32_t n, uint32_t thr,
+                                  uint32_t jlo, uint32_t jhi, ScanShared& sh) {
+  const int lane = threadIdx.x & 63;
+  uint32_t acc = 0, pos = wbase, after = wbase;
+  while (acc < jhi) {
+    const uint32_t w = word_at(p, st, pos + lane);
+    const bool ok = !lemire_rejected(w, n, thr);
+    const unsigned long long m = __ballot(ok);
+    const uint32_t below = (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
+    const uint32_t j = acc + below;
+    if (ok && j >= jlo && j < jhi) {
+      sh.pos[j - jlo] = pos + lane;
+      if (j == jhi - 1) after = pos + lane + 1;
+    }
+    acc += (uint32_t)__builtin_popcountll(m);
+    pos += 64;
+  }
+  // broadcast `after` from the lane that set it
+  uint32_t a = after;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) a = max(a, __shfl_xor(a, d, 64));
+  return a;
+}
+
+// ------------------------------------------------------------------ rng finalisation ----
+// Called by the last (ticket) block of the last pass of a step/reset: publishes the next
+// PCG64 state into the other ctl record, clears the other parity's tickets/status, flips parity.
+__device__ void finalize_rng(const GridDev& p, const Stream& st, uint32_t parity, uint32_t wtot) {
+  if (threadIdx.x == 0) {
+    uint32_t used, h, u;
+    if (wtot == 0) {
+      used = 0; h = st.h0; u = st.u0;
+    } else if (st.h0) {
+      used = wtot >> 1;          // ceil((wtot-1)/2)
+      h = (wtot - 1) & 1;
+      u = st.u0;
+    } else {
+      used = (wtot + 1) >> 1;    // ceil(wtot/2)
+      h = wtot & 1;
+      u = st.u0;
+    }
+    u128 s = pcg_jump(p.jt, st.s0, st.U0 + used);
+    // numpy keeps the last buffered half in `uinteger` even after it has been consumed
+    if (used) u = (uint32_t)(pcg_output(s) >> 32);
+    GridCtl* N = &p.ctl->rec[parity ^ 1];
+    N->s_hi = hi64(s);
+    N->s_lo = lo64(s);
+    N->inc_hi = hi64(st.inc);
+    N->inc_lo = lo64(st.inc);
+    N->has_u32 = h;
+    N->uinteger = u;
+    N->ticket[0] = 0;
+    N->ticket[1] = 0;
+    N->b_total = 0;
+    N->w_after1 = 0;
+  }
+  uint64_t* other = p.status + (size_t)(parity ^ 1) * 2 * p.nblk;
+  for (int i = threadIdx.x; i < 2 * p.nblk; i += TPB) other[i] = 0;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    __hip_atomic_store(&p.ctl->parity, parity ^ 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+__device__ __forceinline__ uint32_t read_parity(const GridDev& p) {
+  return __hip_atomic_load(&p.ctl->parity, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Per-block metrics (episode count / return / length / env-steps) -> 4 atomics per block.
+__device__ void add_metrics(const GridDev& p, float rsum, uint32_t eps, uint32_t lens, uint32_t nsteps) {
+  __shared__ float s_r[TPB / 64];
+  __shared__ uint32_t s_e[TPB / 64], s_l[TPB / 64], s_n[TPB / 64];
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    rsum += __shfl_xor(rsum, d, 64);
+    eps += __shfl_xor(eps, d, 64);
+    lens += __shfl_xor(lens, d, 64);
+    nsteps += __shfl_xor(nsteps, d, 64);
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) { s_r[wid] = rsum; s_e[wid] = eps; s_l[wid] = lens; s_n[wid] = nsteps; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float r = 0; uint32_t e = 0, l = 0, n = 0;
+    for (int w = 0; w < TPB / 64; ++w) { r += s_r[w]; e += s_e[w]; l += s_l[w]; n += s_n[w]; }
+    if (r != 0.f) atomicAdd(&p.ctl->return_sum, (double)r);
+    if (e) atomicAdd(&p.ctl->episodes, (unsigned long long)e);
+    if (l) atomicAdd(&p.ctl->length_sum, (unsigned long long)l);
+    atomicAdd(&p.ctl->env_steps, (unsigned long long)n);
+  }
+}
+
+// ------------------------------------------------------------------ the env transition ----
+// msrooms.py:398-411 / rooms.py:208-220 for one env, given its effective action.
+struct Trans {
+  int agent, goal, elapsed;
+  float rew;
+  uint8_t term, trunc;
+};
+
+__device__ __forceinline__ uint32_t effective_action(const uint64_t* __restrict__ thr, int nact, int a, uint64_t k) {
+  // action_utils.py:84-90: #{j : cumsum(P[a])_j < k*2^-53}  <=>  #{j : k > floor(cumsum_j * 2^53)}
+  uint32_t e = 0;
+  const uint64_t* t = thr + a * nact;
+  for (int j = 0; j < nact; ++j) e += (k > t[j]) ? 1u : 0u;
+  return e;
+}
+
+__device__ __forceinline__ Trans transition(const GridDev& p, uint32_t ae, int goal, int a, uint64_t k53,
+                                            const uint64_t* thr) {
+  Trans t;
+  const int agent = (int)(ae & 0xFFFF);
+  t.elapsed = (int)(ae >> 16) + 1;
+  if (a < 0) a += p.nact;               // numpy negative indexing of action_matrix[action]
+  a = min(max(a, 0), p.nact - 1);       // (out-of-range actions raise in the reference; clamped here)
+  const uint32_t eff = min(effective_action(thr, p.nact, a, k53), (uint32_t)p.nact - 1);
+  const uint16_t m = p.move[agent * p.nact + (int)eff];
+  t.agent = m & 0x7FFF;
+  const bool blocked = (m >> 15) != 0;
+  t.goal = goal;
+  t.term = (t.agent == goal) ? 1 : 0;
+  t.rew = t.term ? p.r_goal : (blocked ? p.r_wall : p.r_step);
+  t.trunc = (t.elapsed > p.time_limit) ? 1 : 0;
+  return t;
+}
+
+// ------------------------------------------------------------------ kernels: numpy mode ----
+// Pass flags
+#define PF_FUSED_CALL 1   // this pass performs a choice() call for its resetting envs
+#define PF_CALL_GOAL 2    // the call samples goals (else agents)
+#define PF_FINAL 4        // this pass publishes the next rng state
+#define PF_OBS_RESET 8    // write obs for the resetting envs (their sampling is complete)
+#define PF_STEP 16        // (choice pass) flags come from term|trunc, else every env resets
+
+template <int OK>
+__global__ __launch_bounds__(TPB) void grid_step_numpy(GridDev p, const int32_t* __restrict__ act,
+                                                       void* __restrict__ obs, float* __restrict__ rew,
+                                                       uint8_t* __restrict__ term, uint8_t* __restrict__ trunc,
+                                                       int flags) {
+  __shared__ ScanShared sh;
+  __shared__ uint64_t s_thr[64];
+  const uint32_t parity = read_parity(p);
+  GridCtl* C = &p.ctl->rec[parity];
+  if (threadIdx.x == 0) sh.ticket = atomicAdd(&C->ticket[0], 1u);
+  if (threadIdx.x < p.nact * p.nact) s_thr[threadIdx.x] = p.thr[threadIdx.x];
+  __syncthreads();
+  const int blk = (int)sh.ticket;
+  Stream st;
+  st.s0 = mk128(C->s_hi, C->s_lo);
+  st.inc = mk128(C->inc_hi, C->inc_lo);
+  st.h0 = C->has_u32;
+  st.u0 = C->uinteger;
+  st.U0 = (uint32_t)p.B;
+  const int env0 = blk * EPB + threadIdx.x * EPT;
+
+  int32_t a4[4];
+  uint32_t ae4[4];
+  load4<int32_t>(act, env0, p.B, a4);
+  load4<uint32_t>(p.ae, env0, p.B, ae4);
+  int g4[4];
+  if (p.fixed_goal < 0) {
+    uint16_t gg[4];
+    load4<uint16_t>(p.goal, env0, p.B, gg);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) g4[i] = gg[i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) g4[i] = p.fixed_goal;
+  }
+
+  // random(B): env e draws the u64 at stream position e+1 (action_utils.py:84)
+  uint64_t k4[4];
+  {
+    u128 s = pcg_jump(p.jt, st.s0, (uint32_t)env0 + 1);
+    k4[0] = pcg_output(s) >> 11;
+#pragma unroll
+    for (int i = 1; i < 4; ++i) {
+      s = pcg_step(s, st.inc);
+      k4[i] = pcg_output(s) >> 11;
+    }
+  }
+  Trans t4[4];
+  uint32_t c = 0;
+  int f4[4];
+  float rsum = 0.f;
+  uint32_t eps = 0, lens = 0, nst = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    t4[i] = transition(p, ae4[i], g4[i], a4[i], k4[i], s_thr);
+    const bool valid = env0 + i < p.B;
+    f4[i] = valid && (t4[i].term | t4[i].trunc);
+    c += f4[i];
+    if (valid) {
+      rsum += t4[i].rew;
+      nst += 1;
+      if (f4[i]) { eps += 1; lens += t4[i].elapsed; }
+    }
+  }
+
+  // choice(valid, b) for the resetting envs, in ascending env order (msrooms.py:383-388)
+  const bool fused = flags & PF_FUSED_CALL;
+  const bool call_goal = flags & PF_CALL_GOAL;
+  const uint32_t n = call_goal ? (uint32_t)p.n_goal_valid : (uint32_t)p.n_agent_valid;
+  const uint32_t thr = call_goal ? p.thr_goal : p.thr_agent;
+  uint32_t rj = 0;
+  if (fused) {
+    uint32_t w4[4];
+    words4(p, st, (uint32_t)env0, w4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) rj |= lemire_rejected(w4[i], n, thr) ? 1u : 0u;
+  }
+  uint64_t* status = p.status + (size_t)parity * 2 * p.nblk;
+  uint32_t excl_t;
+  scan_and_lookback(p, status, blk, c, rj, excl_t, sh);
+  const bool slow = fused && sh.total && (sh.exrej | sh.blkrej);
+  if (slow) {
+    if (threadIdx.x < 64) scan_accepted(p, st, 0, n, thr, sh.excl, sh.excl + sh.total, sh);
+    __syncthreads();
+  }
+
+  int agent4[4], goal4[4];
+  uint32_t j = excl_t;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    agent4[i] = t4[i].agent;
+    goal4[i] = t4[i].goal;
+    if (f4[i]) {
+      t4[i].elapsed = 0;
+      if (fused) {
+        const uint32_t w = slow ? sh.pos[j] : sh.excl + j;
+        const uint32_t v = lemire_value(word_at(p, st, w), n);
+        if (call_goal) goal4[i] = p.goal_valid[v];
+        else agent4[i] = p.agent_valid[v];
+      }
+      if (p.fixed_agent >= 0) agent4[i] = p.fixed_agent;
+      if (p.fixed_goal >= 0) goal4[i] = p.fixed_goal;
+      ++j;
+    }
+  }
+
+  // outputs + state
+  {
+    float r[4];
+    uint8_t tm[4], tr[4];
+    uint32_t nae[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      r[i] = t4[i].rew;
+      tm[i] = t4[i].term;
+      tr[i] = t4[i].trunc;
+      nae[i] = (uint32_t)agent4[i] | ((uint32_t)t4[i].elapsed << 16);
+    }
+    store4<float>(rew, env0, p.B, r);
+    store4<uint8_t>(term, env0, p.B, tm);
+    store4<uint8_t>(trunc, env0, p.B, tr);
+    store4<uint32_t>(p.ae, env0, p.B, nae);
+    if (p.fixed_goal < 0) {
+      uint16_t gg[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) gg[i] = (uint16_t)goal4[i];
+      store4<uint16_t>(p.goal, env0, p.B, gg);
+    }
+    if (flags & PF_OBS_RESET) {
+      write_obs4<OK>(p, env0, agent4, goal4, obs);
+    } else {
+      // resetters get their obs from the second pass
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (env0 + i < p.B && !f4[i]) write_obs<OK>(p, env0 + i, agent4[i], goal4[i], obs);
+    }
+  }
+  add_metrics(p, rsum, eps, lens, nst);
+
+  // last block: bookkeeping for the next pass / next step
+  if (blk == p.nblk - 1) {
+    const uint32_t btot = sh.excl + sh.total;
+    uint32_t wafter = 0;
+    if (fused && btot) {
+      if (sh.exrej | sh.blkrej) {
+        uint32_t a = 0;
+        if (threadIdx.x < 64) a = scan_accepted(p, st, 0, n, thr, btot - 1, btot, sh);
+        if (threadIdx.x == 0) sh.ticket = a;
+        __syncthreads();
+        wafter = sh.ticket;
+      } else {
+        wafter = btot;
+      }
+    }
+    if (flags & PF_FINAL) {
+      finalize_rng(p, st, parity, wafter);
+    } else if (threadIdx.x == 0) {
+      C->b_total = btot;
+      C->w_after1 = wafter;
+    }
+  }
+}
+
+// A standalone choice() pass: the agent draws after random goals in step(), and every sampling
+// call of reset(). Flags come from term|trunc (PF_STEP) or are all set (reset).
+template <int OK>
+__global__ __launch_bounds__(TPB) void grid_choice_numpy(GridDev p, const uint8_t* __restrict__ term,
+                                                         const uint8_t* __restrict__ trunc, void* __restrict__ obs,
+                                                         int flags, int set, uint32_t wbase_fixed, int use_wafter1,
+                                                         uint32_t U0) {
+  __shared__ ScanShared sh;
+  const uint32_t parity = read_parity(p);
+  GridCtl* C = &p.ctl->rec[parity];
+  if (threadIdx.x == 0) sh.ticket = atomicAdd(&C->ticket[set], 1u);
+  __syncthreads();
+  const int blk = (int)sh.ticket;
+  Stream st;
+  st.s0 = mk128(C->s_hi, C->s_lo);
+  st.inc = mk128(C->inc_hi, C->inc_lo);
+  st.h0 = C->has_u32;
+  st.u0 = C->uinteger;
+  st.U0 = U0;
+  const uint32_t wbase = use_wafter1 ? C->w_after1 : wbase_fixed;
+  const int env0 = blk * EPB + threadIdx.x * EPT;
+  int f4[4];
+  if (flags & PF_STEP) {
+    uint8_t tm[4], tr[4];
+    load4<uint8_t>(term, env0, p.B, tm);
+    load4<uint8_t>(trunc, env0, p.B, tr);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) f4[i] = (env0 + i < p.B) && (tm[i] | tr[i]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) f4[i] = env0 + i < p.B;
+  }
+  const bool call_goal = flags & PF_CALL_GOAL;
+  const uint32_t n = call_goal ? (uint32_t)p.n_goal_valid : (uint32_t)p.n_agent_valid;
+  const uint32_t thr = call_goal ? p.thr_goal : p.thr_agent;
+  uint32_t c = (uint32_t)(f4[0] + f4[1] + f4[2] + f4[3]);
+  uint32_t rj = 0;
+  {
+    uint32_t w4[4];
+    words4(p, st, wbase + (uint32_t)env0, w4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) rj |= lemire_rejected(w4[i], n, thr) ? 1u : 0u;
+  }
+  uint64_t* status = p.status + ((size_t)parity * 2 + set) * p.nblk;
+  uint32_t excl_t;
+  scan_and_lookback(p, status, blk, c, rj, excl_t, sh);
+  const bool slow = sh.total && (sh.exrej | sh.blkrej);
+  if (slow) {
+    if (threadIdx.x < 64) scan_accepted(p, st, wbase, n, thr, sh.excl, sh.excl + sh.total, sh);
+    __syncthreads();
+  }
+  uint32_t ae4[4];
+  load4<uint32_t>(p.ae, env0, p.B, ae4);
+  int agent4[4], goal4[4];
+  uint16_t gg[4] = {0, 0, 0, 0};
+  if (p.fixed_goal < 0) load4<uint16_t>(p.goal, env0, p.B, gg);
+  uint32_t j = excl_t;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    agent4[i] = (int)(ae4[i] & 0xFFFF);
+    goal4[i] = p.fixed_goal < 0 ? (int)gg[i] : p.fixed_goal;
+    if (f4[i]) {
+      const uint32_t w = slow ? sh.pos[j] : wbase + sh.excl + j;
+      const uint32_t v = lemire_value(word_at(p, st, w), n);
+      if (call_goal) goal4[i] = p.goal_valid[v];
+      else agent4[i] = p.agent_valid[v];
+      ++j;
+    }
+  }
+  if (call_goal) {
+    if (p.fixed_goal < 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) gg[i] = (uint16_t)goal4[i];
+      store4<uint16_t>(p.goal, env0, p.B, gg);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ae4[i] = (ae4[i] & 0xFFFF0000u) | (uint32_t)agent4[i];
+    store4<uint32_t>(p.ae, env0, p.B, ae4);
+  }
+  if (flags & PF_OBS_RESET) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (f4[i]) write_obs<OK>(p, env0 + i, agent4[i], goal4[i], obs);
+  }
+  if (blk == p.nblk - 1) {
+    const uint32_t btot = sh.excl + sh.total;
+    uint32_t wafter = wbase;
+    if (btot) {
+      if (sh.exrej | sh.blkrej) {
+        uint32_t a = 0;
+        if (threadIdx.x < 64) a = scan_accepted(p, st, wbase, n, thr, btot - 1, btot, sh);
+        if (threadIdx.x == 0) sh.ticket = a;
+        __syncthreads();
+        wafter = sh.ticket;
+      } else {
+        wafter = wbase + btot;
+      }
+    }
+    if (flags & PF_FINAL) {
+      finalize_rng(p, st, parity, wafter);
+    } else if (threadIdx.x == 0) {
+      C->b_total = btot;
+      C->w_after1 = wafter;
+    }
+  }
+}
+
+// reset(): elapsed = 0 and the fixed parts (msrooms.py:376-381 / rooms.py:184-189).
+__global__ __launch_bounds__(TPB) void grid_reset_init(GridDev p) {
+  const int env = blockIdx.x * TPB + threadIdx.x;
+  if (env >= p.B) return;
+  p.ae[env] = p.fixed_agent >= 0 ? (uint32_t)p.fixed_agent : 0u;
+  if (p.fixed_goal < 0) p.goal[env] = 0;
+}
+
+template <int OK>
+__global__ __launch_bounds__(TPB) void grid_obs_all(GridDev p, void* __restrict__ obs) {
+  const int env = blockIdx.x * TPB + threadIdx.x;
+  if (env >= p.B) return;
+  const int agent = (int)(p.ae[env] & 0xFFFF);
+  const int goal = p.fixed_goal < 0 ? (int)p.goal[env] : p.fixed_goal;
+  write_obs<OK>(p, env, agent, goal, obs);
+}
+
+// ------------------------------------------------------------------ kernels: counter modes ----
+// Philox: ctr = (env, step_lo, step_hi, 0x67706f21), key = seed-derived. One draw set per
+// env-step: x0,x1 -> 53-bit uniform; x2 -> goal index; x3 -> agent index (multiply-shift).
+__device__ __forceinline__ void philox_draws(const GridDev& p, int env, uint64_t step, uint64_t& k53, uint32_t& gi,
+                                             uint32_t& ai) {
+  Philox4 r = philox4x32_10((uint32_t)env, (uint32_t)step, (uint32_t)(step >> 32), 0x67706f21u, p.key0, p.key1);
+  k53 = ((((uint64_t)r.x[0]) << 32) | r.x[1]) >> 11;
+  gi = lemire_value(r.x[2], (uint32_t)max(p.n_goal_valid, 1));
+  ai = lemire_value(r.x[3], (uint32_t)max(p.n_agent_valid, 1));
+}
+
+// One env-step with explicit draws (counter/replay modes): same transition, reset in place.
+template <int OK>
+__device__ __forceinline__ void counter_env_step(const GridDev& p, const uint64_t* thr, int env, uint32_t& ae,
+                                                 int& goal, int a, uint64_t k53, uint32_t gi, uint32_t ai, float& r,
+                                                 uint8_t& tm, uint8_t& tr, float& rsum, uint32_t& eps, uint32_t& lens) {
+  Trans t = transition(p, ae, goal, a, k53, thr);
+  int agent = t.agent, g = goal, el = t.elapsed;
+  rsum += t.rew;
+  if (t.term | t.trunc) {
+    eps += 1;
+    lens += (uint32_t)el;
+    el = 0;
+    g = p.fixed_goal >= 0 ? p.fixed_goal : (int)p.goal_valid[gi];
+    agent = p.fixed_agent >= 0 ? p.fixed_agent : (int)p.agent_valid[ai];
+  }
+  ae = (uint32_t)agent | ((uint32_t)el << 16);
+  goal = g;
+  r = t.rew;
+  tm = t.term;
+  tr = t.trunc;
+}
+
+template <int OK, bool REPLAY>
+__global__ __launch_bounds__(TPB) void grid_rollout_counter(GridDev p, int K, const int32_t* __restrict__ act,
+                                                            void* __restrict__ obs, float* __restrict__ rew,
+                                                            uint8_t* __restrict__ term, uint8_t* __restrict__ trunc) {
+  __shared__ uint64_t s_thr[64];
+  if (threadIdx.x < p.nact * p.nact) s_thr[threadIdx.x] = p.thr[threadIdx.x];
+  __syncthreads();
+  const uint64_t step0 = p.ctl->step;
+  const int env0 = blockIdx.x * EPB + threadIdx.x * EPT;
+  uint32_t ae4[4];
+  load4<uint32_t>(p.ae, env0, p.B, ae4);
+  int g4[4];
+  if (p.fixed_goal < 0) {
+    uint16_t gg[4];
+    load4<uint16_t>(p.goal, env0, p.B, gg);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) g4[i] = gg[i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) g4[i] = p.fixed_goal;
+  }
+  float rsum = 0.f;
+  uint32_t eps = 0, lens = 0, nst = 0;
+  const size_t ow = (size_t)p.obs_width * ((OK == GP_OBS_HANSEN_VEC || OK == GP_OBS_WINDOW) ? 1 : 4);
+  for (int k = 0; k < K; ++k) {
+    const size_t off = (size_t)k * p.B;
+    int32_t a4[4];
+    load4<int32_t>(act + off, env0, p.B, a4);
+    float r[4];
+    uint8_t tm[4], tr[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int env = env0 + i;
+      uint64_t k53 = 0;
+      uint32_t gi = 0, ai = 0;
+      if (env < p.B) {
+        if constexpr (REPLAY) {
+          k53 = p.rp_u[env];
+          gi = p.rp_goal ? (uint32_t)p.rp_goal[env] : 0u;
+          ai = p.rp_agent ? (uint32_t)p.rp_agent[env] : 0u;
+        } else {
+          philox_draws(p, env, step0 + k, k53, gi, ai);
+        }
+      }
+      counter_env_step<OK>(p, s_thr, env < p.B ? env : 0, ae4[i], g4[i], a4[i], k53, gi, ai, r[i], tm[i], tr[i],
+                           rsum, eps, lens);
+      nst += env < p.B;
+    }
+    store4<float>(rew + off, env0, p.B, r);
+    store4<uint8_t>(term + off, env0, p.B, tm);
+    store4<uint8_t>(trunc + off, env0, p.B, tr);
+    int ag[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ag[i] = (int)(ae4[i] & 0xFFFF);
+    write_obs4<OK>(p, env0, ag, g4, (uint8_t*)obs + (size_t)k * p.B * ow);
+  }
+  store4<uint32_t>(p.ae, env0, p.B, ae4);
+  if (p.fixed_goal < 0) {
+    uint16_t gg[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) gg[i] = (uint16_t)g4[i];
+    store4<uint16_t>(p.goal, env0, p.B, gg);
+  }
+  add_metrics(p, rsum, eps, lens, nst);
+  if (threadIdx.x == 0) {
+    const uint32_t prev = atomicAdd(&p.ctl->done, 1u);
+    if (prev == (uint32_t)gridDim.x - 1) {
+      p.ctl->step = step0 + (uint64_t)K;
+      p.ctl->done = 0;
+    }
+  }
+}
+
+// Philox / replay reset: every env draws goal then agent from its own counter.
+template <int OK, bool REPLAY>
+__global__ __launch_bounds__(TPB) void grid_reset_counter(GridDev p, void* __restrict__ obs) {
+  const int env = blockIdx.x * TPB + threadIdx.x;
+  if (env < p.B) {
+    uint64_t k53;
+    uint32_t gi = 0, ai = 0;
+    if constexpr (REPLAY) {
+      gi = p.rp_goal ? (uint32_t)p.rp_goal[env] : 0u;
+      ai = p.rp_agent ? (uint32_t)p.rp_agent[env] : 0u;
+    } else {
+      philox_draws(p, env, p.ctl->step, k53, gi, ai);
+    }
+    const int g = p.fixed_goal >= 0 ? p.fixed_goal : (int)p.goal_valid[gi];
+    const int a = p.fixed_agent >= 0 ? p.fixed_agent : (int)p.agent_valid[ai];
+    p.ae[env] = (uint32_t)a;
+    if (p.fixed_goal < 0) p.goal[env] = (uint16_t)g;
+    write_obs<OK>(p, env, a, g, obs);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t prev = atomicAdd(&p.ctl->done, 1u);
+    if (prev == (uint32_t)gridDim.x - 1) {
+      p.ctl->step = p.ctl->step + 1;
+      p.ctl->done = 0;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ state access ----
+__global__ void grid_get_state(GridDev p, int32_t* agent, int32_t* goal, int32_t* elapsed) {
+  const int env = blockIdx.x * TPB + threadIdx.x;
+  if (env >= p.B) return;
+  const uint32_t ae = p.ae[env];
+  if (agent) agent[env] = (int32_t)(ae & 0xFFFF);
+  if (elapsed) elapsed[env] = (int32_t)(ae >> 16);
+  if (goal) goal[env] = p.fixed_goal >= 0 ? p.fixed_goal : (int32_t)p.goal[env];
+}
+__global__ void grid_set_state(GridDev p, const int32_t* agent, const int32_t* goal, const int32_t* elapsed) {
+  const int env = blockIdx.x * TPB + threadIdx.x;
+  if (env >= p.B) return;
+  uint32_t ae = p.ae[env];
+  if (agent) ae = (ae & 0xFFFF0000u) | (uint32_t)min(max(agent[env], 0), p.ncells - 1);
+  if (elapsed) ae = (ae & 0xFFFFu) | ((uint32_t)min(max(elapsed[env], 0), 65535) << 16);
+  p.ae[env] = ae;
+  if (goal && p.fixed_goal < 0) p.goal[env] = (uint16_t)min(max(goal[env], 0), p.ncells - 1);
+}
+
+// ------------------------------------------------------------------ host backend ----
+struct GridBackend : EnvBackend {
+  GridDev d{};
+  int flavor = 0;
+  int depth = 1, height = 0, width = 0;
+  std::vector<int32_t> cells;
+  std::vector<uint16_t> goal_valid_h, agent_valid_h;
+  DevBuf b_move, b_thr, b_gv, b_av, b_hbase, b_doff, b_hvec, b_t1, b_t2, b_coords, b_window, b_jt, b_ae, b_goal,
+      b_ctl, b_status;
+  // replay pointers for the next step
+  const uint64_t* rp_u = nullptr;
+  const int32_t* rp_goal = nullptr;
+  const int32_t* rp_agent = nullptr;
+
+  int build(const gp_grid_config* cfg);
+  int upload_rng();
+  int seed(const RngHost& r, const uint32_t key[2]) override {
+    rng = r;
+    philox_key[0] = key[0];
+    philox_key[1] = key[1];
+    d.key0 = key[0];
+    d.key1 = key[1];
+    return upload_rng();
+  }
+  int set_rng_state(const RngHost& r) override {
+    rng = r;
+    return upload_rng();
+  }
+  int get_rng_state(RngHost* r) override;
+  int reset(void* obs, hipStream_t s) override;
+  int step(const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc, hipStream_t s) override;
+  int rollout(int K, const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc, hipStream_t s) override;
+  int get_state(void* a, void* b, void* c, void* dd, hipStream_t s) override {
+    hipLaunchKernelGGL(grid_get_state, dim3((unsigned)((B + TPB - 1) / TPB)), dim3(TPB), 0, s, d, (int32_t*)a,
+                       (int32_t*)b, (int32_t*)c);
+    GP_HIP_CHECK(hipGetLastError());
+    return GP_OK;
+  }
+  int set_state(const void* a, const void* b, const void* c, const void* dd, hipStream_t s) override {
+    hipLaunchKernelGGL(grid_set_state, dim3((unsigned)((B + TPB - 1) / TPB)), dim3(TPB), 0, s, d,
+                       (const int32_t*)a, (const int32_t*)b, (const int32_t*)c);
+    GP_HIP_CHECK(hipGetLastError());
+    has_reset = true;
+    return GP_OK;
+  }
+  int set_replay(const void* u, const void* i0, const void* i1, const void* f0, const void* f1) override {
+    if (rng_mode != GP_RNG_REPLAY) {
+      gp_set_error("gp_set_replay requires GP_RNG_REPLAY");
+      return GP_E_STATE;
+    }
+    rp_u = (const uint64_t*)u;
+    rp_goal = (const int32_t*)i0;
+    rp_agent = (const int32_t*)i1;
+    return GP_OK;
+  }
+  int valid_cells(int which, int32_t* out, int cap) const override {
+    const std::vector<uint16_t>& v = which == 0 ? goal_valid_h : agent_valid_h;
+    for (int i = 0; i < (int)v.size() && i < cap; ++i) out[i] = v[i];
+    return (int)v.size();
+  }
+  int metrics(double out[4]) override;
+};
+
+int GridBackend::upload_rng() {
+  GridCtlBlock h;
+  GP_HIP_CHECK(hipMemcpy(&h, d.ctl, sizeof(h), hipMemcpyDeviceToHost));
+  GridCtl& c = h.rec[h.parity];
+  c.s_hi = hi64(rng.state);
+  c.s_lo = lo64(rng.state);
+  c.inc_hi = hi64(rng.inc);
+  c.inc_lo = lo64(rng.inc);
+  c.has_u32 = rng.has_u32;
+  c.uinteger = rng.uinteger;
+  c.ticket[0] = c.ticket[1] = 0;
+  h.step = 0;
+  h.done = 0;
+  GP_HIP_CHECK(hipMemcpy(d.ctl, &h, sizeof(h), hipMemcpyHostToDevice));
+  std::vector<PcgJump> jt = build_jump_tables(rng.inc);
+  GP_HIP_CHECK(hipMemcpy(b_jt.p, jt.data(), jt.size() * sizeof(PcgJump), hipMemcpyHostToDevice));
+  return GP_OK;
+}
+
+int GridBackend::get_rng_state(RngHost* r) {
+  GP_HIP_CHECK(hipDeviceSynchronize());
+  GridCtlBlock h;
+  GP_HIP_CHECK(hipMemcpy(&h, d.ctl, sizeof(h), hipMemcpyDeviceToHost));
+  const GridCtl& c = h.rec[h.parity];
+  r->state = mk128(c.s_hi, c.s_lo);
+  r->inc = mk128(c.inc_hi, c.inc_lo);
+  r->has_u32 = c.has_u32;
+  r->uinteger = c.uinteger;
+  if (h.err) {
+    gp_set_error("device error flags 0x%x (lookback spin timeout)", h.err);
+    return GP_E_HIP;
+  }
+  return GP_OK;
+}
+
+int GridBackend::metrics(double out[4]) {
+  GP_HIP_CHECK(hipDeviceSynchronize());
+  GridCtlBlock h;
+  GP_HIP_CHECK(hipMemcpy(&h, d.ctl, sizeof(h), hipMemcpyDeviceToHost));
+  out[0] = (double)h.episodes;
+  out[1] = h.return_sum;
+  out[2] = (double)h.length_sum;
+  out[3] = (double)h.env_steps;
+  return GP_OK;
+}
+
+template <class F>
+static int dispatch_obs(int ok, F&& f) {
+  switch (ok) {
+    case GP_OBS_HANSEN: return f(std::integral_constant<int, GP_OBS_HANSEN>());
+    case GP_OBS_HANSEN_VEC: return f(std::integral_constant<int, GP_OBS_HANSEN_VEC>());
+    case GP_OBS_TABLE: return f(std::integral_constant<int, GP_OBS_TABLE>());
+    case GP_OBS_COORDS: return f(std::integral_constant<int, GP_OBS_COORDS>());
+    case GP_OBS_WINDOW: return f(std::integral_constant<int, GP_OBS_WINDOW>());
+  }
+  gp_set_error("bad obs kind %d", ok);
+  return GP_E_INVALID;
+}
+
+int GridBackend::reset(void* obs, hipStream_t s) {
+  // zero metrics
+  {
+    GridCtlBlock h;
+    GP_HIP_CHECK(hipMemcpyAsync(&h, d.ctl, sizeof(h), hipMemcpyDeviceToHost, s));
+    GP_HIP_CHECK(hipStreamSynchronize(s));
+    h.return_sum = 0;
+    h.episodes = h.length_sum = h.env_steps = 0;
+    GP_HIP_CHECK(hipMemcpyAsync(d.ctl, &h, sizeof(h), hipMemcpyHostToDevice, s));
+    GP_HIP_CHECK(hipStreamSynchronize(s));
+  }
+  const unsigned g1 = (unsigned)((B + TPB - 1) / TPB);
+  const bool rgoal = d.fixed_goal < 0, ragent = d.fixed_agent < 0;
+  int e = dispatch_obs(d.obs_kind, [&](auto okc) -> int {
+    constexpr int OK = decltype(okc)::value;
+    if (rng_mode == GP_RNG_NUMPY) {
+      hipLaunchKernelGGL(grid_reset_init, dim3(g1), dim3(TPB), 0, s, d);
+      if (rgoal) {
+        int fl = PF_CALL_GOAL | (ragent ? 0 : (PF_FINAL | PF_OBS_RESET));
+        hipLaunchKernelGGL(grid_choice_numpy<OK>, dim3(d.nblk), dim3(TPB), 0, s, d, (const uint8_t*)nullptr,
+                           (const uint8_t*)nullptr, obs, fl, 0, 0u, 0, 0u);
+      }
+      if (ragent) {
+        int fl = PF_FINAL | PF_OBS_RESET;
+        hipLaunchKernelGGL(grid_choice_numpy<OK>, dim3(d.nblk), dim3(TPB), 0, s, d, (const uint8_t*)nullptr,
+                           (const uint8_t*)nullptr, obs, fl, rgoal ? 1 : 0, 0u, rgoal ? 1 : 0, 0u);
+      }
+      if (!rgoal && !ragent) hipLaunchKernelGGL(grid_obs_all<OK>, dim3(g1), dim3(TPB), 0, s, d, obs);
+    } else if (rng_mode == GP_RNG_PHILOX) {
+      hipLaunchKernelGGL((grid_reset_counter<OK, false>), dim3(g1), dim3(TPB), 0, s, d, obs);
+    } else {
+      GridDev dd = d;
+      dd.rp_u = rp_u; dd.rp_goal = rp_goal; dd.rp_agent = rp_agent;
+      if ((rgoal && !rp_goal) || (ragent && !rp_agent)) {
+        gp_set_error("replay reset needs goal/agent index draws (gp_set_replay)");
+        return GP_E_STATE;
+      }
+      hipLaunchKernelGGL((grid_reset_counter<OK, true>), dim3(g1), dim3(TPB), 0, s, dd, obs);
+    }
+    return GP_OK;
+  });
+  if (e) return e;
+  GP_HIP_CHECK(hipGetLastError());
+  has_reset = true;
+  return GP_OK;
+}
+
+int GridBackend::step(const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc, hipStream_t s) {
+  if (!has_reset) {
+    gp_set_error("step() before reset()");
+    return GP_E_STATE;
+  }
+  const bool rgoal = d.fixed_goal < 0, ragent = d.fixed_agent < 0;
+  int e = dispatch_obs(d.obs_kind, [&](auto okc) -> int {
+    constexpr int OK = decltype(okc)::value;
+    if (rng_mode == GP_RNG_NUMPY) {
+      if (rgoal && ragent) {
+        hipLaunchKernelGGL(grid_step_numpy<OK>, dim3(d.nblk), dim3(TPB), 0, s, d, (const int32_t*)act, obs, rew,
+                           term, trunc, PF_FUSED_CALL | PF_CALL_GOAL);
+        hipLaunchKernelGGL(grid_choice_numpy<OK>, dim3(d.nblk), dim3(TPB), 0, s, d, term, trunc, obs,
+                           PF_STEP | PF_FINAL | PF_OBS_RESET, 1, 0u, 1, (uint32_t)B);
+      } else {
+        int fl = PF_FINAL | PF_OBS_RESET;
+        if (rgoal) fl |= PF_FUSED_CALL | PF_CALL_GOAL;
+        if (ragent) fl |= PF_FUSED_CALL;
+        timer.begin(s);
+        hipLaunchKernelGGL(grid_step_numpy<OK>, dim3(d.nblk), dim3(TPB), 0, s, d, (const int32_t*)act, obs, rew,
+                           term, trunc, fl);
+        timer.end(s);
+      }
+    } else if (rng_mode == GP_RNG_PHILOX) {
+      timer.begin(s);
+      hipLaunchKernelGGL((grid_rollout_counter<OK, false>), dim3(d.nblk), dim3(TPB), 0, s, d, 1,
+                         (const int32_t*)act, obs, rew, term, trunc);
+      timer.end(s);
+    } else {
+      if (!rp_u || (rgoal && !rp_goal) || (ragent && !rp_agent)) {
+        gp_set_error("replay step needs draws (gp_set_replay)");
+        return GP_E_STATE;
+      }
+      GridDev dd = d;
+      dd.rp_u = rp_u; dd.rp_goal = rp_goal; dd.rp_agent = rp_agent;
+      hipLaunchKernelGGL((grid_rollout_counter<OK, true>), dim3(d.nblk), dim3(TPB), 0, s, dd, 1,
+                         (const int32_t*)act, obs, rew, term, trunc);
+    }
+    return GP_OK;
+  });
+  if (e) return e;
+  GP_HIP_CHECK(hipGetLastError());
+  return GP_OK;
+}
+
+int GridBackend::rollout(int K, const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc,
+                         hipStream_t s) {
+  if (rng_mode != GP_RNG_PHILOX) return EnvBackend::rollout(K, act, obs, rew, term, trunc, s);
+  if (!has_reset) {
+    gp_set_error("rollout() before reset()");
+    return GP_E_STATE;
+  }
+  int e = dispatch_obs(d.obs_kind, [&](auto okc) -> int {
+    constexpr int OK = decltype(okc)::value;
+    timer.begin(s);
+    hipLaunchKernelGGL((grid_rollout_counter<OK, false>), dim3(d.nblk), dim3(TPB), 0, s, d, K, (const int32_t*)act,
+                       obs, rew, term, trunc);
+    timer.end(s);
+    return GP_OK;
+  });
+  if (e) return e;
+  GP_HIP_CHECK(hipGetLastError());
+  return GP_OK;
+}
+
+// ---- host-side table construction ----
+static const int DY8[8] = {-1, -1, 0, 1, 1, 1, 0, -1};  // action_utils.py:16-27 N,NE,E,SE,S,SW,W,NW
+static const int DX8[8] = {0, 1, 1, 1, 0, -1, -1, -1};
+
+int GridBackend::build(const gp_grid_config* cfg) {
+  flavor = cfg->flavor;
+  depth = cfg->depth;
+  height = cfg->height;
+  width = cfg->width;
+  const int nc = depth * height * width;
+  if (depth < 1 || height < 3 || width < 3 || nc >= 32768) {
+    gp_set_error("grid shape %dx%dx%d unsupported (cells must be < 32768)", depth, height, width);
+    return GP_E_INVALID;
+  }
+  if (cfg->n_actions != 4 && cfg->n_actions != 8) {
+    gp_set_error("n_actions must be 4 or 8");
+    return GP_E_INVALID;
+  }
+  if (cfg->time_limit < 0 || cfg->time_limit > 65534) {
+    gp_set_error("time_limit must be in [0, 65534] (elapsed is stored in 16 bits)");
+    return GP_E_INVALID;
+  }
+  if (B <= 0 || B > (int64_t)1 << 30) {
+    gp_set_error("num_envs must be in [1, 2^30]");
+    return GP_E_INVALID;
+  }
+  cells.assign(cfg->cells, cfg->cells + nc);
+  const int wallv = flavor == GP_FLAVOR_ROOMS ? -1 : 0;
+  auto idx = [&](int z, int y, int x) { return (z * height + y) * width + x; };
+  auto walkable = [&](int c) { return flavor == GP_FLAVOR_ROOMS ? cells[c] >= 0 : cells[c] > 0; };
+  // floor cells must not touch the border (the reference indexes neighbours without bounds checks)
+  for (int z = 0; z < depth; ++z)
+    for (int y = 0; y < height; ++y)
+      for (int x = 0; x < width; ++x)
+        if (walkable(idx(z, y, x)) && (y == 0 || x == 0 || y == height - 1 || x == width - 1)) {
+          gp_set_error("walkable cell on the map border at (%d,%d,%d)", z, y, x);
+          return GP_E_INVALID;
+        }
+  const int nact = cfg->n_actions;
+  d.nact = nact;
+  d.ncells = nc;
+  // move table: msrooms.py:401-404,415-428 / rooms.py:211-213
+  std::vector<uint16_t> move((size_t)nc * nact);
+  for (int z = 0; z < depth; ++z)
+    for (int y = 0; y < height; ++y)
+      for (int x = 0; x < width; ++x) {
+        const int c = idx(z, y, x);
+        for (int a = 0; a < nact; ++a) {
+          const int o = nact == 4 ? 2 * a : a;
+          const int ny = y + DY8[o], nx = x + DX8[o];
+          uint16_t m = (uint16_t)(c | 0x8000);
+          if (walkable(c) && ny >= 0 && nx >= 0 && ny < height && nx < width) {
+            const int nb = idx(z, ny, nx);
+            if (cells[nb] != wallv) {
+              int dest = nb;
+              if (flavor == GP_FLAVOR_MULTISTORY) {
+                if (cells[nb] == 3 && z + 1 < depth) dest = idx(z + 1, 11, 1);       // up -> (z+1, SW)
+                else if (cells[nb] == 2 && z - 1 >= 0) dest = idx(z - 1, 1, 11);     // down -> (z-1, NE)
+              }
+              m = (uint16_t)dest;
+            }
+          }
+          move[(size_t)c * nact + a] = m;
+        }
+      }
+  // action-failure thresholds (action_utils.py:38-48, 84-90) as exact integers
+  std::vector<uint64_t> thr((size_t)nact * nact);
+  const double p = cfg->action_failure_probability;
+  const double off = p / (nact - 1);
+  for (int a = 0; a < nact; ++a) {
+    double s = 0.0;
+    for (int j = 0; j < nact; ++j) {
+      s += (j == a) ? (1 - p) : off;
+      const double x = std::ldexp(s, 53);
+      thr[(size_t)a * nact + j] = x >= 18446744073709551615.0 ? ~0ull : (uint64_t)std::floor(x);
+    }
+  }
+  // valid spawn cells
+  goal_valid_h.clear();
+  agent_valid_h.clear();
+  for (int c = 0; c < nc; ++c) {
+    const int z = c / (height * width);
+    if (flavor == GP_FLAVOR_ROOMS) {
+      if (cells[c] >= 0) { goal_valid_h.push_back((uint16_t)c); agent_valid_h.push_back((uint16_t)c); }
+    } else if (cells[c] > 0) {
+      if (z == 0) agent_valid_h.push_back((uint16_t)c);
+      if (z == depth - 1) goal_valid_h.push_back((uint16_t)c);
+    }
+  }
+  d.fixed_goal = cfg->fixed_goal;
+  d.fixed_agent = cfg->fixed_agent;
+  if (d.fixed_goal < 0 && goal_valid_h.size() == 1) d.fixed_goal = goal_valid_h[0];   // choice of 1 draws nothing
+  if (d.fixed_agent < 0 && agent_valid_h.size() == 1) d.fixed_agent = agent_valid_h[0];
+  if ((d.fixed_goal < 0 && goal_valid_h.empty()) || (d.fixed_agent < 0 && agent_valid_h.empty())) {
+    gp_set_error("no valid spawn cells");
+    return GP_E_INVALID;
+  }
+  if (d.fixed_agent >= nc) {
+    gp_set_error("fixed agent outside the grid");
+    return GP_E_INVALID;
+  }
+  d.n_goal_valid = (int)goal_valid_h.size();
+  d.n_agent_valid = (int)agent_valid_h.size();
+  d.thr_goal = d.n_goal_valid > 1 ? lemire_threshold((uint32_t)d.n_goal_valid) : 0;
+  d.thr_agent = d.n_agent_valid > 1 ? lemire_threshold((uint32_t)d.n_agent_valid) : 0;
+  if (d.fixed_goal >= 0) {
+    const int fg = d.fixed_goal;
+    // (an off-grid ROOMS goal, e.g. ENDS["32"], decodes as y = fg / W, x = fg % W)
+    d.goal_gz = depth == 1 ? 0 : fg / (height * width);
+    d.goal_gy = depth == 1 ? fg / width : (fg / width) % height;
+    d.goal_gx = fg % width;
+  }
+  d.time_limit = cfg->time_limit;
+  d.r_step = cfg->step_reward;
+  d.r_wall = cfg->wall_reward;
+  d.r_goal = cfg->goal_reward;
+  d.goal_code = flavor == GP_FLAVOR_ROOMS ? 2 : 3;
+  // observation tables
+  d.obs_kind = cfg->obs_kind;
+  d.obs_dirs = cfg->obs_dirs;
+  d.obs_goal = cfg->obs_goal;
+  d.obs_n = cfg->obs_n;
+  d.ndim = flavor == GP_FLAVOR_ROOMS ? 2 : 3;
+  if ((cfg->obs_kind == GP_OBS_HANSEN || cfg->obs_kind == GP_OBS_HANSEN_VEC) && cfg->obs_dirs != 4 &&
+      cfg->obs_dirs != 8) {
+    gp_set_error("obs_dirs must be 4 or 8");
+    return GP_E_INVALID;
+  }
+  std::vector<int32_t> doff(8, 0);
+  for (int i = 0; i < 8; ++i) {
+    const int o = cfg->obs_dirs == 4 ? 2 * i : i;
+    doff[i] = i < (cfg->obs_dirs == 4 ? 4 : 8) ? DY8[o % 8] * width + DX8[o % 8] : 0x7FFFFFFF;
+  }
+  auto digit = [&](int v) -> int {
+    if (flavor == GP_FLAVOR_ROOMS) return v >= 0 ? 1 : 0;   // observations.py:64-66
+    if (v == 0) return 0;                                    // msrooms.py:182-185
+    return v <= 3 ? 2 : 1;
+  };
+  std::vector<uint32_t> hbase(nc, 0);
+  std::vector<uint8_t> hvec((size_t)nc * std::max(cfg->obs_dirs, 1), 0);
+  std::vector<int16_t> coords((size_t)nc * 3);
+  for (int c = 0; c < nc; ++c) {
+    const int z = c / (height * width), y = (c / width) % height, x = c % width;
+    coords[(size_t)c * 3] = (int16_t)z;
+    coords[(size_t)c * 3 + 1] = (int16_t)y;
+    coords[(size_t)c * 3 + 2] = (int16_t)x;
+    if (cfg->obs_kind == GP_OBS_HANSEN || cfg->obs_kind == GP_OBS_HANSEN_VEC) {
+      uint32_t hb = 0, mul = 1;
+      for (int i = 0; i < cfg->obs_dirs; ++i) {
+        const int o = cfg->obs_dirs == 4 ? 2 * i : i;
+        const int ny = y + DY8[o], nx = x + DX8[o];
+        int dg = 0;
+        if (ny >= 0 && nx >= 0 && ny < height && nx < width) dg = digit(cells[idx(z, ny, nx)]);
+        hb += (uint32_t)dg * mul;
+        mul *= flavor == GP_FLAVOR_ROOMS ? 2 : 3;
+        hvec[(size_t)c * cfg->obs_dirs + i] = (uint8_t)dg;
+      }
+      hbase[c] = hb;
+    }
+  }
+  std::vector<uint8_t> window;
+  if (cfg->obs_kind == GP_OBS_WINDOW) {
+    const int n = cfg->obs_n, h = n / 2;
+    if (n < 1 || n > 63) {
+      gp_set_error("obs_n must be in [1, 63]");
+      return GP_E_INVALID;
+    }
+    window.assign((size_t)nc * n * n, 0);
+    for (int c = 0; c < nc; ++c) {
+      const int z = c / (height * width), y = (c / width) % height, x = c % width;
+      for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) {
+          int yy = y + i - h, xx = x + j - h;
+          if (yy < 0 || xx < 0 || yy >= height || xx >= width) yy = xx = 0;  // observations.py:92-98
+          window[((size_t)c * n + i) * n + j] = (uint8_t)(cells[idx(z, yy, xx)] + 1 > 0 ? 1 : 0);
+        }
+    }
+    if (flavor != GP_FLAVOR_ROOMS) {
+      gp_set_error("window obs is only defined for ROOMS");
+      return GP_E_INVALID;
+    }
+  }
+  std::vector<int32_t> t1, t2;
+  if (cfg->obs_kind == GP_OBS_TABLE) {
+    if (!cfg->obs_table) {
+      gp_set_error("GP_OBS_TABLE needs obs_table");
+      return GP_E_INVALID;
+    }
+    t1.assign(cfg->obs_table, cfg->obs_table + nc);
+    if (cfg->obs_table2) {
+      if (d.fixed_goal >= nc) {
+        gp_set_error("goal outside the grid cannot index the goal obs table (reference raises IndexError)");
+        return GP_E_INVALID;
+      }
+      t2.assign(cfg->obs_table2, cfg->obs_table2 + nc);
+    }
+  }
+  switch (cfg->obs_kind) {
+    case GP_OBS_HANSEN: obs_dtype = GP_DTYPE_I32; obs_width = 1; break;
+    case GP_OBS_HANSEN_VEC: obs_dtype = GP_DTYPE_U8; obs_width = cfg->obs_dirs; break;
+    case GP_OBS_TABLE: obs_dtype = GP_DTYPE_I32; obs_width = 1; break;
+    case GP_OBS_COORDS: obs_dtype = GP_DTYPE_I32; obs_width = d.ndim * (cfg->obs_goal ? 2 : 1); break;
+    case GP_OBS_WINDOW: obs_dtype = GP_DTYPE_U8; obs_width = cfg->obs_n * cfg->obs_n; break;
+    default: gp_set_error("obs kind %d not valid for GRID", cfg->obs_kind); return GP_E_INVALID;
+  }
+  d.obs_width = obs_width;
+  d.B = (int32_t)B;
+  d.nblk = (int32_t)((B + EPB - 1) / EPB);
+  int e;
+  if ((e = b_move.upload(move)) || (e = b_thr.upload(thr)) || (e = b_gv.upload(goal_valid_h)) ||
+      (e = b_av.upload(agent_valid_h)) || (e = b_hbase.upload(hbase)) || (e = b_doff.upload(doff)) ||
+      (e = b_hvec.upload(hvec)) || (e = b_coords.upload(coords)) || (e = b_window.upload(window)) ||
+      (e = b_t1.upload(t1)) || (e = b_t2.upload(t2)))
+    return e;
+  if ((e = b_jt.alloc(sizeof(PcgJump) * JT_LEVELS * JT_RADIX)) || (e = b_ae.alloc(sizeof(uint32_t) * (B + 4))) ||
+      (e = b_goal.alloc(sizeof(uint16_t) * (B + 8))) || (e = b_ctl.alloc(sizeof(GridCtlBlock))) ||
+      (e = b_status.alloc(sizeof(uint64_t) * 4 * (size_t)d.nblk)))
+    return e;
+  d.move = b_move.as<uint16_t>();
+  d.thr = b_thr.as<uint64_t>();
+  d.goal_valid = b_gv.as<uint16_t>();
+  d.agent_valid = b_av.as<uint16_t>();
+  d.hbase = b_hbase.as<uint32_t>();
+  d.doff = b_doff.as<int32_t>();
+  d.hvec = b_hvec.as<uint8_t>();
+  d.t1 = t1.empty() ? nullptr : b_t1.as<int32_t>();
+  d.t2 = t2.empty() ? nullptr : b_t2.as<int32_t>();
+  d.coords = b_coords.as<int16_t>();
+  d.window = b_window.as<uint8_t>();
+  d.jt = b_jt.as<PcgJump>();
+  d.ae = b_ae.as<uint32_t>();
+  d.goal = b_goal.as<uint16_t>();
+  d.ctl = b_ctl.as<GridCtlBlock>();
+  d.status = b_status.as<uint64_t>();
+  // default seed: numpy's SeedSequence(0) until the caller seeds
+  rng = pcg64_from_seed({0u}, {});
+  return upload_rng();
+}
+
+}  // namespace
+
+std::unique_ptr<EnvBackend> make_grid_backend(const gp_grid_config* cfg, int64_t B, int device, int rng_mode,
+                                              int* err) {
+  auto g = std::make_unique<GridBackend>();
+  g->B = B;
+  g->device = device;
+  g->rng_mode = rng_mode;
+  *err = g->build(cfg);
+  if (*err) return nullptr;
+  return g;
+}

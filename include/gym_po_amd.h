@@ -1,0 +1,212 @@
+/*
+ * gym_po_amd — C ABI of the MI355X-native vectorised env engine for gym_po's POMDP gridworlds.
+ *
+ * This is the drop-in boundary: a plain C shared library (libgympo_amd.so; no torch types,
+ * plain pointers and sizes). Every device pointer below is a HIP device pointer owned by the
+ * CALLER (e.g. a torch-ROCm tensor's data_ptr()); env state and lookup tables are owned by the
+ * handle. All calls are asynchronous on the given hipStream_t (passed as void*; NULL = the
+ * default stream) unless documented otherwise. A handle is not re-entrant; use one per
+ * stream/thread. Every entry point returns 0 on success, a negative GP_E* code otherwise, and
+ * gp_last_error() returns thread-local text for the last failure.
+ *
+ * Reference interfaces replaced (paths relative to DavidSlayback/gym-po-taxi):
+ *   gp_create(GP_KIND_GRID)   MultistoryFourRoomsEnv.__init__   gym_po/envs/rooms/msrooms.py:266-367
+ *                             RoomsEnv.__init__                  gym_po/envs/rooms/rooms.py:84-175
+ *   gp_create(GP_KIND_TAXI)   TaxiVecEnv.__init__                gym_po/envs/extended_taxi.py:158-230
+ *   gp_create(GP_KIND_CROOMS) CRoomsEnv.__init__                 gym_po/envs/rooms/crooms.py:104-244
+ *   gp_create(GP_KIND_ANTTAG) AntTagEnv task rules (grid restatement, build-defined)
+ *                                                                gym_po/envs/ant_tag.py:88-157
+ *   gp_seed / gp_seed_words   gymnasium Env.reset(seed=) -> seeding.np_random(seed)
+ *                             (msrooms.py:376, rooms.py:184, extended_taxi.py:239, crooms.py:246-249)
+ *   gp_reset                  *.reset()      msrooms.py:369-381, rooms.py:177-189,
+ *                                            extended_taxi.py:232-242, crooms.py:251-266
+ *   gp_step                   *.step()       msrooms.py:390-413, rooms.py:198-222,
+ *                                            extended_taxi.py:244-287, crooms.py:276-298
+ *   gp_rollout                K x step() in one call (agent rollout loop, tester.py:24-26)
+ *   gp_get_state/gp_set_state the env's array state (agent_zyx/goal_zyx/elapsed, s/elapsed/...)
+ *   gp_set_replay             replaces env.np_random's draws with pre-decided per-env values
+ */
+#ifndef GYM_PO_AMD_H
+#define GYM_PO_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GP_ABI_VERSION 1
+
+/* ---- status codes ---- */
+#define GP_OK 0
+#define GP_E_INVALID (-1)   /* bad argument / config (reference would raise)           */
+#define GP_E_HIP (-2)       /* HIP runtime error                                         */
+#define GP_E_UNSUPPORTED (-3)/* mode not available for this env kind                     */
+#define GP_E_STATE (-4)     /* call order (e.g. step before reset)                       */
+
+/* ---- env kinds ---- */
+#define GP_KIND_GRID 1   /* FourRooms (multistory) and ROOMS: discrete cell gridworlds */
+#define GP_KIND_TAXI 2
+#define GP_KIND_CROOMS 3
+#define GP_KIND_ANTTAG 4
+
+/* ---- RNG modes ---- */
+#define GP_RNG_NUMPY 0   /* seed-identical to numpy Generator(PCG64(SeedSequence(seed))) (GRID only) */
+#define GP_RNG_PHILOX 1  /* counter-based Philox4x32-10 keyed by (seed, env, step): fusable rollouts */
+#define GP_RNG_REPLAY 2  /* pre-decided per-env draws supplied by gp_set_replay each step       */
+
+/* ---- observation dtypes reported by gp_obs_info ---- */
+#define GP_DTYPE_I32 0
+#define GP_DTYPE_U8 1
+#define GP_DTYPE_F32 2
+
+/* ---- GRID config (FourRooms / ROOMS) ---- */
+#define GP_FLAVOR_ROOMS 0      /* rooms.py: wall == -1, binary Hansen (observations.py:44-71)       */
+#define GP_FLAVOR_MULTISTORY 1 /* msrooms.py: wall == 0, stairs 2/3, ternary Hansen (msrooms.py:162) */
+
+#define GP_OBS_HANSEN 0     /* scalar Hansen index x goal multiplier            int32 [B]       */
+#define GP_OBS_HANSEN_VEC 1 /* per-direction codes                              uint8 [B,n]     */
+#define GP_OBS_TABLE 2      /* table[agent] + table2[goal] (mdp / room scalars)  int32 [B]       */
+#define GP_OBS_COORDS 3     /* agent (and goal) coordinates                     int32 [B,d|2d]  */
+#define GP_OBS_WINDOW 4     /* n x n local window (observations.py:74-103)      uint8 [B,n,n]   */
+#define GP_OBS_ONEHOT 5     /* one-hot of the scalar obs (taxi)                 uint8 [B,space] */
+#define GP_OBS_F32 6        /* float observation (crooms coords)                float [B,d]     */
+
+typedef struct gp_grid_config {
+  int32_t flavor;          /* GP_FLAVOR_*                                                       */
+  int32_t depth, height, width; /* grid shape (depth = floors; 1 for ROOMS)                     */
+  const int32_t* cells;    /* [depth*height*width] C-order cell values (room id / walk code)    */
+  int32_t n_actions;       /* 4 (cardinal N,E,S,W) or 8 (ordinal N,NE,...,NW) (action_utils.py)  */
+  double action_failure_probability;
+  int32_t obs_kind;        /* GP_OBS_HANSEN / _HANSEN_VEC / _TABLE / _COORDS / _WINDOW          */
+  int32_t obs_dirs;        /* Hansen directions: 4 or 8                                         */
+  int32_t obs_goal;        /* include goal information (obs_type contains "goal")               */
+  int32_t obs_n;           /* window size for GP_OBS_WINDOW                                     */
+  const int32_t* obs_table;  /* GP_OBS_TABLE: per-cell value for the agent    [ncells]          */
+  const int32_t* obs_table2; /* GP_OBS_TABLE: per-cell value for the goal (may be NULL) [ncells] */
+  int32_t fixed_goal;      /* flat cell index, or -1 = random over valid goal cells; a value
+                              >= ncells is an unreachable goal (ROOMS "32" ENDS quirk)          */
+  int32_t fixed_agent;     /* flat cell index, or -1 = random over valid agent cells            */
+  int32_t time_limit;      /* truncated = elapsed > time_limit                                  */
+  float step_reward, wall_reward, goal_reward;
+} gp_grid_config;
+
+typedef struct gp_taxi_config {
+  int32_t rows, cols;      /* navigable grid (5x5 TAXI_MAP, 8x8 EXTENDED_TAXI_MAP)              */
+  int32_t desc_rows, desc_cols;
+  const char* desc;        /* [desc_rows*desc_cols] bordered char map ('|' walls, ':' pseudo)   */
+  int32_t pseudo_walls;    /* 1 if the map uses ':' columns (cc(r,c) = (r+1, 2c+1))            */
+  int32_t n_locs;
+  const int32_t* locs;     /* [n_locs*2] (row, col) of R,G,Y,B in row-major order               */
+  int32_t num_passengers;
+  int32_t time_limit;
+  int32_t obs_kind;        /* GP_OBS_TABLE (raw state), GP_OBS_HANSEN (hansen index) or
+                              GP_OBS_ONEHOT (one-hot of the hansen index, uint8 [B,320])         */
+  float reward_goal, reward_bad, reward_any;
+} gp_taxi_config;
+
+typedef struct gp_crooms_config {
+  int32_t height, width;
+  const int32_t* cells;    /* room-id grid, wall == -1                                          */
+  int32_t use_velocity;
+  float cell_size;
+  int32_t action_kind;     /* 0 = continuous (y,x); 4 / 8 = discrete cardinal / ordinal        */
+  double action_failure_probability;
+  float action_std, action_power;
+  int32_t obs_kind;        /* GP_OBS_F32 (vector mdp) or the discrete kinds on the cell        */
+  int32_t obs_dirs, obs_goal, obs_n;
+  const int32_t* obs_table;
+  const int32_t* obs_table2;
+  int32_t fixed_goal;      /* flat cell or -1                                                   */
+  int32_t fixed_agent;     /* flat cell or -1                                                   */
+  int32_t time_limit;
+  float step_reward, wall_reward, goal_reward, goal_threshold;
+} gp_crooms_config;
+
+typedef struct gp_anttag_config {
+  int32_t size;            /* arena cells per side (interior)                                   */
+  int32_t tag_radius2;     /* squared Chebyshev/Euclid radius (cells^2) for a tag              */
+  int32_t visible_radius2; /* squared radius under which the target is observed                */
+  int32_t min_start_dist2; /* squared minimum start separation                                 */
+  int32_t time_limit;
+  float tag_reward, step_reward;
+} gp_anttag_config;
+
+typedef struct gp_env gp_env;
+
+const char* gp_last_error(void);
+int gp_abi_version(void);
+
+/* kind = GP_KIND_*, config points to the matching gp_*_config. Tables are built and uploaded
+ * to `device` synchronously. rng_mode = GP_RNG_*. */
+int gp_create(int kind, const void* config, int64_t num_envs, int device, int rng_mode, gp_env** out);
+void gp_destroy(gp_env* env);
+
+/* obs layout: dtype = GP_DTYPE_*, width = elements per env (1 for scalar obs). */
+int gp_obs_info(const gp_env* env, int* dtype, int* width);
+int64_t gp_num_envs(const gp_env* env);
+
+/* numpy-compatible seeding: SeedSequence(entropy, spawn_key) -> PCG64 (and the Philox key).
+ * entropy = little-endian uint32 words of a non-negative integer (numpy's convention). */
+int gp_seed_words(gp_env* env, const uint32_t* entropy, int n_entropy, const uint32_t* spawn_key, int n_spawn);
+int gp_seed(gp_env* env, uint64_t seed);
+/* raw PCG64 state: {state_hi, state_lo, inc_hi, inc_lo, has_uint32, uinteger}. get syncs. */
+int gp_set_rng_state(gp_env* env, const uint64_t st[6]);
+int gp_get_rng_state(gp_env* env, uint64_t st[6]);
+
+/* Reset every env (reset()), writing the initial observation to `obs` (device). */
+int gp_reset(gp_env* env, void* obs, void* stream);
+
+/* One batched step with same-step autoreset. actions: int32 [B] (discrete) or float [B,2]
+ * (continuous C-ROOMS); obs as gp_obs_info; rew float [B]; term/trunc uint8 [B]. */
+int gp_step(gp_env* env, const void* actions, void* obs, float* rew, uint8_t* term, uint8_t* trunc,
+            void* stream);
+
+/* K consecutive steps. actions [K,B(,2)], outputs [K,B,...]. Philox mode fuses the K steps in
+ * one launch with the state in registers; numpy/replay modes issue K step launches. */
+int gp_rollout(gp_env* env, int K, const void* actions, void* obs, float* rew, uint8_t* term, uint8_t* trunc,
+               void* stream);
+
+/* Canonical state (device pointers, int32 unless noted). GRID: agent cell, goal cell, elapsed
+ * [B] each. TAXI: s, elapsed, n_dropoffs. CROOMS: agent yx f32[B,2], goal yx f32[B,2],
+ * velocity f32[B,2], elapsed i32[B]. ANTTAG: agent cell, target cell, elapsed. */
+int gp_get_state(gp_env* env, void* a, void* b, void* c, void* d, void* stream);
+int gp_set_state(gp_env* env, const void* a, const void* b, const void* c, const void* d, void* stream);
+
+/* Replay mode: device pointers holding this step's pre-decided per-env draws (read by the next
+ * gp_step). GRID: uniform k53 uint64 [B] (u = k*2^-53), goal index int32 [B], agent index
+ * int32 [B] (indices into the valid-cell lists). TAXI: reset state int32 [B], passenger/dest
+ * pair int32 [B] (p*n_locs+d). CROOMS: action noise f32 [B,2], wall noise f32 [B,2],
+ * goal/agent index int32 [B] each (+ uniform k53 for discrete actions in `u`). */
+int gp_set_replay(gp_env* env, const void* u, const void* i0, const void* i1, const void* f0, const void* f1);
+
+/* Valid-cell lists (host copies) used by the index draws: which = 0 goal, 1 agent. */
+int gp_valid_cells(const gp_env* env, int which, int32_t* out, int cap);
+
+/* On-device episode statistics since the last gp_reset (syncs): {episodes, return_sum,
+ * length_sum, env_steps}. */
+int gp_metrics(gp_env* env, double out[4]);
+
+/* Device-side start-state law of TAXI resets (host copy): P(state index k) over valid states. */
+int gp_taxi_reset_distribution(const gp_env* env, double* out, int cap);
+
+/* Kernel timing: when enabled, hipEvents bracket every launch of the env's step kernel on its
+ * stream; gp_profile_read syncs and returns the summed kernel time (ms) and launch count since
+ * the last read (then clears). Used by bench.py for the live roofline measurement. */
+int gp_set_profiling(gp_env* env, int enable);
+int gp_profile_read(gp_env* env, double* total_ms, int64_t* n_launches);
+
+/* ---- host-only helpers (no device needed) ---- */
+/* PCG64 state {state_hi, state_lo, inc_hi, inc_lo, has_uint32, uinteger} that numpy's
+ * Generator(PCG64(SeedSequence(entropy, spawn_key))) starts from. */
+int gp_pcg64_seed_state(const uint32_t* entropy, int n_entropy, const uint32_t* spawn_key, int n_spawn,
+                        uint64_t out[6]);
+/* P(argmax = k), k < m, for Multinomial(n, uniform over m) counts, ties to the first index:
+ * the law of TaxiVecEnv._reset_mask (extended_taxi.py:344-352). Returns m. */
+int gp_argmax_multinomial_distribution(int m, int n, double* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GYM_PO_AMD_H */
