@@ -36,19 +36,18 @@ constexpr uint32_t SPIN_LIMIT = 1u << 24;
 struct alignas(16) GridCtl {
   uint64_t s_hi, s_lo, inc_hi, inc_lo;  // PCG64 state at step start, increment
   uint32_t has_u32, uinteger;           // numpy's buffered 32-bit half
-  uint32_t ticket[2];                   // dynamic block tickets of the two lookback passes
   uint32_t b_total, w_after1;           // resets this step / absolute word index after call 1
-  uint32_t pad[2];
 };
 
 struct alignas(64) GridCtlBlock {
   GridCtl rec[2];
   uint32_t parity;     // which rec is current
   uint32_t err;        // bit0: lookback spin timeout
-  uint64_t step;       // philox global step counter
-  uint32_t done;       // philox done counter
-  uint32_t pad;
-  double return_sum;   // metrics
+};
+
+// Per-block metric accumulators (each persistent block owns one slot: no atomics).
+struct alignas(32) MetricSlot {
+  double return_sum;
   unsigned long long episodes, length_sum, env_steps;
 };
 
@@ -75,6 +74,9 @@ struct GridDev {
   const int16_t* coords;
   const uint8_t* window;
   const PcgJump* jt;
+  const PcgJump* lt4;   // [256] jump by 4t  (per-thread action-draw offset inside a tile)
+  const PcgJump* lt2;   // [256] jump by 2t  (per-thread word-check offset inside a tile)
+  MetricSlot* mslot;
   uint32_t* ae;
   uint16_t* goal;
   GridCtlBlock* ctl;
@@ -269,9 +271,13 @@ __device__ __forceinline__ void words4(const GridDev& p, const Stream& st, uint3
 struct ScanShared {
   uint32_t wsum[TPB / 64];
   uint32_t wrej[TPB / 64];
+  uint32_t red_min[TPB / 64];
+  uint32_t red_sum[TPB / 64];
+  uint32_t red_rej[TPB / 64];
   uint32_t excl, exrej, total, blkrej;
-  uint32_t ticket;
-  uint32_t pos[EPB];  // slow path: absolute word positions of this block's accepted draws
+  uint32_t bcast;
+  u128 base_a, base_w;  // tile base PCG states (action draws / word checks)
+  uint32_t pos[EPB];    // slow path: absolute word positions of this tile's accepted draws
 };
 
 __device__ __forceinline__ uint64_t ld_status(const uint64_t* p) {
@@ -281,9 +287,12 @@ __device__ __forceinline__ void st_status(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Exclusive block prefix of c (reset count per thread) and OR of r (rejection seen); then the
-// decoupled lookback over predecessor blocks (ticket order). Leaves results in sh.
-__device__ void scan_and_lookback(const GridDev& p, uint64_t* __restrict__ status, int blk, uint32_t c, uint32_t r,
+// Exclusive block prefix of c (reset count per thread) and OR of r (rejection seen) over the
+// tile, then a decoupled lookback over the predecessor tiles with a 256-wide window: every
+// thread polls one predecessor status, the nearest inclusive prefix ends the walk. Tiles are
+// visited in increasing order by the persistent blocks, so every awaited tile is owned by a
+// resident block that waits only on smaller tiles (deadlock-free). Results land in sh.
+__device__ void scan_and_lookback(const GridDev& p, uint64_t* __restrict__ status, int tile, uint32_t c, uint32_t r,
                                   uint32_t& excl_thread, ScanShared& sh) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   uint32_t x = c;
@@ -306,53 +315,65 @@ __device__ void scan_and_lookback(const GridDev& p, uint64_t* __restrict__ statu
     brej |= sh.wrej[w];
   }
   excl_thread = x - c + woff;
-  if (wid == 0) {
-    uint32_t excl = 0, exrej = 0;
-    if (blk == 0) {
-      if (lane == 0) st_status(&status[0], st_pack(ST_FLAG_P, brej, tot));
-    } else {
-      if (lane == 0) st_status(&status[blk], st_pack(ST_FLAG_A, brej, tot));
-      int base = blk - 1;
-      while (true) {
-        const int idx = base - lane;
-        uint64_t s = idx >= 0 ? ld_status(&status[idx]) : st_pack(ST_FLAG_P, 0, 0);
-        uint32_t spins = 0;
-        while (__any(st_flag(s) == ST_FLAG_X)) {
-          if (st_flag(s) == ST_FLAG_X) s = ld_status(&status[idx]);
-          if (++spins > SPIN_LIMIT) {
-            if (lane == 0) atomicOr(&p.ctl->err, 1u);
-            s = st_pack(ST_FLAG_P, 0, 0);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
+  if (tid == 0) st_status(&status[tile], st_pack(tile == 0 ? ST_FLAG_P : ST_FLAG_A, brej, tot));
+  uint32_t excl = 0, exrej = 0;
+  int base = tile - 1;
+  while (base >= 0) {  // block-uniform
+    const int idx = base - tid;
+    uint64_t s = st_pack(ST_FLAG_P, 0, 0);
+    if (idx >= 0) {
+      s = ld_status(&status[idx]);
+      uint32_t spins = 0;
+      while (st_flag(s) == ST_FLAG_X) {
+        __builtin_amdgcn_s_sleep(1);
+        s = ld_status(&status[idx]);
+        if (++spins > SPIN_LIMIT) {
+          atomicOr(&p.ctl->err, 1u);
+          s = st_pack(ST_FLAG_P, 0, 0);
+          break;
         }
-        const unsigned long long pm = __ballot(st_flag(s) == ST_FLAG_P);
-        const int first = pm ? __builtin_ctzll(pm) : 64;
-        uint32_t v = lane <= first ? st_count(s) : 0u;
-        uint32_t rj = lane <= first ? st_rej(s) : 0u;
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) {
-          v += __shfl_xor(v, d, 64);
-          rj |= __shfl_xor(rj, d, 64);
-        }
-        excl += v;
-        exrej |= rj;
-        if (pm) break;
-        base -= 64;
       }
-      if (lane == 0) st_status(&status[blk], st_pack(ST_FLAG_P, exrej | brej, excl + tot));
+    }
+    // nearest inclusive prefix = smallest tid holding a P
+    const unsigned long long pm = __ballot(st_flag(s) == ST_FLAG_P);
+    const uint32_t wmin = pm ? (uint32_t)(wid * 64 + __builtin_ctzll(pm)) : 0xFFFFu;
+    if (lane == 0) sh.red_min[wid] = wmin;
+    __syncthreads();
+    uint32_t first = 0xFFFFu;
+#pragma unroll
+    for (int w = 0; w < TPB / 64; ++w) first = min(first, sh.red_min[w]);
+    uint32_t v = (uint32_t)tid <= first ? st_count(s) : 0u;
+    uint32_t rj = (uint32_t)tid <= first ? st_rej(s) : 0u;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+      v += __shfl_xor(v, d, 64);
+      rj |= __shfl_xor(rj, d, 64);
     }
     if (lane == 0) {
-      sh.excl = excl;
-      sh.exrej = exrej;
-      sh.total = tot;
-      sh.blkrej = brej;
+      sh.red_sum[wid] = v;
+      sh.red_rej[wid] = rj;
     }
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < TPB / 64; ++w) {
+      excl += sh.red_sum[w];
+      exrej |= sh.red_rej[w];
+    }
+    __syncthreads();  // red_* reused next iteration
+    if (first != 0xFFFFu) break;
+    base -= TPB;
+  }
+  if (tid == 0) {
+    if (tile) st_status(&status[tile], st_pack(ST_FLAG_P, exrej | brej, excl + tot));
+    sh.excl = excl;
+    sh.exrej = exrej;
+    sh.total = tot;
+    sh.blkrej = brej;
   }
   __syncthreads();
 }
 
-// Slow path (a Lemire rejection somewhere before this block's draws): wave 0 walks the word
+// Slow path (a Lemire rejection somewhere before this tile's draws): wave 0 walks the word
 // stream from `wbase`, recording the absolute positions of the accepted draws with rank in
 // [jlo, jhi) into sh.pos. Returns (to wave 0) the position after the last recorded draw.
 __device__ uint32_t scan_accepted(const GridDev& p, const Stream& st, uint32_t wbase, uint32_t n, uint32_t thr,
@@ -372,7 +393,6 @@ __device__ uint32_t scan_accepted(const GridDev& p, const Stream& st, uint32_t w
     acc += (uint32_t)__builtin_popcountll(m);
     pos += 64;
   }
-  // broadcast `after` from the lane that set it
   uint32_t a = after;
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) a = max(a, __shfl_xor(a, d, 64));
@@ -380,21 +400,21 @@ __device__ uint32_t scan_accepted(const GridDev& p, const Stream& st, uint32_t w
 }
 
 // ------------------------------------------------------------------ rng finalisation ----
-// Called by the last (ticket) block of the last pass of a step/reset: publishes the next
-// PCG64 state into the other ctl record, clears the other parity's tickets/status, flips parity.
+// Called by the block that owns the last tile of the last pass of a step/reset: publishes the
+// next PCG64 state into the other ctl record, clears the other parity's status words, flips
+// the parity. Every block read the parity before publishing its first tile, and the last
+// tile's lookback saw every tile, so no block of this launch reads the parity afterwards.
 __device__ void finalize_rng(const GridDev& p, const Stream& st, uint32_t parity, uint32_t wtot) {
   if (threadIdx.x == 0) {
-    uint32_t used, h, u;
+    uint32_t used, h, u = st.u0;
     if (wtot == 0) {
-      used = 0; h = st.h0; u = st.u0;
+      used = 0; h = st.h0;
     } else if (st.h0) {
       used = wtot >> 1;          // ceil((wtot-1)/2)
       h = (wtot - 1) & 1;
-      u = st.u0;
     } else {
       used = (wtot + 1) >> 1;    // ceil(wtot/2)
       h = wtot & 1;
-      u = st.u0;
     }
     u128 s = pcg_jump(p.jt, st.s0, st.U0 + used);
     // numpy keeps the last buffered half in `uinteger` even after it has been consumed
@@ -406,8 +426,6 @@ __device__ void finalize_rng(const GridDev& p, const Stream& st, uint32_t parity
     N->inc_lo = lo64(st.inc);
     N->has_u32 = h;
     N->uinteger = u;
-    N->ticket[0] = 0;
-    N->ticket[1] = 0;
     N->b_total = 0;
     N->w_after1 = 0;
   }
@@ -424,7 +442,7 @@ __device__ __forceinline__ uint32_t read_parity(const GridDev& p) {
   return __hip_atomic_load(&p.ctl->parity, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Per-block metrics (episode count / return / length / env-steps) -> 4 atomics per block.
+// Per-block metrics (episode count / return / length / env-steps) into the block's own slot.
 __device__ void add_metrics(const GridDev& p, float rsum, uint32_t eps, uint32_t lens, uint32_t nsteps) {
   __shared__ float s_r[TPB / 64];
   __shared__ uint32_t s_e[TPB / 64], s_l[TPB / 64], s_n[TPB / 64];
@@ -441,10 +459,11 @@ __device__ void add_metrics(const GridDev& p, float rsum, uint32_t eps, uint32_t
   if (threadIdx.x == 0) {
     float r = 0; uint32_t e = 0, l = 0, n = 0;
     for (int w = 0; w < TPB / 64; ++w) { r += s_r[w]; e += s_e[w]; l += s_l[w]; n += s_n[w]; }
-    if (r != 0.f) atomicAdd(&p.ctl->return_sum, (double)r);
-    if (e) atomicAdd(&p.ctl->episodes, (unsigned long long)e);
-    if (l) atomicAdd(&p.ctl->length_sum, (unsigned long long)l);
-    atomicAdd(&p.ctl->env_steps, (unsigned long long)n);
+    MetricSlot& m = p.mslot[blockIdx.x];
+    m.return_sum += (double)r;
+    m.episodes += e;
+    m.length_sum += l;
+    m.env_steps += n;
   }
 }
 
@@ -490,182 +509,212 @@ __device__ __forceinline__ Trans transition(const GridDev& p, uint32_t ae, int g
 #define PF_OBS_RESET 8    // write obs for the resetting envs (their sampling is complete)
 #define PF_STEP 16        // (choice pass) flags come from term|trunc, else every env resets
 
+// The 4 consecutive words w0..w0+3 of a thread whose tile word base (first word w = tile*EPB)
+// state is sh.base_w = u64 #qb (qb = (tile*EPB - h0) >> 1, possibly #-1) and lane offset 2t.
+__device__ __forceinline__ void words4_tile(const GridDev& p, const Stream& st, const u128& base_w, uint32_t w0,
+                                            uint32_t (&out)[4]) {
+  u128 s = apply_jump(p.lt2[threadIdx.x], base_w);
+  uint32_t k = 0, half;
+  uint64_t x;
+  if (!st.h0) {
+    half = 0;
+    x = pcg_output(s);
+  } else if (w0 == 0) {
+    out[0] = st.u0;
+    k = 1;
+    s = pcg_step(s, st.inc);
+    x = pcg_output(s);
+    half = 0;
+  } else {
+    x = pcg_output(s);
+    half = 1;
+  }
+  for (; k < 4; ++k) {
+    out[k] = half ? (uint32_t)(x >> 32) : (uint32_t)x;
+    if (half) {
+      s = pcg_step(s, st.inc);
+      x = pcg_output(s);
+    }
+    half ^= 1;
+  }
+}
+
 template <int OK>
-__global__ __launch_bounds__(TPB) void grid_step_numpy(GridDev p, const int32_t* __restrict__ act,
-                                                       void* __restrict__ obs, float* __restrict__ rew,
-                                                       uint8_t* __restrict__ term, uint8_t* __restrict__ trunc,
-                                                       int flags) {
+__global__ __launch_bounds__(TPB, 4) void grid_step_numpy(GridDev p, const int32_t* __restrict__ act,
+                                                          void* __restrict__ obs, float* __restrict__ rew,
+                                                          uint8_t* __restrict__ term, uint8_t* __restrict__ trunc,
+                                                          int flags) {
   __shared__ ScanShared sh;
   __shared__ uint64_t s_thr[64];
   const uint32_t parity = read_parity(p);
-  GridCtl* C = &p.ctl->rec[parity];
-  if (threadIdx.x == 0) sh.ticket = atomicAdd(&C->ticket[0], 1u);
+  const GridCtl* C = &p.ctl->rec[parity];
   if (threadIdx.x < p.nact * p.nact) s_thr[threadIdx.x] = p.thr[threadIdx.x];
-  __syncthreads();
-  const int blk = (int)sh.ticket;
   Stream st;
   st.s0 = mk128(C->s_hi, C->s_lo);
   st.inc = mk128(C->inc_hi, C->inc_lo);
   st.h0 = C->has_u32;
   st.u0 = C->uinteger;
   st.U0 = (uint32_t)p.B;
-  const int env0 = blk * EPB + threadIdx.x * EPT;
-
-  int32_t a4[4];
-  uint32_t ae4[4];
-  load4<int32_t>(act, env0, p.B, a4);
-  load4<uint32_t>(p.ae, env0, p.B, ae4);
-  int g4[4];
-  if (p.fixed_goal < 0) {
-    uint16_t gg[4];
-    load4<uint16_t>(p.goal, env0, p.B, gg);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) g4[i] = gg[i];
-  } else {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) g4[i] = p.fixed_goal;
-  }
-
-  // random(B): env e draws the u64 at stream position e+1 (action_utils.py:84)
-  uint64_t k4[4];
-  {
-    u128 s = pcg_jump(p.jt, st.s0, (uint32_t)env0 + 1);
-    k4[0] = pcg_output(s) >> 11;
-#pragma unroll
-    for (int i = 1; i < 4; ++i) {
-      s = pcg_step(s, st.inc);
-      k4[i] = pcg_output(s) >> 11;
-    }
-  }
-  Trans t4[4];
-  uint32_t c = 0;
-  int f4[4];
-  float rsum = 0.f;
-  uint32_t eps = 0, lens = 0, nst = 0;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    t4[i] = transition(p, ae4[i], g4[i], a4[i], k4[i], s_thr);
-    const bool valid = env0 + i < p.B;
-    f4[i] = valid && (t4[i].term | t4[i].trunc);
-    c += f4[i];
-    if (valid) {
-      rsum += t4[i].rew;
-      nst += 1;
-      if (f4[i]) { eps += 1; lens += t4[i].elapsed; }
-    }
-  }
-
-  // choice(valid, b) for the resetting envs, in ascending env order (msrooms.py:383-388)
   const bool fused = flags & PF_FUSED_CALL;
   const bool call_goal = flags & PF_CALL_GOAL;
   const uint32_t n = call_goal ? (uint32_t)p.n_goal_valid : (uint32_t)p.n_agent_valid;
   const uint32_t thr = call_goal ? p.thr_goal : p.thr_agent;
-  uint32_t rj = 0;
-  if (fused) {
-    uint32_t w4[4];
-    words4(p, st, (uint32_t)env0, w4);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) rj |= lemire_rejected(w4[i], n, thr) ? 1u : 0u;
-  }
   uint64_t* status = p.status + (size_t)parity * 2 * p.nblk;
-  uint32_t excl_t;
-  scan_and_lookback(p, status, blk, c, rj, excl_t, sh);
-  const bool slow = fused && sh.total && (sh.exrej | sh.blkrej);
-  if (slow) {
-    if (threadIdx.x < 64) scan_accepted(p, st, 0, n, thr, sh.excl, sh.excl + sh.total, sh);
-    __syncthreads();
-  }
+  float rsum = 0.f;
+  uint32_t eps = 0, lens = 0, nst = 0;
 
-  int agent4[4], goal4[4];
-  uint32_t j = excl_t;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    agent4[i] = t4[i].agent;
-    goal4[i] = t4[i].goal;
-    if (f4[i]) {
-      t4[i].elapsed = 0;
+  for (int tile = blockIdx.x; tile < p.nblk; tile += gridDim.x) {
+    const int env0 = tile * EPB + threadIdx.x * EPT;
+    if (threadIdx.x == 0) {
+      // random(B): env e draws the u64 at stream position e+1 (action_utils.py:84)
+      sh.base_a = pcg_jump(p.jt, st.s0, (uint32_t)(tile * EPB) + 1);
       if (fused) {
-        const uint32_t w = slow ? sh.pos[j] : sh.excl + j;
-        const uint32_t v = lemire_value(word_at(p, st, w), n);
-        if (call_goal) goal4[i] = p.goal_valid[v];
-        else agent4[i] = p.agent_valid[v];
+        const int qb = (tile * EPB - (int)st.h0) >> 1;  // -1 when tile 0 starts on the buffered word
+        sh.base_w = pcg_jump(p.jt, st.s0, (uint32_t)((int)st.U0 + qb + 1));
       }
-      if (p.fixed_agent >= 0) agent4[i] = p.fixed_agent;
-      if (p.fixed_goal >= 0) goal4[i] = p.fixed_goal;
-      ++j;
     }
-  }
-
-  // outputs + state
-  {
-    float r[4];
-    uint8_t tm[4], tr[4];
-    uint32_t nae[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      r[i] = t4[i].rew;
-      tm[i] = t4[i].term;
-      tr[i] = t4[i].trunc;
-      nae[i] = (uint32_t)agent4[i] | ((uint32_t)t4[i].elapsed << 16);
-    }
-    store4<float>(rew, env0, p.B, r);
-    store4<uint8_t>(term, env0, p.B, tm);
-    store4<uint8_t>(trunc, env0, p.B, tr);
-    store4<uint32_t>(p.ae, env0, p.B, nae);
+    int32_t a4[4];
+    uint32_t ae4[4];
+    load4<int32_t>(act, env0, p.B, a4);
+    load4<uint32_t>(p.ae, env0, p.B, ae4);
+    int g4[4];
     if (p.fixed_goal < 0) {
       uint16_t gg[4];
+      load4<uint16_t>(p.goal, env0, p.B, gg);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) gg[i] = (uint16_t)goal4[i];
-      store4<uint16_t>(p.goal, env0, p.B, gg);
-    }
-    if (flags & PF_OBS_RESET) {
-      write_obs4<OK>(p, env0, agent4, goal4, obs);
+      for (int i = 0; i < 4; ++i) g4[i] = gg[i];
     } else {
-      // resetters get their obs from the second pass
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (env0 + i < p.B && !f4[i]) write_obs<OK>(p, env0 + i, agent4[i], goal4[i], obs);
+      for (int i = 0; i < 4; ++i) g4[i] = p.fixed_goal;
     }
-  }
-  add_metrics(p, rsum, eps, lens, nst);
-
-  // last block: bookkeeping for the next pass / next step
-  if (blk == p.nblk - 1) {
-    const uint32_t btot = sh.excl + sh.total;
-    uint32_t wafter = 0;
-    if (fused && btot) {
-      if (sh.exrej | sh.blkrej) {
-        uint32_t a = 0;
-        if (threadIdx.x < 64) a = scan_accepted(p, st, 0, n, thr, btot - 1, btot, sh);
-        if (threadIdx.x == 0) sh.ticket = a;
-        __syncthreads();
-        wafter = sh.ticket;
-      } else {
-        wafter = btot;
+    __syncthreads();
+    uint64_t k4[4];
+    {
+      u128 s = apply_jump(p.lt4[threadIdx.x], sh.base_a);
+      k4[0] = pcg_output(s) >> 11;
+#pragma unroll
+      for (int i = 1; i < 4; ++i) {
+        s = pcg_step(s, st.inc);
+        k4[i] = pcg_output(s) >> 11;
       }
     }
-    if (flags & PF_FINAL) {
-      finalize_rng(p, st, parity, wafter);
-    } else if (threadIdx.x == 0) {
-      C->b_total = btot;
-      C->w_after1 = wafter;
+    Trans t4[4];
+    uint32_t c = 0;
+    int f4[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      t4[i] = transition(p, ae4[i], g4[i], a4[i], k4[i], s_thr);
+      const bool valid = env0 + i < p.B;
+      f4[i] = valid && (t4[i].term | t4[i].trunc);
+      c += f4[i];
+      if (valid) {
+        rsum += t4[i].rew;
+        nst += 1;
+        if (f4[i]) { eps += 1; lens += t4[i].elapsed; }
+      }
     }
+    // choice(valid, b) for the resetting envs, ascending env order (msrooms.py:383-388): the
+    // j-th resetter takes word j unless a Lemire rejection happened at or before it. Every
+    // thread checks the 4 word positions equal to its env indices, so the inclusive lookback
+    // flag covers positions [0, (tile+1)*EPB) >= every word this tile's resetters need.
+    uint32_t rj = 0;
+    if (fused) {
+      uint32_t w4[4];
+      words4_tile(p, st, sh.base_w, (uint32_t)env0, w4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) rj |= lemire_rejected(w4[i], n, thr) ? 1u : 0u;
+    }
+    uint32_t excl_t;
+    scan_and_lookback(p, status, tile, c, rj, excl_t, sh);
+    const bool slow = fused && sh.total && (sh.exrej | sh.blkrej);
+    if (slow) {
+      if (threadIdx.x < 64) scan_accepted(p, st, 0, n, thr, sh.excl, sh.excl + sh.total, sh);
+      __syncthreads();
+    }
+    int agent4[4], goal4[4];
+    uint32_t j = excl_t;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      agent4[i] = t4[i].agent;
+      goal4[i] = t4[i].goal;
+      if (f4[i]) {
+        t4[i].elapsed = 0;
+        if (fused) {
+          const uint32_t w = slow ? sh.pos[j] : sh.excl + j;
+          const uint32_t v = lemire_value(word_at(p, st, w), n);
+          if (call_goal) goal4[i] = p.goal_valid[v];
+          else agent4[i] = p.agent_valid[v];
+        }
+        if (p.fixed_agent >= 0) agent4[i] = p.fixed_agent;
+        if (p.fixed_goal >= 0) goal4[i] = p.fixed_goal;
+        ++j;
+      }
+    }
+    {
+      float r[4];
+      uint8_t tm[4], tr[4];
+      uint32_t nae[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        r[i] = t4[i].rew;
+        tm[i] = t4[i].term;
+        tr[i] = t4[i].trunc;
+        nae[i] = (uint32_t)agent4[i] | ((uint32_t)t4[i].elapsed << 16);
+      }
+      store4<float>(rew, env0, p.B, r);
+      store4<uint8_t>(term, env0, p.B, tm);
+      store4<uint8_t>(trunc, env0, p.B, tr);
+      store4<uint32_t>(p.ae, env0, p.B, nae);
+      if (p.fixed_goal < 0) {
+        uint16_t gg[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) gg[i] = (uint16_t)goal4[i];
+        store4<uint16_t>(p.goal, env0, p.B, gg);
+      }
+      if (flags & PF_OBS_RESET) {
+        write_obs4<OK>(p, env0, agent4, goal4, obs);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (env0 + i < p.B && !f4[i]) write_obs<OK>(p, env0 + i, agent4[i], goal4[i], obs);
+      }
+    }
+    if (tile == p.nblk - 1) {
+      const uint32_t btot = sh.excl + sh.total;
+      uint32_t wafter = 0;
+      if (fused && btot) {
+        if (sh.exrej | sh.blkrej) {
+          uint32_t a = 0;
+          if (threadIdx.x < 64) a = scan_accepted(p, st, 0, n, thr, btot - 1, btot, sh);
+          if (threadIdx.x == 0) sh.bcast = a;
+          __syncthreads();
+          wafter = sh.bcast;
+        } else {
+          wafter = btot;
+        }
+      }
+      if (flags & PF_FINAL) {
+        finalize_rng(p, st, parity, wafter);
+      } else if (threadIdx.x == 0) {
+        p.ctl->rec[parity].b_total = btot;
+        p.ctl->rec[parity].w_after1 = wafter;
+      }
+    }
+    __syncthreads();  // sh reused by the next tile
   }
+  add_metrics(p, rsum, eps, lens, nst);
 }
 
 // A standalone choice() pass: the agent draws after random goals in step(), and every sampling
 // call of reset(). Flags come from term|trunc (PF_STEP) or are all set (reset).
 template <int OK>
-__global__ __launch_bounds__(TPB) void grid_choice_numpy(GridDev p, const uint8_t* __restrict__ term,
-                                                         const uint8_t* __restrict__ trunc, void* __restrict__ obs,
-                                                         int flags, int set, uint32_t wbase_fixed, int use_wafter1,
-                                                         uint32_t U0) {
+__global__ __launch_bounds__(TPB, 4) void grid_choice_numpy(GridDev p, const uint8_t* __restrict__ term,
+                                                            const uint8_t* __restrict__ trunc,
+                                                            void* __restrict__ obs, int flags, int set,
+                                                            uint32_t wbase_fixed, int use_wafter1, uint32_t U0) {
   __shared__ ScanShared sh;
   const uint32_t parity = read_parity(p);
-  GridCtl* C = &p.ctl->rec[parity];
-  if (threadIdx.x == 0) sh.ticket = atomicAdd(&C->ticket[set], 1u);
-  __syncthreads();
-  const int blk = (int)sh.ticket;
+  const GridCtl* C = &p.ctl->rec[parity];
   Stream st;
   st.s0 = mk128(C->s_hi, C->s_lo);
   st.inc = mk128(C->inc_hi, C->inc_lo);
@@ -673,91 +722,94 @@ __global__ __launch_bounds__(TPB) void grid_choice_numpy(GridDev p, const uint8_
   st.u0 = C->uinteger;
   st.U0 = U0;
   const uint32_t wbase = use_wafter1 ? C->w_after1 : wbase_fixed;
-  const int env0 = blk * EPB + threadIdx.x * EPT;
-  int f4[4];
-  if (flags & PF_STEP) {
-    uint8_t tm[4], tr[4];
-    load4<uint8_t>(term, env0, p.B, tm);
-    load4<uint8_t>(trunc, env0, p.B, tr);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) f4[i] = (env0 + i < p.B) && (tm[i] | tr[i]);
-  } else {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) f4[i] = env0 + i < p.B;
-  }
   const bool call_goal = flags & PF_CALL_GOAL;
   const uint32_t n = call_goal ? (uint32_t)p.n_goal_valid : (uint32_t)p.n_agent_valid;
   const uint32_t thr = call_goal ? p.thr_goal : p.thr_agent;
-  uint32_t c = (uint32_t)(f4[0] + f4[1] + f4[2] + f4[3]);
-  uint32_t rj = 0;
-  {
-    uint32_t w4[4];
-    words4(p, st, wbase + (uint32_t)env0, w4);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) rj |= lemire_rejected(w4[i], n, thr) ? 1u : 0u;
-  }
   uint64_t* status = p.status + ((size_t)parity * 2 + set) * p.nblk;
-  uint32_t excl_t;
-  scan_and_lookback(p, status, blk, c, rj, excl_t, sh);
-  const bool slow = sh.total && (sh.exrej | sh.blkrej);
-  if (slow) {
-    if (threadIdx.x < 64) scan_accepted(p, st, wbase, n, thr, sh.excl, sh.excl + sh.total, sh);
-    __syncthreads();
-  }
-  uint32_t ae4[4];
-  load4<uint32_t>(p.ae, env0, p.B, ae4);
-  int agent4[4], goal4[4];
-  uint16_t gg[4] = {0, 0, 0, 0};
-  if (p.fixed_goal < 0) load4<uint16_t>(p.goal, env0, p.B, gg);
-  uint32_t j = excl_t;
+  for (int tile = blockIdx.x; tile < p.nblk; tile += gridDim.x) {
+    const int env0 = tile * EPB + threadIdx.x * EPT;
+    int f4[4];
+    if (flags & PF_STEP) {
+      uint8_t tm[4], tr[4];
+      load4<uint8_t>(term, env0, p.B, tm);
+      load4<uint8_t>(trunc, env0, p.B, tr);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    agent4[i] = (int)(ae4[i] & 0xFFFF);
-    goal4[i] = p.fixed_goal < 0 ? (int)gg[i] : p.fixed_goal;
-    if (f4[i]) {
-      const uint32_t w = slow ? sh.pos[j] : wbase + sh.excl + j;
-      const uint32_t v = lemire_value(word_at(p, st, w), n);
-      if (call_goal) goal4[i] = p.goal_valid[v];
-      else agent4[i] = p.agent_valid[v];
-      ++j;
+      for (int i = 0; i < 4; ++i) f4[i] = (env0 + i < p.B) && (tm[i] | tr[i]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) f4[i] = env0 + i < p.B;
     }
-  }
-  if (call_goal) {
-    if (p.fixed_goal < 0) {
+    uint32_t c = (uint32_t)(f4[0] + f4[1] + f4[2] + f4[3]);
+    uint32_t rj = 0;
+    {
+      uint32_t w4[4];
+      words4(p, st, wbase + (uint32_t)env0, w4);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) gg[i] = (uint16_t)goal4[i];
-      store4<uint16_t>(p.goal, env0, p.B, gg);
+      for (int i = 0; i < 4; ++i) rj |= lemire_rejected(w4[i], n, thr) ? 1u : 0u;
     }
-  } else {
+    uint32_t excl_t;
+    scan_and_lookback(p, status, tile, c, rj, excl_t, sh);
+    const bool slow = sh.total && (sh.exrej | sh.blkrej);
+    if (slow) {
+      if (threadIdx.x < 64) scan_accepted(p, st, wbase, n, thr, sh.excl, sh.excl + sh.total, sh);
+      __syncthreads();
+    }
+    uint32_t ae4[4];
+    load4<uint32_t>(p.ae, env0, p.B, ae4);
+    int agent4[4], goal4[4];
+    uint16_t gg[4] = {0, 0, 0, 0};
+    if (p.fixed_goal < 0) load4<uint16_t>(p.goal, env0, p.B, gg);
+    uint32_t j = excl_t;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) ae4[i] = (ae4[i] & 0xFFFF0000u) | (uint32_t)agent4[i];
-    store4<uint32_t>(p.ae, env0, p.B, ae4);
-  }
-  if (flags & PF_OBS_RESET) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      if (f4[i]) write_obs<OK>(p, env0 + i, agent4[i], goal4[i], obs);
-  }
-  if (blk == p.nblk - 1) {
-    const uint32_t btot = sh.excl + sh.total;
-    uint32_t wafter = wbase;
-    if (btot) {
-      if (sh.exrej | sh.blkrej) {
-        uint32_t a = 0;
-        if (threadIdx.x < 64) a = scan_accepted(p, st, wbase, n, thr, btot - 1, btot, sh);
-        if (threadIdx.x == 0) sh.ticket = a;
-        __syncthreads();
-        wafter = sh.ticket;
-      } else {
-        wafter = wbase + btot;
+    for (int i = 0; i < 4; ++i) {
+      agent4[i] = (int)(ae4[i] & 0xFFFF);
+      goal4[i] = p.fixed_goal < 0 ? (int)gg[i] : p.fixed_goal;
+      if (f4[i]) {
+        const uint32_t w = slow ? sh.pos[j] : wbase + sh.excl + j;
+        const uint32_t v = lemire_value(word_at(p, st, w), n);
+        if (call_goal) goal4[i] = p.goal_valid[v];
+        else agent4[i] = p.agent_valid[v];
+        ++j;
       }
     }
-    if (flags & PF_FINAL) {
-      finalize_rng(p, st, parity, wafter);
-    } else if (threadIdx.x == 0) {
-      C->b_total = btot;
-      C->w_after1 = wafter;
+    if (call_goal) {
+      if (p.fixed_goal < 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) gg[i] = (uint16_t)goal4[i];
+        store4<uint16_t>(p.goal, env0, p.B, gg);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ae4[i] = (ae4[i] & 0xFFFF0000u) | (uint32_t)agent4[i];
+      store4<uint32_t>(p.ae, env0, p.B, ae4);
     }
+    if (flags & PF_OBS_RESET) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (f4[i]) write_obs<OK>(p, env0 + i, agent4[i], goal4[i], obs);
+    }
+    if (tile == p.nblk - 1) {
+      const uint32_t btot = sh.excl + sh.total;
+      uint32_t wafter = wbase;
+      if (btot) {
+        if (sh.exrej | sh.blkrej) {
+          uint32_t a = 0;
+          if (threadIdx.x < 64) a = scan_accepted(p, st, wbase, n, thr, btot - 1, btot, sh);
+          if (threadIdx.x == 0) sh.bcast = a;
+          __syncthreads();
+          wafter = sh.bcast;
+        } else {
+          wafter = wbase + btot;
+        }
+      }
+      if (flags & PF_FINAL) {
+        finalize_rng(p, st, parity, wafter);
+      } else if (threadIdx.x == 0) {
+        p.ctl->rec[parity].b_total = btot;
+        p.ctl->rec[parity].w_after1 = wafter;
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -781,6 +833,7 @@ __global__ __launch_bounds__(TPB) void grid_obs_all(GridDev p, void* __restrict_
 // ------------------------------------------------------------------ kernels: counter modes ----
 // Philox: ctr = (env, step_lo, step_hi, 0x67706f21), key = seed-derived. One draw set per
 // env-step: x0,x1 -> 53-bit uniform; x2 -> goal index; x3 -> agent index (multiply-shift).
+// The global step index is host-tracked and passed by value.
 __device__ __forceinline__ void philox_draws(const GridDev& p, int env, uint64_t step, uint64_t& k53, uint32_t& gi,
                                              uint32_t& ai) {
   Philox4 r = philox4x32_10((uint32_t)env, (uint32_t)step, (uint32_t)(step >> 32), 0x67706f21u, p.key0, p.key1);
@@ -789,11 +842,10 @@ __device__ __forceinline__ void philox_draws(const GridDev& p, int env, uint64_t
   ai = lemire_value(r.x[3], (uint32_t)max(p.n_agent_valid, 1));
 }
 
-// One env-step with explicit draws (counter/replay modes): same transition, reset in place.
 template <int OK>
-__device__ __forceinline__ void counter_env_step(const GridDev& p, const uint64_t* thr, int env, uint32_t& ae,
-                                                 int& goal, int a, uint64_t k53, uint32_t gi, uint32_t ai, float& r,
-                                                 uint8_t& tm, uint8_t& tr, float& rsum, uint32_t& eps, uint32_t& lens) {
+__device__ __forceinline__ void counter_env_step(const GridDev& p, const uint64_t* thr, uint32_t& ae, int& goal, int a,
+                                                 uint64_t k53, uint32_t gi, uint32_t ai, float& r, uint8_t& tm,
+                                                 uint8_t& tr, float& rsum, uint32_t& eps, uint32_t& lens) {
   Trans t = transition(p, ae, goal, a, k53, thr);
   int agent = t.agent, g = goal, el = t.elapsed;
   rsum += t.rew;
@@ -812,13 +864,13 @@ __device__ __forceinline__ void counter_env_step(const GridDev& p, const uint64_
 }
 
 template <int OK, bool REPLAY>
-__global__ __launch_bounds__(TPB) void grid_rollout_counter(GridDev p, int K, const int32_t* __restrict__ act,
-                                                            void* __restrict__ obs, float* __restrict__ rew,
-                                                            uint8_t* __restrict__ term, uint8_t* __restrict__ trunc) {
+__global__ __launch_bounds__(TPB) void grid_rollout_counter(GridDev p, int K, uint64_t step0,
+                                                            const int32_t* __restrict__ act, void* __restrict__ obs,
+                                                            float* __restrict__ rew, uint8_t* __restrict__ term,
+                                                            uint8_t* __restrict__ trunc) {
   __shared__ uint64_t s_thr[64];
   if (threadIdx.x < p.nact * p.nact) s_thr[threadIdx.x] = p.thr[threadIdx.x];
   __syncthreads();
-  const uint64_t step0 = p.ctl->step;
   const int env0 = blockIdx.x * EPB + threadIdx.x * EPT;
   uint32_t ae4[4];
   load4<uint32_t>(p.ae, env0, p.B, ae4);
@@ -855,8 +907,7 @@ __global__ __launch_bounds__(TPB) void grid_rollout_counter(GridDev p, int K, co
           philox_draws(p, env, step0 + k, k53, gi, ai);
         }
       }
-      counter_env_step<OK>(p, s_thr, env < p.B ? env : 0, ae4[i], g4[i], a4[i], k53, gi, ai, r[i], tm[i], tr[i],
-                           rsum, eps, lens);
+      counter_env_step<OK>(p, s_thr, ae4[i], g4[i], a4[i], k53, gi, ai, r[i], tm[i], tr[i], rsum, eps, lens);
       nst += env < p.B;
     }
     store4<float>(rew + off, env0, p.B, r);
@@ -875,42 +926,26 @@ __global__ __launch_bounds__(TPB) void grid_rollout_counter(GridDev p, int K, co
     store4<uint16_t>(p.goal, env0, p.B, gg);
   }
   add_metrics(p, rsum, eps, lens, nst);
-  if (threadIdx.x == 0) {
-    const uint32_t prev = atomicAdd(&p.ctl->done, 1u);
-    if (prev == (uint32_t)gridDim.x - 1) {
-      p.ctl->step = step0 + (uint64_t)K;
-      p.ctl->done = 0;
-    }
-  }
 }
 
 // Philox / replay reset: every env draws goal then agent from its own counter.
 template <int OK, bool REPLAY>
-__global__ __launch_bounds__(TPB) void grid_reset_counter(GridDev p, void* __restrict__ obs) {
+__global__ __launch_bounds__(TPB) void grid_reset_counter(GridDev p, uint64_t step, void* __restrict__ obs) {
   const int env = blockIdx.x * TPB + threadIdx.x;
-  if (env < p.B) {
-    uint64_t k53;
-    uint32_t gi = 0, ai = 0;
-    if constexpr (REPLAY) {
-      gi = p.rp_goal ? (uint32_t)p.rp_goal[env] : 0u;
-      ai = p.rp_agent ? (uint32_t)p.rp_agent[env] : 0u;
-    } else {
-      philox_draws(p, env, p.ctl->step, k53, gi, ai);
-    }
-    const int g = p.fixed_goal >= 0 ? p.fixed_goal : (int)p.goal_valid[gi];
-    const int a = p.fixed_agent >= 0 ? p.fixed_agent : (int)p.agent_valid[ai];
-    p.ae[env] = (uint32_t)a;
-    if (p.fixed_goal < 0) p.goal[env] = (uint16_t)g;
-    write_obs<OK>(p, env, a, g, obs);
+  if (env >= p.B) return;
+  uint64_t k53;
+  uint32_t gi = 0, ai = 0;
+  if constexpr (REPLAY) {
+    gi = p.rp_goal ? (uint32_t)p.rp_goal[env] : 0u;
+    ai = p.rp_agent ? (uint32_t)p.rp_agent[env] : 0u;
+  } else {
+    philox_draws(p, env, step, k53, gi, ai);
   }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t prev = atomicAdd(&p.ctl->done, 1u);
-    if (prev == (uint32_t)gridDim.x - 1) {
-      p.ctl->step = p.ctl->step + 1;
-      p.ctl->done = 0;
-    }
-  }
+  const int g = p.fixed_goal >= 0 ? p.fixed_goal : (int)p.goal_valid[gi];
+  const int a = p.fixed_agent >= 0 ? p.fixed_agent : (int)p.agent_valid[ai];
+  p.ae[env] = (uint32_t)a;
+  if (p.fixed_goal < 0) p.goal[env] = (uint16_t)g;
+  write_obs<OK>(p, env, a, g, obs);
 }
 
 // ------------------------------------------------------------------ state access ----
@@ -937,10 +972,13 @@ struct GridBackend : EnvBackend {
   GridDev d{};
   int flavor = 0;
   int depth = 1, height = 0, width = 0;
+  int grid_persist = 1;        // resident blocks of the persistent numpy-mode kernels
+  int nslots = 1;              // metric slots (max grid size of any kernel writing them)
+  uint64_t philox_step = 0;    // host-tracked global step for the counter-based mode
   std::vector<int32_t> cells;
   std::vector<uint16_t> goal_valid_h, agent_valid_h;
-  DevBuf b_move, b_thr, b_gv, b_av, b_hbase, b_doff, b_hvec, b_t1, b_t2, b_coords, b_window, b_jt, b_ae, b_goal,
-      b_ctl, b_status;
+  DevBuf b_move, b_thr, b_gv, b_av, b_hbase, b_doff, b_hvec, b_t1, b_t2, b_coords, b_window, b_jt, b_lt4, b_lt2,
+      b_ae, b_goal, b_ctl, b_status, b_mslot;
   // replay pointers for the next step
   const uint64_t* rp_u = nullptr;
   const int32_t* rp_goal = nullptr;
@@ -954,6 +992,7 @@ struct GridBackend : EnvBackend {
     philox_key[1] = key[1];
     d.key0 = key[0];
     d.key1 = key[1];
+    philox_step = 0;
     return upload_rng();
   }
   int set_rng_state(const RngHost& r) override {
@@ -1005,12 +1044,16 @@ int GridBackend::upload_rng() {
   c.inc_lo = lo64(rng.inc);
   c.has_u32 = rng.has_u32;
   c.uinteger = rng.uinteger;
-  c.ticket[0] = c.ticket[1] = 0;
-  h.step = 0;
-  h.done = 0;
   GP_HIP_CHECK(hipMemcpy(d.ctl, &h, sizeof(h), hipMemcpyHostToDevice));
   std::vector<PcgJump> jt = build_jump_tables(rng.inc);
   GP_HIP_CHECK(hipMemcpy(b_jt.p, jt.data(), jt.size() * sizeof(PcgJump), hipMemcpyHostToDevice));
+  std::vector<PcgJump> l4(TPB), l2(TPB);
+  for (int t = 0; t < TPB; ++t) {
+    l4[t] = pcg_jump_params((u128)(4 * t), rng.inc);
+    l2[t] = pcg_jump_params((u128)(2 * t), rng.inc);
+  }
+  GP_HIP_CHECK(hipMemcpy(b_lt4.p, l4.data(), l4.size() * sizeof(PcgJump), hipMemcpyHostToDevice));
+  GP_HIP_CHECK(hipMemcpy(b_lt2.p, l2.data(), l2.size() * sizeof(PcgJump), hipMemcpyHostToDevice));
   return GP_OK;
 }
 
@@ -1032,12 +1075,15 @@ int GridBackend::get_rng_state(RngHost* r) {
 
 int GridBackend::metrics(double out[4]) {
   GP_HIP_CHECK(hipDeviceSynchronize());
-  GridCtlBlock h;
-  GP_HIP_CHECK(hipMemcpy(&h, d.ctl, sizeof(h), hipMemcpyDeviceToHost));
-  out[0] = (double)h.episodes;
-  out[1] = h.return_sum;
-  out[2] = (double)h.length_sum;
-  out[3] = (double)h.env_steps;
+  std::vector<MetricSlot> m(nslots);
+  GP_HIP_CHECK(hipMemcpy(m.data(), d.mslot, sizeof(MetricSlot) * nslots, hipMemcpyDeviceToHost));
+  out[0] = out[1] = out[2] = out[3] = 0;
+  for (const MetricSlot& x : m) {
+    out[0] += (double)x.episodes;
+    out[1] += x.return_sum;
+    out[2] += (double)x.length_sum;
+    out[3] += (double)x.env_steps;
+  }
   return GP_OK;
 }
 
@@ -1055,35 +1101,28 @@ static int dispatch_obs(int ok, F&& f) {
 }
 
 int GridBackend::reset(void* obs, hipStream_t s) {
-  // zero metrics
-  {
-    GridCtlBlock h;
-    GP_HIP_CHECK(hipMemcpyAsync(&h, d.ctl, sizeof(h), hipMemcpyDeviceToHost, s));
-    GP_HIP_CHECK(hipStreamSynchronize(s));
-    h.return_sum = 0;
-    h.episodes = h.length_sum = h.env_steps = 0;
-    GP_HIP_CHECK(hipMemcpyAsync(d.ctl, &h, sizeof(h), hipMemcpyHostToDevice, s));
-    GP_HIP_CHECK(hipStreamSynchronize(s));
-  }
+  GP_HIP_CHECK(hipMemsetAsync(d.mslot, 0, sizeof(MetricSlot) * nslots, s));
   const unsigned g1 = (unsigned)((B + TPB - 1) / TPB);
   const bool rgoal = d.fixed_goal < 0, ragent = d.fixed_agent < 0;
+  const unsigned gp = (unsigned)grid_persist;
   int e = dispatch_obs(d.obs_kind, [&](auto okc) -> int {
     constexpr int OK = decltype(okc)::value;
     if (rng_mode == GP_RNG_NUMPY) {
       hipLaunchKernelGGL(grid_reset_init, dim3(g1), dim3(TPB), 0, s, d);
       if (rgoal) {
         int fl = PF_CALL_GOAL | (ragent ? 0 : (PF_FINAL | PF_OBS_RESET));
-        hipLaunchKernelGGL(grid_choice_numpy<OK>, dim3(d.nblk), dim3(TPB), 0, s, d, (const uint8_t*)nullptr,
+        hipLaunchKernelGGL(grid_choice_numpy<OK>, dim3(gp), dim3(TPB), 0, s, d, (const uint8_t*)nullptr,
                            (const uint8_t*)nullptr, obs, fl, 0, 0u, 0, 0u);
       }
       if (ragent) {
         int fl = PF_FINAL | PF_OBS_RESET;
-        hipLaunchKernelGGL(grid_choice_numpy<OK>, dim3(d.nblk), dim3(TPB), 0, s, d, (const uint8_t*)nullptr,
+        hipLaunchKernelGGL(grid_choice_numpy<OK>, dim3(gp), dim3(TPB), 0, s, d, (const uint8_t*)nullptr,
                            (const uint8_t*)nullptr, obs, fl, rgoal ? 1 : 0, 0u, rgoal ? 1 : 0, 0u);
       }
       if (!rgoal && !ragent) hipLaunchKernelGGL(grid_obs_all<OK>, dim3(g1), dim3(TPB), 0, s, d, obs);
     } else if (rng_mode == GP_RNG_PHILOX) {
-      hipLaunchKernelGGL((grid_reset_counter<OK, false>), dim3(g1), dim3(TPB), 0, s, d, obs);
+      hipLaunchKernelGGL((grid_reset_counter<OK, false>), dim3(g1), dim3(TPB), 0, s, d, philox_step, obs);
+      ++philox_step;
     } else {
       GridDev dd = d;
       dd.rp_u = rp_u; dd.rp_goal = rp_goal; dd.rp_agent = rp_agent;
@@ -1091,7 +1130,7 @@ int GridBackend::reset(void* obs, hipStream_t s) {
         gp_set_error("replay reset needs goal/agent index draws (gp_set_replay)");
         return GP_E_STATE;
       }
-      hipLaunchKernelGGL((grid_reset_counter<OK, true>), dim3(g1), dim3(TPB), 0, s, dd, obs);
+      hipLaunchKernelGGL((grid_reset_counter<OK, true>), dim3(g1), dim3(TPB), 0, s, dd, (uint64_t)0, obs);
     }
     return GP_OK;
   });
@@ -1107,28 +1146,32 @@ int GridBackend::step(const void* act, void* obs, float* rew, uint8_t* term, uin
     return GP_E_STATE;
   }
   const bool rgoal = d.fixed_goal < 0, ragent = d.fixed_agent < 0;
+  const unsigned gp = (unsigned)grid_persist;
   int e = dispatch_obs(d.obs_kind, [&](auto okc) -> int {
     constexpr int OK = decltype(okc)::value;
     if (rng_mode == GP_RNG_NUMPY) {
       if (rgoal && ragent) {
-        hipLaunchKernelGGL(grid_step_numpy<OK>, dim3(d.nblk), dim3(TPB), 0, s, d, (const int32_t*)act, obs, rew,
-                           term, trunc, PF_FUSED_CALL | PF_CALL_GOAL);
-        hipLaunchKernelGGL(grid_choice_numpy<OK>, dim3(d.nblk), dim3(TPB), 0, s, d, term, trunc, obs,
+        timer.begin(s);
+        hipLaunchKernelGGL(grid_step_numpy<OK>, dim3(gp), dim3(TPB), 0, s, d, (const int32_t*)act, obs, rew, term,
+                           trunc, PF_FUSED_CALL | PF_CALL_GOAL);
+        timer.end(s);
+        hipLaunchKernelGGL(grid_choice_numpy<OK>, dim3(gp), dim3(TPB), 0, s, d, term, trunc, obs,
                            PF_STEP | PF_FINAL | PF_OBS_RESET, 1, 0u, 1, (uint32_t)B);
       } else {
         int fl = PF_FINAL | PF_OBS_RESET;
         if (rgoal) fl |= PF_FUSED_CALL | PF_CALL_GOAL;
         if (ragent) fl |= PF_FUSED_CALL;
         timer.begin(s);
-        hipLaunchKernelGGL(grid_step_numpy<OK>, dim3(d.nblk), dim3(TPB), 0, s, d, (const int32_t*)act, obs, rew,
-                           term, trunc, fl);
+        hipLaunchKernelGGL(grid_step_numpy<OK>, dim3(gp), dim3(TPB), 0, s, d, (const int32_t*)act, obs, rew, term,
+                           trunc, fl);
         timer.end(s);
       }
     } else if (rng_mode == GP_RNG_PHILOX) {
       timer.begin(s);
-      hipLaunchKernelGGL((grid_rollout_counter<OK, false>), dim3(d.nblk), dim3(TPB), 0, s, d, 1,
+      hipLaunchKernelGGL((grid_rollout_counter<OK, false>), dim3(d.nblk), dim3(TPB), 0, s, d, 1, philox_step,
                          (const int32_t*)act, obs, rew, term, trunc);
       timer.end(s);
+      ++philox_step;
     } else {
       if (!rp_u || (rgoal && !rp_goal) || (ragent && !rp_agent)) {
         gp_set_error("replay step needs draws (gp_set_replay)");
@@ -1136,7 +1179,7 @@ int GridBackend::step(const void* act, void* obs, float* rew, uint8_t* term, uin
       }
       GridDev dd = d;
       dd.rp_u = rp_u; dd.rp_goal = rp_goal; dd.rp_agent = rp_agent;
-      hipLaunchKernelGGL((grid_rollout_counter<OK, true>), dim3(d.nblk), dim3(TPB), 0, s, dd, 1,
+      hipLaunchKernelGGL((grid_rollout_counter<OK, true>), dim3(d.nblk), dim3(TPB), 0, s, dd, 1, (uint64_t)0,
                          (const int32_t*)act, obs, rew, term, trunc);
     }
     return GP_OK;
@@ -1156,12 +1199,13 @@ int GridBackend::rollout(int K, const void* act, void* obs, float* rew, uint8_t*
   int e = dispatch_obs(d.obs_kind, [&](auto okc) -> int {
     constexpr int OK = decltype(okc)::value;
     timer.begin(s);
-    hipLaunchKernelGGL((grid_rollout_counter<OK, false>), dim3(d.nblk), dim3(TPB), 0, s, d, K, (const int32_t*)act,
-                       obs, rew, term, trunc);
+    hipLaunchKernelGGL((grid_rollout_counter<OK, false>), dim3(d.nblk), dim3(TPB), 0, s, d, K, philox_step,
+                       (const int32_t*)act, obs, rew, term, trunc);
     timer.end(s);
     return GP_OK;
   });
   if (e) return e;
+  philox_step += (uint64_t)K;
   GP_HIP_CHECK(hipGetLastError());
   return GP_OK;
 }
@@ -1380,9 +1424,26 @@ int GridBackend::build(const gp_grid_config* cfg) {
       (e = b_hvec.upload(hvec)) || (e = b_coords.upload(coords)) || (e = b_window.upload(window)) ||
       (e = b_t1.upload(t1)) || (e = b_t2.upload(t2)))
     return e;
-  if ((e = b_jt.alloc(sizeof(PcgJump) * JT_LEVELS * JT_RADIX)) || (e = b_ae.alloc(sizeof(uint32_t) * (B + 4))) ||
+  // persistent grid for the lookback kernels: every block must be resident (see scan_and_lookback)
+  {
+    int occ = 0;
+    GP_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, grid_step_numpy<GP_OBS_HANSEN>, TPB, 0));
+    int occ2 = 0;
+    GP_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ2, grid_choice_numpy<GP_OBS_WINDOW>, TPB, 0));
+    occ = std::min(occ, occ2);
+    hipDeviceProp_t prop;
+    GP_HIP_CHECK(hipGetDeviceProperties(&prop, device));
+    // VGPR-limited (114-120 VGPRs -> 4 waves/SIMD); the SGPR bound (106 -> 6 blocks/CU) is looser,
+    // so the API's answer is exact here (MI355X_MICROARCH.md, Residency). Capped at 4 blocks/CU.
+    const int bpc = std::max(1, std::min(4, occ));
+    grid_persist = std::max(1, std::min(d.nblk, prop.multiProcessorCount * bpc));
+  }
+  nslots = std::max(d.nblk, grid_persist);
+  if ((e = b_jt.alloc(sizeof(PcgJump) * JT_LEVELS * JT_RADIX)) || (e = b_lt4.alloc(sizeof(PcgJump) * TPB)) ||
+      (e = b_lt2.alloc(sizeof(PcgJump) * TPB)) || (e = b_ae.alloc(sizeof(uint32_t) * (B + 4))) ||
       (e = b_goal.alloc(sizeof(uint16_t) * (B + 8))) || (e = b_ctl.alloc(sizeof(GridCtlBlock))) ||
-      (e = b_status.alloc(sizeof(uint64_t) * 4 * (size_t)d.nblk)))
+      (e = b_status.alloc(sizeof(uint64_t) * 4 * (size_t)d.nblk)) ||
+      (e = b_mslot.alloc(sizeof(MetricSlot) * (size_t)nslots)))
     return e;
   d.move = b_move.as<uint16_t>();
   d.thr = b_thr.as<uint64_t>();
@@ -1396,6 +1457,9 @@ int GridBackend::build(const gp_grid_config* cfg) {
   d.coords = b_coords.as<int16_t>();
   d.window = b_window.as<uint8_t>();
   d.jt = b_jt.as<PcgJump>();
+  d.lt4 = b_lt4.as<PcgJump>();
+  d.lt2 = b_lt2.as<PcgJump>();
+  d.mslot = b_mslot.as<MetricSlot>();
   d.ae = b_ae.as<uint32_t>();
   d.goal = b_goal.as<uint16_t>();
   d.ctl = b_ctl.as<GridCtlBlock>();

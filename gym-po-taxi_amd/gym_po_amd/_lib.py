@@ -96,6 +96,21 @@ class GymPoError(RuntimeError):
     pass
 
 
+def _bind_torch_hip_runtime():
+    """Make libgympo_amd.so bind to the SAME HIP runtime torch uses (torch wheels bundle their
+    own libamdhip64.so.7). Device pointers and hipStream_t handles from torch are only valid in
+    that runtime, so it is loaded (RTLD_GLOBAL, same soname) before our library."""
+    try:
+        import torch
+    except Exception:  # noqa: BLE001 - pure-C users without torch use the system runtime
+        return
+    tl = os.path.join(os.path.dirname(torch.__file__), "lib")
+    for name in ("libhsa-runtime64.so", "libamdhip64.so"):
+        p = os.path.join(tl, name)
+        if os.path.exists(p):
+            ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
+
+
 def lib():
     """Load (once) and return the shared library. Raises if it is missing — no fallback."""
     global _lib
@@ -103,6 +118,7 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise GymPoError(f"{LIB_PATH} not found: build it with `python gym-po-taxi_amd/build.py` "
                              "(gym_po_amd has no CPU fallback)")
+        _bind_torch_hip_runtime()
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(L, name)

@@ -1,0 +1,8 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 240 python __graft_entry__.py smoke > gpurun_out/smoke.log 2>&1 || { echo SMOKE_FAIL; tail -30 gpurun_out/smoke.log; exit 1; }
+timeout -k 10 900 python -m pytest tests/ -x -q -m gpu > gpurun_out/gpu_tests.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -30 gpurun_out/gpu_tests.log
+[ $rc -eq 0 ] || exit 1
+timeout -k 10 300 python bench.py --steps 1000 --warmup 100 > gpurun_out/bench.log 2>&1; echo "bench rc=$?"; tail -1 gpurun_out/bench.log
+timeout -k 10 300 python bench.py --steps 1000 --warmup 100 --mode philox --no-cpu-baseline > gpurun_out/bench_philox.log 2>&1; echo "bench philox rc=$?"; tail -1 gpurun_out/bench_philox.log
