@@ -32,6 +32,7 @@ constexpr int TPB = 256;
 constexpr int EPT = 4;
 constexpr int EPB = TPB * EPT;
 constexpr uint32_t SPIN_LIMIT = 1u << 24;
+constexpr int LB_WIN = 4;  // lookback window = LB_WIN * TPB predecessor tiles per round
 
 struct alignas(16) GridCtl {
   uint64_t s_hi, s_lo, inc_hi, inc_lo;  // PCG64 state at step start, increment
@@ -76,6 +77,8 @@ struct GridDev {
   const PcgJump* jt;
   const PcgJump* lt4;   // [256] jump by 4t  (per-thread action-draw offset inside a tile)
   const PcgJump* lt2;   // [256] jump by 2t  (per-thread word-check offset inside a tile)
+  const PcgJump* tja;   // [nblk] jump by tile*EPB + 1      (tile base of the action draws)
+  const PcgJump* tjw;   // [nblk] jump by B + tile*EPB/2     (tile base of the word checks)
   MetricSlot* mslot;
   uint32_t* ae;
   uint16_t* goal;
@@ -276,7 +279,6 @@ struct ScanShared {
   uint32_t red_rej[TPB / 64];
   uint32_t excl, exrej, total, blkrej;
   uint32_t bcast;
-  u128 base_a, base_w;  // tile base PCG states (action draws / word checks)
   uint32_t pos[EPB];    // slow path: absolute word positions of this tile's accepted draws
 };
 
@@ -318,32 +320,46 @@ __device__ void scan_and_lookback(const GridDev& p, uint64_t* __restrict__ statu
   if (tid == 0) st_status(&status[tile], st_pack(tile == 0 ? ST_FLAG_P : ST_FLAG_A, brej, tot));
   uint32_t excl = 0, exrej = 0;
   int base = tile - 1;
-  while (base >= 0) {  // block-uniform
-    const int idx = base - tid;
-    uint64_t s = st_pack(ST_FLAG_P, 0, 0);
-    if (idx >= 0) {
-      s = ld_status(&status[idx]);
+  while (base >= 0) {  // block-uniform; a window of LB_WIN * TPB predecessors per round
+    uint64_t sv[LB_WIN];
+#pragma unroll
+    for (int r = 0; r < LB_WIN; ++r) {
+      const int idx = base - r * TPB - tid;
+      sv[r] = idx >= 0 ? ld_status(&status[idx]) : st_pack(ST_FLAG_P, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < LB_WIN; ++r) {
+      const int idx = base - r * TPB - tid;
       uint32_t spins = 0;
-      while (st_flag(s) == ST_FLAG_X) {
+      while (st_flag(sv[r]) == ST_FLAG_X) {
         __builtin_amdgcn_s_sleep(1);
-        s = ld_status(&status[idx]);
+        sv[r] = ld_status(&status[idx]);
         if (++spins > SPIN_LIMIT) {
           atomicOr(&p.ctl->err, 1u);
-          s = st_pack(ST_FLAG_P, 0, 0);
+          sv[r] = st_pack(ST_FLAG_P, 0, 0);
           break;
         }
       }
     }
-    // nearest inclusive prefix = smallest tid holding a P
-    const unsigned long long pm = __ballot(st_flag(s) == ST_FLAG_P);
-    const uint32_t wmin = pm ? (uint32_t)(wid * 64 + __builtin_ctzll(pm)) : 0xFFFFu;
-    if (lane == 0) sh.red_min[wid] = wmin;
+    // nearest inclusive prefix = smallest window position (r*TPB + tid) holding a P
+    uint32_t mypos = 0xFFFFFu;
+#pragma unroll
+    for (int r = LB_WIN - 1; r >= 0; --r)
+      if (st_flag(sv[r]) == ST_FLAG_P) mypos = (uint32_t)(r * TPB + tid);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) mypos = min(mypos, (uint32_t)__shfl_xor(mypos, d, 64));
+    if (lane == 0) sh.red_min[wid] = mypos;
     __syncthreads();
-    uint32_t first = 0xFFFFu;
+    uint32_t first = 0xFFFFFu;
 #pragma unroll
     for (int w = 0; w < TPB / 64; ++w) first = min(first, sh.red_min[w]);
-    uint32_t v = (uint32_t)tid <= first ? st_count(s) : 0u;
-    uint32_t rj = (uint32_t)tid <= first ? st_rej(s) : 0u;
+    uint32_t v = 0, rj = 0;
+#pragma unroll
+    for (int r = 0; r < LB_WIN; ++r)
+      if ((uint32_t)(r * TPB + tid) <= first) {
+        v += st_count(sv[r]);
+        rj |= st_rej(sv[r]);
+      }
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) {
       v += __shfl_xor(v, d, 64);
@@ -359,9 +375,9 @@ __device__ void scan_and_lookback(const GridDev& p, uint64_t* __restrict__ statu
       excl += sh.red_sum[w];
       exrej |= sh.red_rej[w];
     }
-    __syncthreads();  // red_* reused next iteration
-    if (first != 0xFFFFu) break;
-    base -= TPB;
+    __syncthreads();  // red_* reused next round
+    if (first != 0xFFFFFu) break;
+    base -= LB_WIN * TPB;
   }
   if (tid == 0) {
     if (tile) st_status(&status[tile], st_pack(ST_FLAG_P, exrej | brej, excl + tot));
@@ -509,11 +525,9 @@ __device__ __forceinline__ Trans transition(const GridDev& p, uint32_t ae, int g
 #define PF_OBS_RESET 8    // write obs for the resetting envs (their sampling is complete)
 #define PF_STEP 16        // (choice pass) flags come from term|trunc, else every env resets
 
-// The 4 consecutive words w0..w0+3 of a thread whose tile word base (first word w = tile*EPB)
-// state is sh.base_w = u64 #qb (qb = (tile*EPB - h0) >> 1, possibly #-1) and lane offset 2t.
-__device__ __forceinline__ void words4_tile(const GridDev& p, const Stream& st, const u128& base_w, uint32_t w0,
-                                            uint32_t (&out)[4]) {
-  u128 s = apply_jump(p.lt2[threadIdx.x], base_w);
+// The 4 consecutive words of a thread, given the lane state of u64 #(qb + 2t) (qb = (tile*EPB -
+// h0) >> 1; for tile 0 with a buffered half that is "#-1", i.e. the state before the first draw).
+__device__ __forceinline__ void words4_lane(const Stream& st, u128 s, uint32_t w0, uint32_t (&out)[4]) {
   uint32_t k = 0, half;
   uint64_t x;
   if (!st.h0) {
@@ -562,17 +576,10 @@ __global__ __launch_bounds__(TPB, 4) void grid_step_numpy(GridDev p, const int32
   uint64_t* status = p.status + (size_t)parity * 2 * p.nblk;
   float rsum = 0.f;
   uint32_t eps = 0, lens = 0, nst = 0;
+  __syncthreads();
 
   for (int tile = blockIdx.x; tile < p.nblk; tile += gridDim.x) {
     const int env0 = tile * EPB + threadIdx.x * EPT;
-    if (threadIdx.x == 0) {
-      // random(B): env e draws the u64 at stream position e+1 (action_utils.py:84)
-      sh.base_a = pcg_jump(p.jt, st.s0, (uint32_t)(tile * EPB) + 1);
-      if (fused) {
-        const int qb = (tile * EPB - (int)st.h0) >> 1;  // -1 when tile 0 starts on the buffered word
-        sh.base_w = pcg_jump(p.jt, st.s0, (uint32_t)((int)st.U0 + qb + 1));
-      }
-    }
     int32_t a4[4];
     uint32_t ae4[4];
     load4<int32_t>(act, env0, p.B, a4);
@@ -587,10 +594,11 @@ __global__ __launch_bounds__(TPB, 4) void grid_step_numpy(GridDev p, const int32
 #pragma unroll
       for (int i = 0; i < 4; ++i) g4[i] = p.fixed_goal;
     }
-    __syncthreads();
+    // random(B): env e draws the u64 at stream position e+1 (action_utils.py:84). Lane state =
+    // (jump by 4t) o (jump by tile*EPB + 1) applied to s0, both tables precomputed per seed.
     uint64_t k4[4];
     {
-      u128 s = apply_jump(p.lt4[threadIdx.x], sh.base_a);
+      u128 s = apply_jump(p.lt4[threadIdx.x], apply_jump(p.tja[tile], st.s0));
       k4[0] = pcg_output(s) >> 11;
 #pragma unroll
       for (int i = 1; i < 4; ++i) {
@@ -613,14 +621,42 @@ __global__ __launch_bounds__(TPB, 4) void grid_step_numpy(GridDev p, const int32
         if (f4[i]) { eps += 1; lens += t4[i].elapsed; }
       }
     }
+    // Everything that does not depend on the reset draws leaves now, so the stores drain while
+    // the lookback below waits on the predecessor tiles.
+    {
+      float r[4];
+      uint8_t tm[4], tr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        r[i] = t4[i].rew;
+        tm[i] = t4[i].term;
+        tr[i] = t4[i].trunc;
+      }
+      store4<float>(rew, env0, p.B, r);
+      store4<uint8_t>(term, env0, p.B, tm);
+      store4<uint8_t>(trunc, env0, p.B, tr);
+    }
+    if (c == 0) {
+      uint32_t nae[4];
+      int ag[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        nae[i] = (uint32_t)t4[i].agent | ((uint32_t)t4[i].elapsed << 16);
+        ag[i] = t4[i].agent;
+      }
+      store4<uint32_t>(p.ae, env0, p.B, nae);
+      write_obs4<OK>(p, env0, ag, g4, obs);
+    }
     // choice(valid, b) for the resetting envs, ascending env order (msrooms.py:383-388): the
     // j-th resetter takes word j unless a Lemire rejection happened at or before it. Every
     // thread checks the 4 word positions equal to its env indices, so the inclusive lookback
     // flag covers positions [0, (tile+1)*EPB) >= every word this tile's resetters need.
     uint32_t rj = 0;
     if (fused) {
+      u128 s = apply_jump(p.lt2[threadIdx.x], apply_jump(p.tjw[tile], st.s0));
+      if (!st.h0) s = pcg_step(s, st.inc);
       uint32_t w4[4];
-      words4_tile(p, st, sh.base_w, (uint32_t)env0, w4);
+      words4_lane(st, s, (uint32_t)env0, w4);
 #pragma unroll
       for (int i = 0; i < 4; ++i) rj |= lemire_rejected(w4[i], n, thr) ? 1u : 0u;
     }
@@ -631,39 +667,29 @@ __global__ __launch_bounds__(TPB, 4) void grid_step_numpy(GridDev p, const int32
       if (threadIdx.x < 64) scan_accepted(p, st, 0, n, thr, sh.excl, sh.excl + sh.total, sh);
       __syncthreads();
     }
-    int agent4[4], goal4[4];
-    uint32_t j = excl_t;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      agent4[i] = t4[i].agent;
-      goal4[i] = t4[i].goal;
-      if (f4[i]) {
-        t4[i].elapsed = 0;
-        if (fused) {
-          const uint32_t w = slow ? sh.pos[j] : sh.excl + j;
-          const uint32_t v = lemire_value(word_at(p, st, w), n);
-          if (call_goal) goal4[i] = p.goal_valid[v];
-          else agent4[i] = p.agent_valid[v];
-        }
-        if (p.fixed_agent >= 0) agent4[i] = p.fixed_agent;
-        if (p.fixed_goal >= 0) goal4[i] = p.fixed_goal;
-        ++j;
-      }
-    }
-    {
-      float r[4];
-      uint8_t tm[4], tr[4];
-      uint32_t nae[4];
+    if (c) {
+      int agent4[4], goal4[4];
+      uint32_t j = excl_t;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        r[i] = t4[i].rew;
-        tm[i] = t4[i].term;
-        tr[i] = t4[i].trunc;
-        nae[i] = (uint32_t)agent4[i] | ((uint32_t)t4[i].elapsed << 16);
+        agent4[i] = t4[i].agent;
+        goal4[i] = t4[i].goal;
+        if (f4[i]) {
+          t4[i].elapsed = 0;
+          if (fused) {
+            const uint32_t w = slow ? sh.pos[j] : sh.excl + j;
+            const uint32_t v = lemire_value(word_at(p, st, w), n);
+            if (call_goal) goal4[i] = p.goal_valid[v];
+            else agent4[i] = p.agent_valid[v];
+          }
+          if (p.fixed_agent >= 0) agent4[i] = p.fixed_agent;
+          if (p.fixed_goal >= 0) goal4[i] = p.fixed_goal;
+          ++j;
+        }
       }
-      store4<float>(rew, env0, p.B, r);
-      store4<uint8_t>(term, env0, p.B, tm);
-      store4<uint8_t>(trunc, env0, p.B, tr);
+      uint32_t nae[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) nae[i] = (uint32_t)agent4[i] | ((uint32_t)t4[i].elapsed << 16);
       store4<uint32_t>(p.ae, env0, p.B, nae);
       if (p.fixed_goal < 0) {
         uint16_t gg[4];
@@ -978,7 +1004,7 @@ struct GridBackend : EnvBackend {
   std::vector<int32_t> cells;
   std::vector<uint16_t> goal_valid_h, agent_valid_h;
   DevBuf b_move, b_thr, b_gv, b_av, b_hbase, b_doff, b_hvec, b_t1, b_t2, b_coords, b_window, b_jt, b_lt4, b_lt2,
-      b_ae, b_goal, b_ctl, b_status, b_mslot;
+      b_tja, b_tjw, b_ae, b_goal, b_ctl, b_status, b_mslot;
   // replay pointers for the next step
   const uint64_t* rp_u = nullptr;
   const int32_t* rp_goal = nullptr;
@@ -1054,6 +1080,22 @@ int GridBackend::upload_rng() {
   }
   GP_HIP_CHECK(hipMemcpy(b_lt4.p, l4.data(), l4.size() * sizeof(PcgJump), hipMemcpyHostToDevice));
   GP_HIP_CHECK(hipMemcpy(b_lt2.p, l2.data(), l2.size() * sizeof(PcgJump), hipMemcpyHostToDevice));
+  // per-tile bases: tja[k] = jump(k*EPB + 1), tjw[k] = jump(B + k*EPB/2), built by composition
+  std::vector<PcgJump> ta(d.nblk), tw(d.nblk);
+  const PcgJump step_tile = pcg_jump_params((u128)EPB, rng.inc), step_half = pcg_jump_params((u128)(EPB / 2), rng.inc);
+  auto compose = [](const PcgJump& j2, const PcgJump& j1) {  // j2 o j1
+    const u128 a = mk128(j2.a_hi, j2.a_lo) * mk128(j1.a_hi, j1.a_lo);
+    const u128 c = mk128(j2.a_hi, j2.a_lo) * mk128(j1.c_hi, j1.c_lo) + mk128(j2.c_hi, j2.c_lo);
+    return PcgJump{hi64(a), lo64(a), hi64(c), lo64(c)};
+  };
+  ta[0] = pcg_jump_params((u128)1, rng.inc);
+  tw[0] = pcg_jump_params((u128)B, rng.inc);
+  for (int k = 1; k < d.nblk; ++k) {
+    ta[k] = compose(step_tile, ta[k - 1]);
+    tw[k] = compose(step_half, tw[k - 1]);
+  }
+  GP_HIP_CHECK(hipMemcpy(b_tja.p, ta.data(), ta.size() * sizeof(PcgJump), hipMemcpyHostToDevice));
+  GP_HIP_CHECK(hipMemcpy(b_tjw.p, tw.data(), tw.size() * sizeof(PcgJump), hipMemcpyHostToDevice));
   return GP_OK;
 }
 
@@ -1440,7 +1482,8 @@ int GridBackend::build(const gp_grid_config* cfg) {
   }
   nslots = std::max(d.nblk, grid_persist);
   if ((e = b_jt.alloc(sizeof(PcgJump) * JT_LEVELS * JT_RADIX)) || (e = b_lt4.alloc(sizeof(PcgJump) * TPB)) ||
-      (e = b_lt2.alloc(sizeof(PcgJump) * TPB)) || (e = b_ae.alloc(sizeof(uint32_t) * (B + 4))) ||
+      (e = b_lt2.alloc(sizeof(PcgJump) * TPB)) || (e = b_tja.alloc(sizeof(PcgJump) * (size_t)d.nblk)) ||
+      (e = b_tjw.alloc(sizeof(PcgJump) * (size_t)d.nblk)) || (e = b_ae.alloc(sizeof(uint32_t) * (B + 4))) ||
       (e = b_goal.alloc(sizeof(uint16_t) * (B + 8))) || (e = b_ctl.alloc(sizeof(GridCtlBlock))) ||
       (e = b_status.alloc(sizeof(uint64_t) * 4 * (size_t)d.nblk)) ||
       (e = b_mslot.alloc(sizeof(MetricSlot) * (size_t)nslots)))
@@ -1459,6 +1502,8 @@ int GridBackend::build(const gp_grid_config* cfg) {
   d.jt = b_jt.as<PcgJump>();
   d.lt4 = b_lt4.as<PcgJump>();
   d.lt2 = b_lt2.as<PcgJump>();
+  d.tja = b_tja.as<PcgJump>();
+  d.tjw = b_tjw.as<PcgJump>();
   d.mslot = b_mslot.as<MetricSlot>();
   d.ae = b_ae.as<uint32_t>();
   d.goal = b_goal.as<uint16_t>();
