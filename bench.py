@@ -31,6 +31,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec); 6.29 TB/s measur
 #   read  action int32 (4) + state agent|elapsed uint32 (4)
 #   write state (4) + obs int32 (4) + reward f32 (4) + terminated u8 (1) + truncated u8 (1)
 BYTES_PER_ENV_STEP = 22
+# Philox fused rollout: per env-step action 4 + obs 4 + reward 4 + term 1 + trunc 1; state once per launch
+ROLLOUT_BYTES_PER_ENV_STEP = 14
 
 
 def lib_hash():
@@ -147,9 +149,15 @@ def main():
     prof_steps = min(max(args.steps // 2, 50), 2000)
     run(prof_steps)
     kms, nk = env.profile_read()
+    rms, nr = env.profile_read_resolver()
     env.set_profiling(False)
     kavg_ms = kms / max(nk, 1)
-    achieved = BYTES_PER_ENV_STEP * B / (kavg_ms * 1e-3) / 1e9
+    ravg_ms = rms / max(nr, 1)
+    if args.mode == "philox":  # one fused launch = C steps; state read+written once per launch
+        bytes_per_launch = B * (ROLLOUT_BYTES_PER_ENV_STEP * C + 8)
+    else:
+        bytes_per_launch = B * BYTES_PER_ENV_STEP
+    achieved = bytes_per_launch / (kavg_ms * 1e-3) / 1e9
 
     m = env.metrics()
     mt = torch.tensor([m["episodes"], m["return_sum"], m["length_sum"], m["env_steps"]], dtype=torch.float64,
@@ -182,8 +190,11 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "grid_step_numpy<GP_OBS_HANSEN>" if args.mode == "numpy" else
                                "grid_rollout_counter<GP_OBS_HANSEN,false>",
-                     "kernel_avg_us": kavg_ms * 1e3, "bytes_per_env_step": BYTES_PER_ENV_STEP,
-                     "kernel_launches_timed": nk},
+                     "kernel_avg_us": kavg_ms * 1e3,
+                     "bytes_per_launch": bytes_per_launch,
+                     "kernel_launches_timed": nk,
+                     "resolver_kernel": "grid_resolve_numpy<GP_OBS_HANSEN>" if args.mode == "numpy" else None,
+                     "resolver_avg_us": ravg_ms * 1e3 if nr else None},
         "episodes": {"count": mt[0].item(), "mean_return": mt[1].item() / max(mt[0].item(), 1),
                      "mean_length": mt[2].item() / max(mt[0].item(), 1)},
         "lib_hash": lib_hash(),

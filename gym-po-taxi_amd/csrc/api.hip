@@ -332,7 +332,20 @@ int gp_taxi_reset_distribution(const gp_env* env, double* out, int cap) {
 int gp_set_profiling(gp_env* env, int enable) {
   GP_REQUIRE_ENV();
   env->be->timer.on = enable != 0;
+  env->be->timer2.on = enable != 0;
   return GP_OK;
+}
+
+int gp_profile_read_resolver(gp_env* env, double* total_ms, int64_t* n_launches) {
+  GP_REQUIRE_ENV();
+  double ms = 0;
+  int64_t n = 0;
+  int e = env->be->timer2.read(&ms, &n);
+  if (total_ms) *total_ms = ms + env->be->timer2.acc_ms;
+  if (n_launches) *n_launches = n + env->be->timer2.acc_n;
+  env->be->timer2.acc_ms = 0;
+  env->be->timer2.acc_n = 0;
+  return e;
 }
 
 int gp_profile_read(gp_env* env, double* total_ms, int64_t* n_launches) {

@@ -37,7 +37,8 @@ struct KernelTimer {
 };
 
 struct EnvBackend {
-  KernelTimer timer;
+  KernelTimer timer;   // the step kernel (K1 / fused rollout)
+  KernelTimer timer2;  // the reset resolver (K2, numpy mode)
   int64_t B = 0;
   int device = 0;
   int rng_mode = GP_RNG_NUMPY;

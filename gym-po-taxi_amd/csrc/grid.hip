@@ -32,18 +32,14 @@ constexpr int TPB = 256;
 constexpr int EPT = 4;
 constexpr int EPB = TPB * EPT;
 constexpr uint32_t SPIN_LIMIT = 1u << 24;
-constexpr int LB_WIN = 4;  // lookback window = LB_WIN * TPB predecessor tiles per round
+constexpr int MAX_TPB2 = 1024;  // max tiles per K2 block (B <= 256 * 1024 * EPB)
 
-struct alignas(16) GridCtl {
-  uint64_t s_hi, s_lo, inc_hi, inc_lo;  // PCG64 state at step start, increment
+struct alignas(64) GridCtl {
+  uint64_t s_hi, s_lo, inc_hi, inc_lo;  // numpy-mode PCG64 state at step start, increment
   uint32_t has_u32, uinteger;           // numpy's buffered 32-bit half
-  uint32_t b_total, w_after1;           // resets this step / absolute word index after call 1
-};
-
-struct alignas(64) GridCtlBlock {
-  GridCtl rec[2];
-  uint32_t parity;     // which rec is current
-  uint32_t err;        // bit0: lookback spin timeout
+  uint32_t epoch;                       // K2 launches so far (tags the per-block flags)
+  uint32_t err;                         // bit0: spin timeout
+  uint32_t b_total;                     // resets resolved by the last K2 (diagnostic)
 };
 
 // Per-block metric accumulators (each persistent block owns one slot: no atomics).
@@ -82,8 +78,10 @@ struct GridDev {
   MetricSlot* mslot;
   uint32_t* ae;
   uint16_t* goal;
-  GridCtlBlock* ctl;
-  uint64_t* status;  // [2 parities][2 sets][nblk]
+  GridCtl* ctl;
+  uint32_t* tcount;  // [nblk] resets per tile (K1 -> K2)
+  uint16_t* tlist;   // [nblk*EPB] local offsets of a tile's resetting envs, ascending
+  uint32_t* rflag;   // [<=256] K2 per-block rejection flags, tagged with the epoch
   // philox / replay
   uint32_t key0, key1;
   const uint64_t* rp_u;
@@ -270,130 +268,79 @@ __device__ __forceinline__ void words4(const GridDev& p, const Stream& st, uint3
   }
 }
 
-// ------------------------------------------------------------------ block scan + lookback ----
-struct ScanShared {
-  uint32_t wsum[TPB / 64];
-  uint32_t wrej[TPB / 64];
-  uint32_t red_min[TPB / 64];
-  uint32_t red_sum[TPB / 64];
-  uint32_t red_rej[TPB / 64];
-  uint32_t excl, exrej, total, blkrej;
-  uint32_t bcast;
-  uint32_t pos[EPB];    // slow path: absolute word positions of this tile's accepted draws
+// Sequential reader of the 32-bit word stream from absolute word index w (numpy next_uint32
+// semantics: buffered half first if present, then low/high halves of successive u64 draws).
+struct WordIter {
+  u128 s;
+  uint64_t x;
+  uint32_t half;
+  bool buf;
+  __device__ __forceinline__ void init(const GridDev& p, const Stream& st, uint32_t w) {
+    if (st.h0 && w == 0) {
+      buf = true;
+      s = pcg_jump(p.jt, st.s0, st.U0);  // state before u64 #0
+      x = 0;
+      half = 0;
+    } else {
+      buf = false;
+      const uint32_t ww = w - st.h0;
+      s = pcg_jump(p.jt, st.s0, st.U0 + (ww >> 1) + 1);
+      x = pcg_output(s);
+      half = ww & 1;
+    }
+  }
+  __device__ __forceinline__ uint32_t next(const Stream& st) {
+    if (buf) {
+      buf = false;
+      s = pcg_step(s, st.inc);
+      x = pcg_output(s);
+      half = 0;
+      return st.u0;
+    }
+    const uint32_t v = half ? (uint32_t)(x >> 32) : (uint32_t)x;
+    if (half) {
+      s = pcg_step(s, st.inc);
+      x = pcg_output(s);
+    }
+    half ^= 1;
+    return v;
+  }
 };
 
-__device__ __forceinline__ uint64_t ld_status(const uint64_t* p) {
+struct ResolveShared {
+  uint32_t red[TPB / 64];
+  uint32_t red2[TPB / 64];
+  uint32_t tpre[MAX_TPB2 + 1];   // exclusive prefix of this block's tile counts
+  uint32_t P, btot, n, anyrej, w1, bcast;
+  uint32_t pos[EPB];              // slow path: accepted-word positions of one batch of ranks
+  uint32_t pos2[EPB];
+};
+
+__device__ __forceinline__ uint32_t ld_flag(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void st_status(uint64_t* p, uint64_t v) {
+__device__ __forceinline__ void st_flag32(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Exclusive block prefix of c (reset count per thread) and OR of r (rejection seen) over the
-// tile, then a decoupled lookback over the predecessor tiles with a 256-wide window: every
-// thread polls one predecessor status, the nearest inclusive prefix ends the walk. Tiles are
-// visited in increasing order by the persistent blocks, so every awaited tile is owned by a
-// resident block that waits only on smaller tiles (deadlock-free). Results land in sh.
-__device__ void scan_and_lookback(const GridDev& p, uint64_t* __restrict__ status, int tile, uint32_t c, uint32_t r,
-                                  uint32_t& excl_thread, ScanShared& sh) {
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  uint32_t x = c;
+template <class T>
+__device__ __forceinline__ T block_sum(T v, T* red) {
 #pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    uint32_t y = __shfl_up(x, d, 64);
-    if (lane >= d) x += y;
-  }
-  const bool wr = __any((int)r);
-  if (lane == 63) {
-    sh.wsum[wid] = x;
-    sh.wrej[wid] = wr ? 1u : 0u;
-  }
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
   __syncthreads();
-  uint32_t woff = 0, tot = 0, brej = 0;
-#pragma unroll
-  for (int w = 0; w < TPB / 64; ++w) {
-    if (w < wid) woff += sh.wsum[w];
-    tot += sh.wsum[w];
-    brej |= sh.wrej[w];
-  }
-  excl_thread = x - c + woff;
-  if (tid == 0) st_status(&status[tile], st_pack(tile == 0 ? ST_FLAG_P : ST_FLAG_A, brej, tot));
-  uint32_t excl = 0, exrej = 0;
-  int base = tile - 1;
-  while (base >= 0) {  // block-uniform; a window of LB_WIN * TPB predecessors per round
-    uint64_t sv[LB_WIN];
-#pragma unroll
-    for (int r = 0; r < LB_WIN; ++r) {
-      const int idx = base - r * TPB - tid;
-      sv[r] = idx >= 0 ? ld_status(&status[idx]) : st_pack(ST_FLAG_P, 0, 0);
-    }
-#pragma unroll
-    for (int r = 0; r < LB_WIN; ++r) {
-      const int idx = base - r * TPB - tid;
-      uint32_t spins = 0;
-      while (st_flag(sv[r]) == ST_FLAG_X) {
-        __builtin_amdgcn_s_sleep(1);
-        sv[r] = ld_status(&status[idx]);
-        if (++spins > SPIN_LIMIT) {
-          atomicOr(&p.ctl->err, 1u);
-          sv[r] = st_pack(ST_FLAG_P, 0, 0);
-          break;
-        }
-      }
-    }
-    // nearest inclusive prefix = smallest window position (r*TPB + tid) holding a P
-    uint32_t mypos = 0xFFFFFu;
-#pragma unroll
-    for (int r = LB_WIN - 1; r >= 0; --r)
-      if (st_flag(sv[r]) == ST_FLAG_P) mypos = (uint32_t)(r * TPB + tid);
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) mypos = min(mypos, (uint32_t)__shfl_xor(mypos, d, 64));
-    if (lane == 0) sh.red_min[wid] = mypos;
-    __syncthreads();
-    uint32_t first = 0xFFFFFu;
-#pragma unroll
-    for (int w = 0; w < TPB / 64; ++w) first = min(first, sh.red_min[w]);
-    uint32_t v = 0, rj = 0;
-#pragma unroll
-    for (int r = 0; r < LB_WIN; ++r)
-      if ((uint32_t)(r * TPB + tid) <= first) {
-        v += st_count(sv[r]);
-        rj |= st_rej(sv[r]);
-      }
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-      v += __shfl_xor(v, d, 64);
-      rj |= __shfl_xor(rj, d, 64);
-    }
-    if (lane == 0) {
-      sh.red_sum[wid] = v;
-      sh.red_rej[wid] = rj;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int w = 0; w < TPB / 64; ++w) {
-      excl += sh.red_sum[w];
-      exrej |= sh.red_rej[w];
-    }
-    __syncthreads();  // red_* reused next round
-    if (first != 0xFFFFFu) break;
-    base -= LB_WIN * TPB;
-  }
-  if (tid == 0) {
-    if (tile) st_status(&status[tile], st_pack(ST_FLAG_P, exrej | brej, excl + tot));
-    sh.excl = excl;
-    sh.exrej = exrej;
-    sh.total = tot;
-    sh.blkrej = brej;
-  }
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
+  T s = 0;
+#pragma unroll
+  for (int w = 0; w < TPB / 64; ++w) s += red[w];
+  return s;
 }
 
-// Slow path (a Lemire rejection somewhere before this tile's draws): wave 0 walks the word
-// stream from `wbase`, recording the absolute positions of the accepted draws with rank in
-// [jlo, jhi) into sh.pos. Returns (to wave 0) the position after the last recorded draw.
+// Slow path (a Lemire rejection somewhere): wave 0 walks the word stream from `wbase`,
+// recording the absolute positions of the accepted draws with rank in [jlo, jhi) into out.
+// Returns (to wave 0) the position after the last recorded draw.
 __device__ uint32_t scan_accepted(const GridDev& p, const Stream& st, uint32_t wbase, uint32_t n, uint32_t thr,
-                                  uint32_t jlo, uint32_t jhi, ScanShared& sh) {
+                                  uint32_t jlo, uint32_t jhi, uint32_t* out) {
   const int lane = threadIdx.x & 63;
   uint32_t acc = 0, pos = wbase, after = wbase;
   while (acc < jhi) {
@@ -403,7 +350,7 @@ __device__ uint32_t scan_accepted(const GridDev& p, const Stream& st, uint32_t w
     const uint32_t below = (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
     const uint32_t j = acc + below;
     if (ok && j >= jlo && j < jhi) {
-      sh.pos[j - jlo] = pos + lane;
+      if (out) out[j - jlo] = pos + lane;
       if (j == jhi - 1) after = pos + lane + 1;
     }
     acc += (uint32_t)__builtin_popcountll(m);
@@ -413,49 +360,6 @@ __device__ uint32_t scan_accepted(const GridDev& p, const Stream& st, uint32_t w
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) a = max(a, __shfl_xor(a, d, 64));
   return a;
-}
-
-// ------------------------------------------------------------------ rng finalisation ----
-// Called by the block that owns the last tile of the last pass of a step/reset: publishes the
-// next PCG64 state into the other ctl record, clears the other parity's status words, flips
-// the parity. Every block read the parity before publishing its first tile, and the last
-// tile's lookback saw every tile, so no block of this launch reads the parity afterwards.
-__device__ void finalize_rng(const GridDev& p, const Stream& st, uint32_t parity, uint32_t wtot) {
-  if (threadIdx.x == 0) {
-    uint32_t used, h, u = st.u0;
-    if (wtot == 0) {
-      used = 0; h = st.h0;
-    } else if (st.h0) {
-      used = wtot >> 1;          // ceil((wtot-1)/2)
-      h = (wtot - 1) & 1;
-    } else {
-      used = (wtot + 1) >> 1;    // ceil(wtot/2)
-      h = wtot & 1;
-    }
-    u128 s = pcg_jump(p.jt, st.s0, st.U0 + used);
-    // numpy keeps the last buffered half in `uinteger` even after it has been consumed
-    if (used) u = (uint32_t)(pcg_output(s) >> 32);
-    GridCtl* N = &p.ctl->rec[parity ^ 1];
-    N->s_hi = hi64(s);
-    N->s_lo = lo64(s);
-    N->inc_hi = hi64(st.inc);
-    N->inc_lo = lo64(st.inc);
-    N->has_u32 = h;
-    N->uinteger = u;
-    N->b_total = 0;
-    N->w_after1 = 0;
-  }
-  uint64_t* other = p.status + (size_t)(parity ^ 1) * 2 * p.nblk;
-  for (int i = threadIdx.x; i < 2 * p.nblk; i += TPB) other[i] = 0;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    __hip_atomic_store(&p.ctl->parity, parity ^ 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-__device__ __forceinline__ uint32_t read_parity(const GridDev& p) {
-  return __hip_atomic_load(&p.ctl->parity, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Per-block metrics (episode count / return / length / env-steps) into the block's own slot.
@@ -518,324 +422,274 @@ __device__ __forceinline__ Trans transition(const GridDev& p, uint32_t ae, int g
 }
 
 // ------------------------------------------------------------------ kernels: numpy mode ----
-// Pass flags
-#define PF_FUSED_CALL 1   // this pass performs a choice() call for its resetting envs
-#define PF_CALL_GOAL 2    // the call samples goals (else agents)
-#define PF_FINAL 4        // this pass publishes the next rng state
-#define PF_OBS_RESET 8    // write obs for the resetting envs (their sampling is complete)
-#define PF_STEP 16        // (choice pass) flags come from term|trunc, else every env resets
-
-// The 4 consecutive words of a thread, given the lane state of u64 #(qb + 2t) (qb = (tile*EPB -
-// h0) >> 1; for tile 0 with a buffered half that is "#-1", i.e. the state before the first draw).
-__device__ __forceinline__ void words4_lane(const Stream& st, u128 s, uint32_t w0, uint32_t (&out)[4]) {
-  uint32_t k = 0, half;
-  uint64_t x;
-  if (!st.h0) {
-    half = 0;
-    x = pcg_output(s);
-  } else if (w0 == 0) {
-    out[0] = st.u0;
-    k = 1;
-    s = pcg_step(s, st.inc);
-    x = pcg_output(s);
-    half = 0;
-  } else {
-    x = pcg_output(s);
-    half = 1;
-  }
-  for (; k < 4; ++k) {
-    out[k] = half ? (uint32_t)(x >> 32) : (uint32_t)x;
-    if (half) {
-      s = pcg_step(s, st.inc);
-      x = pcg_output(s);
-    }
-    half ^= 1;
-  }
-}
-
+// K1 — the streaming step (msrooms.py:398-411): random(B) action-failure draws, move, reward,
+// terminated/truncated, and every output for every env. Envs that reset get elapsed = 0 and
+// provisional agent/goal/obs; their indices go to a per-tile list for K2. No inter-block
+// dependency: a pure load -> compute -> store kernel.
 template <int OK>
-__global__ __launch_bounds__(TPB, 4) void grid_step_numpy(GridDev p, const int32_t* __restrict__ act,
-                                                          void* __restrict__ obs, float* __restrict__ rew,
-                                                          uint8_t* __restrict__ term, uint8_t* __restrict__ trunc,
-                                                          int flags) {
-  __shared__ ScanShared sh;
+__global__ __launch_bounds__(TPB) void grid_step_numpy(GridDev p, const int32_t* __restrict__ act,
+                                                       void* __restrict__ obs, float* __restrict__ rew,
+                                                       uint8_t* __restrict__ term, uint8_t* __restrict__ trunc) {
   __shared__ uint64_t s_thr[64];
-  const uint32_t parity = read_parity(p);
-  const GridCtl* C = &p.ctl->rec[parity];
+  __shared__ uint32_t s_red[TPB / 64];
   if (threadIdx.x < p.nact * p.nact) s_thr[threadIdx.x] = p.thr[threadIdx.x];
-  Stream st;
-  st.s0 = mk128(C->s_hi, C->s_lo);
-  st.inc = mk128(C->inc_hi, C->inc_lo);
-  st.h0 = C->has_u32;
-  st.u0 = C->uinteger;
-  st.U0 = (uint32_t)p.B;
-  const bool fused = flags & PF_FUSED_CALL;
-  const bool call_goal = flags & PF_CALL_GOAL;
-  const uint32_t n = call_goal ? (uint32_t)p.n_goal_valid : (uint32_t)p.n_agent_valid;
-  const uint32_t thr = call_goal ? p.thr_goal : p.thr_agent;
-  uint64_t* status = p.status + (size_t)parity * 2 * p.nblk;
+  const GridCtl* C = p.ctl;
+  const u128 s0 = mk128(C->s_hi, C->s_lo);
+  const u128 inc = mk128(C->inc_hi, C->inc_lo);
+  const int tile = blockIdx.x;
+  const int env0 = tile * EPB + threadIdx.x * EPT;
+  int32_t a4[4];
+  uint32_t ae4[4];
+  load4<int32_t>(act, env0, p.B, a4);
+  load4<uint32_t>(p.ae, env0, p.B, ae4);
+  int g4[4];
+  if (p.fixed_goal < 0) {
+    uint16_t gg[4];
+    load4<uint16_t>(p.goal, env0, p.B, gg);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) g4[i] = gg[i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) g4[i] = p.fixed_goal;
+  }
+  // random(B): env e draws the u64 at stream position e+1 (action_utils.py:84). Lane state =
+  // (jump by 4t) o (jump by tile*EPB + 1) applied to s0, both tables precomputed per seed.
+  uint64_t k4[4];
+  {
+    u128 s = apply_jump(p.lt4[threadIdx.x], apply_jump(p.tja[tile], s0));
+    k4[0] = pcg_output(s) >> 11;
+#pragma unroll
+    for (int i = 1; i < 4; ++i) {
+      s = pcg_step(s, inc);
+      k4[i] = pcg_output(s) >> 11;
+    }
+  }
+  __syncthreads();  // s_thr
+  float r[4];
+  uint8_t tm[4], tr[4];
+  uint32_t nae[4];
+  int ag[4], gl[4];
+  uint32_t c = 0, fm = 0;
   float rsum = 0.f;
   uint32_t eps = 0, lens = 0, nst = 0;
-  __syncthreads();
-
-  for (int tile = blockIdx.x; tile < p.nblk; tile += gridDim.x) {
-    const int env0 = tile * EPB + threadIdx.x * EPT;
-    int32_t a4[4];
-    uint32_t ae4[4];
-    load4<int32_t>(act, env0, p.B, a4);
-    load4<uint32_t>(p.ae, env0, p.B, ae4);
-    int g4[4];
-    if (p.fixed_goal < 0) {
-      uint16_t gg[4];
-      load4<uint16_t>(p.goal, env0, p.B, gg);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) g4[i] = gg[i];
-    } else {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) g4[i] = p.fixed_goal;
+  for (int i = 0; i < 4; ++i) {
+    const Trans t = transition(p, ae4[i], g4[i], a4[i], k4[i], s_thr);
+    const bool valid = env0 + i < p.B;
+    const bool f = valid && (t.term | t.trunc);
+    r[i] = t.rew;
+    tm[i] = t.term;
+    tr[i] = t.trunc;
+    ag[i] = f && p.fixed_agent >= 0 ? p.fixed_agent : t.agent;
+    gl[i] = t.goal;
+    nae[i] = (uint32_t)ag[i] | ((uint32_t)(f ? 0 : t.elapsed) << 16);
+    c += f;
+    fm |= (f ? 1u : 0u) << i;
+    if (valid) {
+      rsum += t.rew;
+      nst += 1;
+      if (f) { eps += 1; lens += (uint32_t)t.elapsed; }
     }
-    // random(B): env e draws the u64 at stream position e+1 (action_utils.py:84). Lane state =
-    // (jump by 4t) o (jump by tile*EPB + 1) applied to s0, both tables precomputed per seed.
-    uint64_t k4[4];
-    {
-      u128 s = apply_jump(p.lt4[threadIdx.x], apply_jump(p.tja[tile], st.s0));
-      k4[0] = pcg_output(s) >> 11;
-#pragma unroll
-      for (int i = 1; i < 4; ++i) {
-        s = pcg_step(s, st.inc);
-        k4[i] = pcg_output(s) >> 11;
-      }
-    }
-    Trans t4[4];
-    uint32_t c = 0;
-    int f4[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      t4[i] = transition(p, ae4[i], g4[i], a4[i], k4[i], s_thr);
-      const bool valid = env0 + i < p.B;
-      f4[i] = valid && (t4[i].term | t4[i].trunc);
-      c += f4[i];
-      if (valid) {
-        rsum += t4[i].rew;
-        nst += 1;
-        if (f4[i]) { eps += 1; lens += t4[i].elapsed; }
-      }
-    }
-    // Everything that does not depend on the reset draws leaves now, so the stores drain while
-    // the lookback below waits on the predecessor tiles.
-    {
-      float r[4];
-      uint8_t tm[4], tr[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        r[i] = t4[i].rew;
-        tm[i] = t4[i].term;
-        tr[i] = t4[i].trunc;
-      }
-      store4<float>(rew, env0, p.B, r);
-      store4<uint8_t>(term, env0, p.B, tm);
-      store4<uint8_t>(trunc, env0, p.B, tr);
-    }
-    if (c == 0) {
-      uint32_t nae[4];
-      int ag[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        nae[i] = (uint32_t)t4[i].agent | ((uint32_t)t4[i].elapsed << 16);
-        ag[i] = t4[i].agent;
-      }
-      store4<uint32_t>(p.ae, env0, p.B, nae);
-      write_obs4<OK>(p, env0, ag, g4, obs);
-    }
-    // choice(valid, b) for the resetting envs, ascending env order (msrooms.py:383-388): the
-    // j-th resetter takes word j unless a Lemire rejection happened at or before it. Every
-    // thread checks the 4 word positions equal to its env indices, so the inclusive lookback
-    // flag covers positions [0, (tile+1)*EPB) >= every word this tile's resetters need.
-    uint32_t rj = 0;
-    if (fused) {
-      u128 s = apply_jump(p.lt2[threadIdx.x], apply_jump(p.tjw[tile], st.s0));
-      if (!st.h0) s = pcg_step(s, st.inc);
-      uint32_t w4[4];
-      words4_lane(st, s, (uint32_t)env0, w4);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) rj |= lemire_rejected(w4[i], n, thr) ? 1u : 0u;
-    }
-    uint32_t excl_t;
-    scan_and_lookback(p, status, tile, c, rj, excl_t, sh);
-    const bool slow = fused && sh.total && (sh.exrej | sh.blkrej);
-    if (slow) {
-      if (threadIdx.x < 64) scan_accepted(p, st, 0, n, thr, sh.excl, sh.excl + sh.total, sh);
-      __syncthreads();
-    }
-    if (c) {
-      int agent4[4], goal4[4];
-      uint32_t j = excl_t;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        agent4[i] = t4[i].agent;
-        goal4[i] = t4[i].goal;
-        if (f4[i]) {
-          t4[i].elapsed = 0;
-          if (fused) {
-            const uint32_t w = slow ? sh.pos[j] : sh.excl + j;
-            const uint32_t v = lemire_value(word_at(p, st, w), n);
-            if (call_goal) goal4[i] = p.goal_valid[v];
-            else agent4[i] = p.agent_valid[v];
-          }
-          if (p.fixed_agent >= 0) agent4[i] = p.fixed_agent;
-          if (p.fixed_goal >= 0) goal4[i] = p.fixed_goal;
-          ++j;
-        }
-      }
-      uint32_t nae[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) nae[i] = (uint32_t)agent4[i] | ((uint32_t)t4[i].elapsed << 16);
-      store4<uint32_t>(p.ae, env0, p.B, nae);
-      if (p.fixed_goal < 0) {
-        uint16_t gg[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) gg[i] = (uint16_t)goal4[i];
-        store4<uint16_t>(p.goal, env0, p.B, gg);
-      }
-      if (flags & PF_OBS_RESET) {
-        write_obs4<OK>(p, env0, agent4, goal4, obs);
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (env0 + i < p.B && !f4[i]) write_obs<OK>(p, env0 + i, agent4[i], goal4[i], obs);
-      }
-    }
-    if (tile == p.nblk - 1) {
-      const uint32_t btot = sh.excl + sh.total;
-      uint32_t wafter = 0;
-      if (fused && btot) {
-        if (sh.exrej | sh.blkrej) {
-          uint32_t a = 0;
-          if (threadIdx.x < 64) a = scan_accepted(p, st, 0, n, thr, btot - 1, btot, sh);
-          if (threadIdx.x == 0) sh.bcast = a;
-          __syncthreads();
-          wafter = sh.bcast;
-        } else {
-          wafter = btot;
-        }
-      }
-      if (flags & PF_FINAL) {
-        finalize_rng(p, st, parity, wafter);
-      } else if (threadIdx.x == 0) {
-        p.ctl->rec[parity].b_total = btot;
-        p.ctl->rec[parity].w_after1 = wafter;
-      }
-    }
-    __syncthreads();  // sh reused by the next tile
   }
+  store4<float>(rew, env0, p.B, r);
+  store4<uint8_t>(term, env0, p.B, tm);
+  store4<uint8_t>(trunc, env0, p.B, tr);
+  store4<uint32_t>(p.ae, env0, p.B, nae);
+  write_obs4<OK>(p, env0, ag, gl, obs);
+  // compact this tile's resetters (ascending env order) for K2
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t x = c;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) s_red[wid] = x;
+  __syncthreads();
+  uint32_t off = x - c, tot = 0;
+#pragma unroll
+  for (int w = 0; w < TPB / 64; ++w) {
+    if (w < wid) off += s_red[w];
+    tot += s_red[w];
+  }
+  if (c) {
+    uint16_t* lst = p.tlist + (size_t)tile * EPB;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (fm & (1u << i)) lst[off++] = (uint16_t)(threadIdx.x * EPT + i);
+  }
+  if (threadIdx.x == 0) p.tcount[tile] = tot;
   add_metrics(p, rsum, eps, lens, nst);
 }
 
-// A standalone choice() pass: the agent draws after random goals in step(), and every sampling
-// call of reset(). Flags come from term|trunc (PF_STEP) or are all set (reset).
+// K2 — choice(valid, b) for the b resetting envs in ascending env order (goal call, then agent
+// call; msrooms.py:383-388 / rooms.py:191-196), and the next PCG64 state. Block i owns tiles
+// [i*T, (i+1)*T): its resetters have ranks [P_i, P_i + n_i), P_i = resets in earlier tiles.
+// Fast path: the j-th resetter of a call takes word (call base + j). Every block checks its own
+// words for Lemire rejections and publishes a flag; a block whose range or any predecessor's
+// range holds a rejection recomputes exact positions by walking the stream (rare: p ~ 1e-8
+// per word). The last block publishes the next RNG state (it waited on every other block).
+#define RM_RESET 1  // every env resets (reset()); U0 = 0, no random(B) before the words
+
 template <int OK>
-__global__ __launch_bounds__(TPB, 4) void grid_choice_numpy(GridDev p, const uint8_t* __restrict__ term,
-                                                            const uint8_t* __restrict__ trunc,
-                                                            void* __restrict__ obs, int flags, int set,
-                                                            uint32_t wbase_fixed, int use_wafter1, uint32_t U0) {
-  __shared__ ScanShared sh;
-  const uint32_t parity = read_parity(p);
-  const GridCtl* C = &p.ctl->rec[parity];
+__global__ __launch_bounds__(TPB) void grid_resolve_numpy(GridDev p, void* __restrict__ obs, int mode, uint32_t U0) {
+  __shared__ ResolveShared sh;
+  GridCtl* C = p.ctl;
   Stream st;
   st.s0 = mk128(C->s_hi, C->s_lo);
   st.inc = mk128(C->inc_hi, C->inc_lo);
   st.h0 = C->has_u32;
   st.u0 = C->uinteger;
   st.U0 = U0;
-  const uint32_t wbase = use_wafter1 ? C->w_after1 : wbase_fixed;
-  const bool call_goal = flags & PF_CALL_GOAL;
-  const uint32_t n = call_goal ? (uint32_t)p.n_goal_valid : (uint32_t)p.n_agent_valid;
-  const uint32_t thr = call_goal ? p.thr_goal : p.thr_agent;
-  uint64_t* status = p.status + ((size_t)parity * 2 + set) * p.nblk;
-  for (int tile = blockIdx.x; tile < p.nblk; tile += gridDim.x) {
-    const int env0 = tile * EPB + threadIdx.x * EPT;
-    int f4[4];
-    if (flags & PF_STEP) {
-      uint8_t tm[4], tr[4];
-      load4<uint8_t>(term, env0, p.B, tm);
-      load4<uint8_t>(trunc, env0, p.B, tr);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) f4[i] = (env0 + i < p.B) && (tm[i] | tr[i]);
-    } else {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) f4[i] = env0 + i < p.B;
+  const uint32_t epoch = C->epoch;
+  const bool reset_all = mode & RM_RESET;
+  const bool rgoal = p.fixed_goal < 0, ragent = p.fixed_agent < 0;
+  const int ncalls = (int)rgoal + (int)ragent;
+  const int T = (p.nblk + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int t0 = min((int)blockIdx.x * T, p.nblk), t1 = min(t0 + T, p.nblk);
+  auto count_of = [&](int k) -> uint32_t {
+    return reset_all ? (uint32_t)min(EPB, p.B - k * EPB) : p.tcount[k];
+  };
+  // prefix of the tile counts before my tiles, and the total
+  uint32_t pre = 0, all = 0;
+  for (int k = threadIdx.x; k < p.nblk; k += TPB) {
+    const uint32_t v = count_of(k);
+    all += v;
+    if (k < t0) pre += v;
+  }
+  const uint32_t P = block_sum(pre, sh.red);
+  const uint32_t btot = block_sum(all, sh.red2);
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    for (int k = t0; k < t1; ++k) {
+      sh.tpre[k - t0] = acc;
+      acc += count_of(k);
     }
-    uint32_t c = (uint32_t)(f4[0] + f4[1] + f4[2] + f4[3]);
-    uint32_t rj = 0;
-    {
-      uint32_t w4[4];
-      words4(p, st, wbase + (uint32_t)env0, w4);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) rj |= lemire_rejected(w4[i], n, thr) ? 1u : 0u;
-    }
-    uint32_t excl_t;
-    scan_and_lookback(p, status, tile, c, rj, excl_t, sh);
-    const bool slow = sh.total && (sh.exrej | sh.blkrej);
-    if (slow) {
-      if (threadIdx.x < 64) scan_accepted(p, st, wbase, n, thr, sh.excl, sh.excl + sh.total, sh);
-      __syncthreads();
-    }
-    uint32_t ae4[4];
-    load4<uint32_t>(p.ae, env0, p.B, ae4);
-    int agent4[4], goal4[4];
-    uint16_t gg[4] = {0, 0, 0, 0};
-    if (p.fixed_goal < 0) load4<uint16_t>(p.goal, env0, p.B, gg);
-    uint32_t j = excl_t;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      agent4[i] = (int)(ae4[i] & 0xFFFF);
-      goal4[i] = p.fixed_goal < 0 ? (int)gg[i] : p.fixed_goal;
-      if (f4[i]) {
-        const uint32_t w = slow ? sh.pos[j] : wbase + sh.excl + j;
-        const uint32_t v = lemire_value(word_at(p, st, w), n);
-        if (call_goal) goal4[i] = p.goal_valid[v];
-        else agent4[i] = p.agent_valid[v];
-        ++j;
+    sh.tpre[t1 - t0] = acc;
+    sh.n = acc;
+  }
+  __syncthreads();
+  const uint32_t n = sh.n;
+  // pass A: Lemire rejections among my words (fast-path positions)
+  uint32_t rj = 0;
+  if (n) {
+    const uint32_t m = (n + TPB - 1) / TPB;
+    const uint32_t q0 = threadIdx.x * m, q1 = min(q0 + m, n);
+    for (int cidx = 0; cidx < ncalls; ++cidx) {
+      const bool goal_call = rgoal && cidx == 0;
+      const uint32_t nv = goal_call ? (uint32_t)p.n_goal_valid : (uint32_t)p.n_agent_valid;
+      const uint32_t th = goal_call ? p.thr_goal : p.thr_agent;
+      if (q0 < q1) {
+        WordIter it;
+        it.init(p, st, (uint32_t)cidx * btot + P + q0);
+        for (uint32_t q = q0; q < q1; ++q) rj |= lemire_rejected(it.next(st), nv, th) ? 1u : 0u;
       }
     }
-    if (call_goal) {
-      if (p.fixed_goal < 0) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) gg[i] = (uint16_t)goal4[i];
-        store4<uint16_t>(p.goal, env0, p.B, gg);
+  }
+  const uint32_t myrej = __syncthreads_or((int)rj) ? 1u : 0u;
+  if (threadIdx.x == 0) st_flag32(&p.rflag[blockIdx.x], ((epoch + 1u) << 1) | myrej);
+  // wait for every predecessor block's flag (all K2 blocks are resident: gridDim <= 256)
+  uint32_t prej = 0;
+  for (int j = threadIdx.x; j < (int)blockIdx.x; j += TPB) {
+    uint32_t f = ld_flag(&p.rflag[j]);
+    uint32_t spins = 0;
+    while ((f >> 1) != epoch + 1u) {
+      __builtin_amdgcn_s_sleep(1);
+      f = ld_flag(&p.rflag[j]);
+      if (++spins > SPIN_LIMIT) {
+        atomicOr(&C->err, 1u);
+        break;
       }
-    } else {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) ae4[i] = (ae4[i] & 0xFFFF0000u) | (uint32_t)agent4[i];
-      store4<uint32_t>(p.ae, env0, p.B, ae4);
     }
-    if (flags & PF_OBS_RESET) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (f4[i]) write_obs<OK>(p, env0 + i, agent4[i], goal4[i], obs);
-    }
-    if (tile == p.nblk - 1) {
-      const uint32_t btot = sh.excl + sh.total;
-      uint32_t wafter = wbase;
-      if (btot) {
-        if (sh.exrej | sh.blkrej) {
-          uint32_t a = 0;
-          if (threadIdx.x < 64) a = scan_accepted(p, st, wbase, n, thr, btot - 1, btot, sh);
-          if (threadIdx.x == 0) sh.bcast = a;
-          __syncthreads();
-          wafter = sh.bcast;
-        } else {
-          wafter = wbase + btot;
-        }
-      }
-      if (flags & PF_FINAL) {
-        finalize_rng(p, st, parity, wafter);
-      } else if (threadIdx.x == 0) {
-        p.ctl->rec[parity].b_total = btot;
-        p.ctl->rec[parity].w_after1 = wafter;
-      }
+    prej |= f & 1u;
+  }
+  const bool slow = __syncthreads_or((int)(prej | myrej)) != 0;
+  // exact call-2 base when a rejection is anywhere before or in call 1
+  uint32_t w1 = btot;
+  if (slow && ncalls == 2 && btot) {
+    if (threadIdx.x < 64) {
+      const uint32_t a = scan_accepted(p, st, 0, (uint32_t)p.n_goal_valid, p.thr_goal, btot - 1, btot, nullptr);
+      if (threadIdx.x == 0) sh.w1 = a;
     }
     __syncthreads();
+    w1 = sh.w1;
+  }
+  // pass B: resolve my resetters, in batches of EPB ranks
+  for (uint32_t b0 = 0; b0 < n; b0 += EPB) {
+    const uint32_t bl = min((uint32_t)EPB, n - b0);
+    if (slow) {
+      if (threadIdx.x < 64) {
+        if (rgoal)
+          scan_accepted(p, st, 0, (uint32_t)p.n_goal_valid, p.thr_goal, P + b0, P + b0 + bl, sh.pos);
+        if (ragent)
+          scan_accepted(p, st, rgoal ? w1 : 0, (uint32_t)p.n_agent_valid, p.thr_agent, P + b0, P + b0 + bl,
+                        rgoal ? sh.pos2 : sh.pos);
+      }
+      __syncthreads();
+    }
+    for (uint32_t q = b0 + threadIdx.x; q < b0 + bl; q += TPB) {
+      int kt = 0;
+      while (sh.tpre[kt + 1] <= q) ++kt;  // my tile holding flattened resetter q (T is small)
+      const int k = t0 + kt;
+      const uint32_t local = q - sh.tpre[kt];
+      const int env = k * EPB + (reset_all ? (int)local : (int)p.tlist[(size_t)k * EPB + local]);
+      const uint32_t j = P + q;
+      int goal = p.fixed_goal, agent = p.fixed_agent;
+      if (rgoal) {
+        const uint32_t w = slow ? sh.pos[q - b0] : j;
+        goal = p.goal_valid[lemire_value(word_at(p, st, w), (uint32_t)p.n_goal_valid)];
+      } else if (goal < 0) {
+        goal = 0;
+      }
+      if (ragent) {
+        const uint32_t w = slow ? (rgoal ? sh.pos2[q - b0] : sh.pos[q - b0]) : (rgoal ? btot : 0u) + j;
+        agent = p.agent_valid[lemire_value(word_at(p, st, w), (uint32_t)p.n_agent_valid)];
+      }
+      if (rgoal) p.goal[env] = (uint16_t)goal;
+      p.ae[env] = (uint32_t)agent;  // elapsed = 0
+      write_obs<OK>(p, env, agent, goal, obs);
+    }
+    __syncthreads();
+  }
+  // the last block has seen every flag: publish the next RNG state
+  if (blockIdx.x == gridDim.x - 1) {
+    uint32_t wtot = 0;
+    if (btot && ncalls) {
+      if (!slow) {
+        wtot = (uint32_t)ncalls * btot;
+      } else {
+        if (threadIdx.x < 64) {
+          uint32_t a = ncalls == 2 ? w1 : 0u;
+          const bool last_goal = ncalls == 1 && rgoal;
+          a = scan_accepted(p, st, a, last_goal ? (uint32_t)p.n_goal_valid : (uint32_t)p.n_agent_valid,
+                            last_goal ? p.thr_goal : p.thr_agent, btot - 1, btot, nullptr);
+          if (threadIdx.x == 0) sh.bcast = a;
+        }
+        __syncthreads();
+        wtot = sh.bcast;
+      }
+    }
+    if (threadIdx.x == 0) {
+      uint32_t used, h, u = st.u0;
+      if (wtot == 0) {
+        used = 0; h = st.h0;
+      } else if (st.h0) {
+        used = wtot >> 1;          // ceil((wtot-1)/2)
+        h = (wtot - 1) & 1;
+      } else {
+        used = (wtot + 1) >> 1;    // ceil(wtot/2)
+        h = wtot & 1;
+      }
+      const u128 s = pcg_jump(p.jt, st.s0, st.U0 + used);
+      // numpy keeps the last buffered half in `uinteger` even after it has been consumed
+      if (used) u = (uint32_t)(pcg_output(s) >> 32);
+      C->s_hi = hi64(s);
+      C->s_lo = lo64(s);
+      C->has_u32 = h;
+      C->uinteger = u;
+      C->b_total = btot;
+      C->epoch = epoch + 1u;
+    }
   }
 }
 
@@ -845,15 +699,6 @@ __global__ __launch_bounds__(TPB) void grid_reset_init(GridDev p) {
   if (env >= p.B) return;
   p.ae[env] = p.fixed_agent >= 0 ? (uint32_t)p.fixed_agent : 0u;
   if (p.fixed_goal < 0) p.goal[env] = 0;
-}
-
-template <int OK>
-__global__ __launch_bounds__(TPB) void grid_obs_all(GridDev p, void* __restrict__ obs) {
-  const int env = blockIdx.x * TPB + threadIdx.x;
-  if (env >= p.B) return;
-  const int agent = (int)(p.ae[env] & 0xFFFF);
-  const int goal = p.fixed_goal < 0 ? (int)p.goal[env] : p.fixed_goal;
-  write_obs<OK>(p, env, agent, goal, obs);
 }
 
 // ------------------------------------------------------------------ kernels: counter modes ----
@@ -1004,7 +849,7 @@ struct GridBackend : EnvBackend {
   std::vector<int32_t> cells;
   std::vector<uint16_t> goal_valid_h, agent_valid_h;
   DevBuf b_move, b_thr, b_gv, b_av, b_hbase, b_doff, b_hvec, b_t1, b_t2, b_coords, b_window, b_jt, b_lt4, b_lt2,
-      b_tja, b_tjw, b_ae, b_goal, b_ctl, b_status, b_mslot;
+      b_tja, b_tjw, b_ae, b_goal, b_ctl, b_tcount, b_tlist, b_rflag, b_mslot;
   // replay pointers for the next step
   const uint64_t* rp_u = nullptr;
   const int32_t* rp_goal = nullptr;
@@ -1061,16 +906,16 @@ struct GridBackend : EnvBackend {
 };
 
 int GridBackend::upload_rng() {
-  GridCtlBlock h;
-  GP_HIP_CHECK(hipMemcpy(&h, d.ctl, sizeof(h), hipMemcpyDeviceToHost));
-  GridCtl& c = h.rec[h.parity];
+  GP_HIP_CHECK(hipDeviceSynchronize());
+  GridCtl c;
+  GP_HIP_CHECK(hipMemcpy(&c, d.ctl, sizeof(c), hipMemcpyDeviceToHost));
   c.s_hi = hi64(rng.state);
   c.s_lo = lo64(rng.state);
   c.inc_hi = hi64(rng.inc);
   c.inc_lo = lo64(rng.inc);
   c.has_u32 = rng.has_u32;
   c.uinteger = rng.uinteger;
-  GP_HIP_CHECK(hipMemcpy(d.ctl, &h, sizeof(h), hipMemcpyHostToDevice));
+  GP_HIP_CHECK(hipMemcpy(d.ctl, &c, sizeof(c), hipMemcpyHostToDevice));
   std::vector<PcgJump> jt = build_jump_tables(rng.inc);
   GP_HIP_CHECK(hipMemcpy(b_jt.p, jt.data(), jt.size() * sizeof(PcgJump), hipMemcpyHostToDevice));
   std::vector<PcgJump> l4(TPB), l2(TPB);
@@ -1101,15 +946,14 @@ int GridBackend::upload_rng() {
 
 int GridBackend::get_rng_state(RngHost* r) {
   GP_HIP_CHECK(hipDeviceSynchronize());
-  GridCtlBlock h;
-  GP_HIP_CHECK(hipMemcpy(&h, d.ctl, sizeof(h), hipMemcpyDeviceToHost));
-  const GridCtl& c = h.rec[h.parity];
+  GridCtl c;
+  GP_HIP_CHECK(hipMemcpy(&c, d.ctl, sizeof(c), hipMemcpyDeviceToHost));
   r->state = mk128(c.s_hi, c.s_lo);
   r->inc = mk128(c.inc_hi, c.inc_lo);
   r->has_u32 = c.has_u32;
   r->uinteger = c.uinteger;
-  if (h.err) {
-    gp_set_error("device error flags 0x%x (lookback spin timeout)", h.err);
+  if (c.err) {
+    gp_set_error("device error flags 0x%x (spin timeout)", c.err);
     return GP_E_HIP;
   }
   return GP_OK;
@@ -1151,17 +995,7 @@ int GridBackend::reset(void* obs, hipStream_t s) {
     constexpr int OK = decltype(okc)::value;
     if (rng_mode == GP_RNG_NUMPY) {
       hipLaunchKernelGGL(grid_reset_init, dim3(g1), dim3(TPB), 0, s, d);
-      if (rgoal) {
-        int fl = PF_CALL_GOAL | (ragent ? 0 : (PF_FINAL | PF_OBS_RESET));
-        hipLaunchKernelGGL(grid_choice_numpy<OK>, dim3(gp), dim3(TPB), 0, s, d, (const uint8_t*)nullptr,
-                           (const uint8_t*)nullptr, obs, fl, 0, 0u, 0, 0u);
-      }
-      if (ragent) {
-        int fl = PF_FINAL | PF_OBS_RESET;
-        hipLaunchKernelGGL(grid_choice_numpy<OK>, dim3(gp), dim3(TPB), 0, s, d, (const uint8_t*)nullptr,
-                           (const uint8_t*)nullptr, obs, fl, rgoal ? 1 : 0, 0u, rgoal ? 1 : 0, 0u);
-      }
-      if (!rgoal && !ragent) hipLaunchKernelGGL(grid_obs_all<OK>, dim3(g1), dim3(TPB), 0, s, d, obs);
+      hipLaunchKernelGGL(grid_resolve_numpy<OK>, dim3(gp), dim3(TPB), 0, s, d, obs, RM_RESET, 0u);
     } else if (rng_mode == GP_RNG_PHILOX) {
       hipLaunchKernelGGL((grid_reset_counter<OK, false>), dim3(g1), dim3(TPB), 0, s, d, philox_step, obs);
       ++philox_step;
@@ -1192,22 +1026,13 @@ int GridBackend::step(const void* act, void* obs, float* rew, uint8_t* term, uin
   int e = dispatch_obs(d.obs_kind, [&](auto okc) -> int {
     constexpr int OK = decltype(okc)::value;
     if (rng_mode == GP_RNG_NUMPY) {
-      if (rgoal && ragent) {
-        timer.begin(s);
-        hipLaunchKernelGGL(grid_step_numpy<OK>, dim3(gp), dim3(TPB), 0, s, d, (const int32_t*)act, obs, rew, term,
-                           trunc, PF_FUSED_CALL | PF_CALL_GOAL);
-        timer.end(s);
-        hipLaunchKernelGGL(grid_choice_numpy<OK>, dim3(gp), dim3(TPB), 0, s, d, term, trunc, obs,
-                           PF_STEP | PF_FINAL | PF_OBS_RESET, 1, 0u, 1, (uint32_t)B);
-      } else {
-        int fl = PF_FINAL | PF_OBS_RESET;
-        if (rgoal) fl |= PF_FUSED_CALL | PF_CALL_GOAL;
-        if (ragent) fl |= PF_FUSED_CALL;
-        timer.begin(s);
-        hipLaunchKernelGGL(grid_step_numpy<OK>, dim3(gp), dim3(TPB), 0, s, d, (const int32_t*)act, obs, rew, term,
-                           trunc, fl);
-        timer.end(s);
-      }
+      timer.begin(s);
+      hipLaunchKernelGGL(grid_step_numpy<OK>, dim3(d.nblk), dim3(TPB), 0, s, d, (const int32_t*)act, obs, rew, term,
+                         trunc);
+      timer.end(s);
+      timer2.begin(s);
+      hipLaunchKernelGGL(grid_resolve_numpy<OK>, dim3(gp), dim3(TPB), 0, s, d, obs, 0, (uint32_t)B);
+      timer2.end(s);
     } else if (rng_mode == GP_RNG_PHILOX) {
       timer.begin(s);
       hipLaunchKernelGGL((grid_rollout_counter<OK, false>), dim3(d.nblk), dim3(TPB), 0, s, d, 1, philox_step,
@@ -1466,26 +1291,23 @@ int GridBackend::build(const gp_grid_config* cfg) {
       (e = b_hvec.upload(hvec)) || (e = b_coords.upload(coords)) || (e = b_window.upload(window)) ||
       (e = b_t1.upload(t1)) || (e = b_t2.upload(t2)))
     return e;
-  // persistent grid for the lookback kernels: every block must be resident (see scan_and_lookback)
+  // K2 grid: at most one block per CU (all resident: blocks wait on lower-index blocks' flags)
   {
-    int occ = 0;
-    GP_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, grid_step_numpy<GP_OBS_HANSEN>, TPB, 0));
-    int occ2 = 0;
-    GP_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ2, grid_choice_numpy<GP_OBS_WINDOW>, TPB, 0));
-    occ = std::min(occ, occ2);
     hipDeviceProp_t prop;
     GP_HIP_CHECK(hipGetDeviceProperties(&prop, device));
-    // VGPR-limited (114-120 VGPRs -> 4 waves/SIMD); the SGPR bound (106 -> 6 blocks/CU) is looser,
-    // so the API's answer is exact here (MI355X_MICROARCH.md, Residency). Capped at 4 blocks/CU.
-    const int bpc = std::max(1, std::min(4, occ));
-    grid_persist = std::max(1, std::min(d.nblk, prop.multiProcessorCount * bpc));
+    grid_persist = std::max(1, std::min({d.nblk, prop.multiProcessorCount, 256}));
+    if ((d.nblk + grid_persist - 1) / grid_persist > MAX_TPB2) {
+      gp_set_error("num_envs too large for the resolver (max %d)", 256 * MAX_TPB2 * EPB);
+      return GP_E_INVALID;
+    }
   }
   nslots = std::max(d.nblk, grid_persist);
   if ((e = b_jt.alloc(sizeof(PcgJump) * JT_LEVELS * JT_RADIX)) || (e = b_lt4.alloc(sizeof(PcgJump) * TPB)) ||
       (e = b_lt2.alloc(sizeof(PcgJump) * TPB)) || (e = b_tja.alloc(sizeof(PcgJump) * (size_t)d.nblk)) ||
       (e = b_tjw.alloc(sizeof(PcgJump) * (size_t)d.nblk)) || (e = b_ae.alloc(sizeof(uint32_t) * (B + 4))) ||
-      (e = b_goal.alloc(sizeof(uint16_t) * (B + 8))) || (e = b_ctl.alloc(sizeof(GridCtlBlock))) ||
-      (e = b_status.alloc(sizeof(uint64_t) * 4 * (size_t)d.nblk)) ||
+      (e = b_goal.alloc(sizeof(uint16_t) * (B + 8))) || (e = b_ctl.alloc(sizeof(GridCtl))) ||
+      (e = b_tcount.alloc(sizeof(uint32_t) * (size_t)d.nblk)) ||
+      (e = b_tlist.alloc(sizeof(uint16_t) * (size_t)d.nblk * EPB)) || (e = b_rflag.alloc(sizeof(uint32_t) * 256)) ||
       (e = b_mslot.alloc(sizeof(MetricSlot) * (size_t)nslots)))
     return e;
   d.move = b_move.as<uint16_t>();
@@ -1507,8 +1329,10 @@ int GridBackend::build(const gp_grid_config* cfg) {
   d.mslot = b_mslot.as<MetricSlot>();
   d.ae = b_ae.as<uint32_t>();
   d.goal = b_goal.as<uint16_t>();
-  d.ctl = b_ctl.as<GridCtlBlock>();
-  d.status = b_status.as<uint64_t>();
+  d.ctl = b_ctl.as<GridCtl>();
+  d.tcount = b_tcount.as<uint32_t>();
+  d.tlist = b_tlist.as<uint16_t>();
+  d.rflag = b_rflag.as<uint32_t>();
   // default seed: numpy's SeedSequence(0) until the caller seeds
   rng = pcg64_from_seed({0u}, {});
   return upload_rng();

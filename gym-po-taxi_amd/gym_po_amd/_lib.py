@@ -82,6 +82,8 @@ SIGNATURES = {
     "gp_taxi_reset_distribution": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
     "gp_set_profiling": (ctypes.c_int, [_vp, ctypes.c_int]),
     "gp_profile_read": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]),
+    "gp_profile_read_resolver": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double),
+                                                 ctypes.POINTER(ctypes.c_int64)]),
     "gp_pcg64_seed_state": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32), ctypes.c_int,
                                            ctypes.POINTER(ctypes.c_uint32), ctypes.c_int,
                                            ctypes.POINTER(ctypes.c_uint64)]),

@@ -225,5 +225,12 @@ class NativeVecEnv:
         check(lib().gp_profile_read(self._handle, ctypes.byref(ms), ctypes.byref(n)), "gp_profile_read")
         return ms.value, n.value
 
+    def profile_read_resolver(self):
+        """(summed reset-resolver-kernel ms, launches) since the last read (syncs; numpy mode)."""
+        ms, n = ctypes.c_double(), ctypes.c_int64()
+        check(lib().gp_profile_read_resolver(self._handle, ctypes.byref(ms), ctypes.byref(n)),
+              "gp_profile_read_resolver")
+        return ms.value, n.value
+
     def render(self):
         raise NotImplementedError("rendering is out of scope (SURVEY.md §2)")

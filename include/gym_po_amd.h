@@ -196,6 +196,8 @@ int gp_taxi_reset_distribution(const gp_env* env, double* out, int cap);
  * the last read (then clears). Used by bench.py for the live roofline measurement. */
 int gp_set_profiling(gp_env* env, int enable);
 int gp_profile_read(gp_env* env, double* total_ms, int64_t* n_launches);
+/* Same for the numpy-mode reset resolver kernel that follows each step kernel. */
+int gp_profile_read_resolver(gp_env* env, double* total_ms, int64_t* n_launches);
 
 /* ---- host-only helpers (no device needed) ---- */
 /* PCG64 state {state_hi, state_lo, inc_hi, inc_lo, has_uint32, uinteger} that numpy's
