@@ -19,6 +19,7 @@
 //   GP_RNG_REPLAY pre-decided per-env draws (parity harness for the Philox path).
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -40,6 +41,7 @@ struct alignas(64) GridCtl {
   uint32_t epoch;                       // K2 launches so far (tags the per-block flags)
   uint32_t err;                         // bit0: spin timeout
   uint32_t b_total;                     // resets resolved by the last K2 (diagnostic)
+  uint32_t step;                        // numpy-mode steps taken (fused-kernel granule tags)
 };
 
 // Per-block metric accumulators (each persistent block owns one slot: no atomics).
@@ -82,6 +84,12 @@ struct GridDev {
   uint32_t* tcount;  // [nblk] resets per tile (K1 -> K2)
   uint16_t* tlist;   // [nblk*EPB] local offsets of a tile's resetting envs, ascending
   uint32_t* rflag;   // [<=256] K2 per-block rejection flags, tagged with the epoch
+  // fused numpy rollout
+  int32_t fnt;              // 4096-env tiles
+  const PcgJump* ftj;       // [fnt] jump by tau*FEPB + 1
+  const PcgJump* flt4;      // [FTPB] jump by 4t
+  const PcgJump* fjB;       // [1] jump by B
+  uint64_t* fslot;          // [2][3][fnt] tagged granules
   // philox / replay
   uint32_t key0, key1;
   const uint64_t* rp_u;
@@ -701,6 +709,453 @@ __global__ __launch_bounds__(TPB) void grid_reset_init(GridDev p) {
   if (p.fixed_goal < 0) p.goal[env] = 0;
 }
 
+// ------------------------------------------------------------------ kernel: fused numpy rollout ----
+// K numpy-exact steps in ONE persistent launch. Block b (1024 threads, 4 envs each) owns the
+// 4096-env tiles tau = q*G + b (q < QPT); their state lives in registers for the whole launch.
+// Per step t:
+//   1. every env draws its action-failure u64 (stream position e+1 from the step's s0) and
+//      transitions; rewards/flags and the obs of non-resetting envs are stored at once.
+//   2. each tile publishes one tagged 8-B granule {tag, Lemire-rejection bit, reset count}; the
+//      rejection bit covers a speculative window of RCOV word positions per tile.
+//   3. every block all-gathers the nt granules (the only inter-block exchange): prefix of the
+//      reset counts (ranks of this block's resetters), total b, any rejection.
+//   4. resetters draw choice() words at positions rank (+b for the agent call) — extra check
+//      rounds extend the rejection coverage when b exceeds it (mass resets) or for the second
+//      call; a rejection anywhere switches to the exact stream walk (p ~ 1e-8 per word).
+//   5. every block derives the next step's PCG64 state from (s0, B, b) by itself.
+// Granule tags = (global step + 1) * 4 + round, so a granule from an earlier step or launch
+// never matches; slots alternate by step parity (a block publishes step t+2 only after every
+// block has published step t+1, i.e. finished reading step t's slots).
+constexpr int FTPB = 1024;
+constexpr int FEPB = FTPB * EPT;  // 4096 envs per fused tile
+constexpr int RCOV = 64;          // speculative rejection-check words per tile per step
+constexpr int FMAXG = 256;
+constexpr int FMAXT = 1024;       // max tiles (4M envs) for the fused path
+
+struct FusedShared {
+  uint32_t wsum_lo[FTPB / 64], wsum_hi[FTPB / 64];
+  uint32_t red[FTPB / 64], red2[FTPB / 64];
+  uint32_t tpre[FMAXT];             // exclusive prefix of the tile counts (all tiles)
+  uint32_t tcnt[4], trej[4];
+  uint32_t btot, anyrej, w1, wtot, slow;
+  uint64_t ns_hi, ns_lo;
+  uint32_t nh, nu;
+  uint32_t pos[FEPB];
+  uint32_t pos2[FEPB];
+};
+
+__device__ __forceinline__ uint64_t gran(uint32_t tag, uint32_t rej, uint32_t count) {
+  return ((uint64_t)tag << 32) | ((uint64_t)(rej & 1u) << 31) | (uint64_t)count;
+}
+
+// Publish-and-gather round: tile-owner threads have stored their granules; every thread
+// tid < nt polls granule tid until its tag matches, then the block reduces. Returns the
+// gathered (count, rej) of tile `tid` (0 for tid >= nt).
+__device__ __forceinline__ uint64_t gather_granule(const GridDev& p, const uint64_t* slots, int nt, uint32_t tag) {
+  uint64_t g = 0;
+  if ((int)threadIdx.x < nt) {
+    g = __hip_atomic_load(&slots[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t spins = 0;
+    while ((uint32_t)(g >> 32) != tag) {
+      __builtin_amdgcn_s_sleep(1);
+      g = __hip_atomic_load(&slots[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (++spins > SPIN_LIMIT) {
+        atomicOr(&p.ctl->err, 1u);
+        g = gran(tag, 0, 0);
+        break;
+      }
+    }
+  }
+  return g;
+}
+
+template <class T>
+__device__ __forceinline__ T fblock_sum(T v, uint32_t* red) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = (uint32_t)v;
+  __syncthreads();
+  T s = 0;
+#pragma unroll
+  for (int w = 0; w < FTPB / 64; ++w) s += (T)red[w];
+  return s;
+}
+
+// Lemire check of `cnt` consecutive words from `w0` (one thread).
+__device__ __forceinline__ uint32_t check_words(const GridDev& p, const Stream& st, uint32_t w0, uint32_t cnt,
+                                                uint32_t n, uint32_t thr) {
+  if (!cnt) return 0;
+  WordIter it;
+  it.init(p, st, w0);
+  uint32_t r = 0;
+  for (uint32_t i = 0; i < cnt; ++i) r |= lemire_rejected(it.next(st), n, thr) ? 1u : 0u;
+  return r;
+}
+
+// An extra coverage round: tile tau checks words [base + tau*R, base + (tau+1)*R) (R =
+// ceil(total / nt)); returns whether any word in [base, base + total) is rejected.
+__device__ uint32_t coverage_round(const GridDev& p, const Stream& st, uint64_t* slots, int nt, int G, int QPT,
+                                   uint32_t tag, uint32_t base, uint32_t total, uint32_t n, uint32_t thr,
+                                   FusedShared& sh) {
+  const uint32_t R = (total + nt - 1) / nt;
+  const uint32_t per = (R + 63) / 64;  // words per checking lane (64 lanes per tile)
+  for (int q = 0; q < QPT; ++q) {
+    const int tau = q * G + (int)blockIdx.x;
+    uint32_t r = 0;
+    if (tau < nt && (int)threadIdx.x >= q * 64 && (int)threadIdx.x < (q + 1) * 64) {
+      const uint32_t l = threadIdx.x - q * 64;
+      const uint32_t lo = tau * R + l * per, hi = min(min(lo + per, (uint32_t)(tau + 1) * R), total);
+      if (lo < hi) r = check_words(p, st, base + lo, hi - lo, n, thr);
+    }
+    const uint32_t any = __syncthreads_or((int)r) ? 1u : 0u;
+    if (threadIdx.x == 0 && tau < nt)
+      __hip_atomic_store(&slots[tau], gran(tag, any, 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  const uint64_t g = gather_granule(p, slots, nt, tag);
+  return __syncthreads_or((int)((g >> 31) & 1u)) ? 1u : 0u;
+}
+
+template <int OK, int QPT>
+__global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p, int K, const int32_t* __restrict__ act,
+                                                           void* __restrict__ obs, float* __restrict__ rew,
+                                                           uint8_t* __restrict__ term, uint8_t* __restrict__ trunc) {
+  __shared__ FusedShared sh;
+  __shared__ uint64_t s_thr[64];
+  if (threadIdx.x < p.nact * p.nact) s_thr[threadIdx.x] = p.thr[threadIdx.x];
+  GridCtl* C = p.ctl;
+  const int G = (int)gridDim.x;
+  const int nt = p.fnt;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const bool rgoal = p.fixed_goal < 0, ragent = p.fixed_agent < 0;
+  const int ncalls = (int)rgoal + (int)ragent;
+  const uint32_t n1 = rgoal ? (uint32_t)p.n_goal_valid : (uint32_t)p.n_agent_valid;
+  const uint32_t thr1 = rgoal ? p.thr_goal : p.thr_agent;
+  Stream st;
+  st.s0 = mk128(C->s_hi, C->s_lo);
+  st.inc = mk128(C->inc_hi, C->inc_lo);
+  st.h0 = C->has_u32;
+  st.u0 = C->uinteger;
+  st.U0 = (uint32_t)p.B;
+  const uint32_t step_base = C->step;
+  const size_t ow = (size_t)p.obs_width * ((OK == GP_OBS_HANSEN_VEC || OK == GP_OBS_WINDOW) ? 1 : 4);
+  // env state in registers
+  uint32_t ae[QPT][4];
+  int gl[QPT][4];
+#pragma unroll
+  for (int q = 0; q < QPT; ++q) {
+    const int env0 = (q * G + (int)blockIdx.x) * FEPB + tid * EPT;
+    load4<uint32_t>(p.ae, env0, p.B, ae[q]);
+    if (rgoal) {
+      uint16_t gg[4];
+      load4<uint16_t>(p.goal, env0, p.B, gg);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) gl[q][i] = gg[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) gl[q][i] = p.fixed_goal;
+    }
+  }
+  int32_t a_cur[QPT][4];
+#pragma unroll
+  for (int q = 0; q < QPT; ++q) load4<int32_t>(act, (q * G + (int)blockIdx.x) * FEPB + tid * EPT, p.B, a_cur[q]);
+  float rsum = 0.f;
+  uint32_t eps = 0, lens = 0, nst = 0;
+  __syncthreads();
+
+  for (int k = 0; k < K; ++k) {
+    const uint32_t tag0 = (step_base + (uint32_t)k + 1u) * 4u;
+    uint64_t* slots = p.fslot + (size_t)((step_base + (uint32_t)k) & 1u) * 3 * nt;
+    // prefetch the next step's actions
+    int32_t a_nxt[QPT][4];
+    if (k + 1 < K) {
+#pragma unroll
+      for (int q = 0; q < QPT; ++q)
+        load4<int32_t>(act + (size_t)(k + 1) * p.B, (q * G + (int)blockIdx.x) * FEPB + tid * EPT, p.B, a_nxt[q]);
+    }
+    // speculative Lemire check of this tile's RCOV window (call 1): 16 lanes x 4 words per tile
+    uint32_t srej[QPT];
+#pragma unroll
+    for (int q = 0; q < QPT; ++q) {
+      srej[q] = 0;
+      const int tau = q * G + (int)blockIdx.x;
+      if (ncalls && tid >= q * 16 && tid < q * 16 + RCOV / 4 && tau < nt)
+        srej[q] = check_words(p, st, (uint32_t)tau * RCOV + (uint32_t)(tid - q * 16) * 4, 4, n1, thr1);
+    }
+    // 1. transitions
+    uint32_t fm[QPT];
+    uint32_t cnt[QPT];
+#pragma unroll
+    for (int q = 0; q < QPT; ++q) {
+      const int tau = q * G + (int)blockIdx.x;
+      const int env0 = tau * FEPB + tid * EPT;
+      uint64_t k4[4];
+      {
+        u128 s = apply_jump(p.flt4[tid], apply_jump(p.ftj[tau], st.s0));
+        k4[0] = pcg_output(s) >> 11;
+#pragma unroll
+        for (int i = 1; i < 4; ++i) {
+          s = pcg_step(s, st.inc);
+          k4[i] = pcg_output(s) >> 11;
+        }
+      }
+      float r[4];
+      uint8_t tm[4], tr[4];
+      int ag[4];
+      fm[q] = 0;
+      cnt[q] = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const Trans t = transition(p, ae[q][i], gl[q][i], a_cur[q][i], k4[i], s_thr);
+        const bool valid = env0 + i < p.B;
+        const bool f = valid && (t.term | t.trunc);
+        r[i] = t.rew;
+        tm[i] = t.term;
+        tr[i] = t.trunc;
+        ag[i] = f && p.fixed_agent >= 0 ? p.fixed_agent : t.agent;
+        ae[q][i] = (uint32_t)ag[i] | ((uint32_t)(f ? 0 : t.elapsed) << 16);
+        if (f && p.fixed_goal >= 0) gl[q][i] = p.fixed_goal;
+        fm[q] |= (f ? 1u : 0u) << i;
+        cnt[q] += f;
+        if (valid) {
+          rsum += t.rew;
+          nst += 1;
+          if (f) { eps += 1; lens += (uint32_t)t.elapsed; }
+        }
+      }
+      const size_t off = (size_t)k * p.B;
+      store4<float>(rew + off, env0, p.B, r);
+      store4<uint8_t>(term + off, env0, p.B, tm);
+      store4<uint8_t>(trunc + off, env0, p.B, tr);
+      void* ob = (uint8_t*)obs + off * ow;
+      if (fm[q] == 0 || ncalls == 0) {
+        write_obs4<OK>(p, env0, ag, gl[q], ob);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (!(fm[q] & (1u << i)) && env0 + i < p.B) write_obs<OK>(p, env0 + i, ag[i], gl[q][i], ob);
+      }
+    }
+    // 2. per-tile reset counts (packed 16 bits per tile) and rejection bits -> granules
+    uint64_t x = 0;
+#pragma unroll
+    for (int q = 0; q < QPT; ++q) x |= (uint64_t)cnt[q] << (16 * q);
+    const uint64_t c_self = x;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint64_t y = ((uint64_t)__shfl_up((uint32_t)(x >> 32), d, 64) << 32) | __shfl_up((uint32_t)x, d, 64);
+      if (lane >= d) x += y;
+    }
+    if (lane == 63) {
+      sh.wsum_lo[wid] = (uint32_t)x;
+      sh.wsum_hi[wid] = (uint32_t)(x >> 32);
+    }
+    uint32_t rj = 0;
+#pragma unroll
+    for (int q = 0; q < QPT; ++q) rj |= srej[q] << q;
+    const unsigned long long rm = __ballot(rj != 0);
+    if (lane == 0) sh.red[wid] = 0;
+    __syncthreads();
+    if (rm) atomicOr(&sh.red[wid], rj);  // rare
+    uint64_t woff = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < FTPB / 64; ++w) {
+      const uint64_t v = ((uint64_t)sh.wsum_hi[w] << 32) | sh.wsum_lo[w];
+      if (w < wid) woff += v;
+      tot += v;
+    }
+    const uint64_t excl_local = x - c_self + woff;  // my exclusive rank per tile (16-bit fields)
+    __syncthreads();
+    if (tid < QPT) {
+      uint32_t rr = 0;
+      for (int w = 0; w < FTPB / 64; ++w) rr |= sh.red[w];
+      const int tau = tid * G + (int)blockIdx.x;
+      if (tau < nt)
+        __hip_atomic_store(&slots[tau], gran(tag0, (rr >> tid) & 1u, (uint32_t)(tot >> (16 * tid)) & 0xFFFFu),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // 3. all-gather of the nt granules
+    {
+      const uint64_t g = gather_granule(p, slots, nt, tag0);
+      const uint32_t c = (uint32_t)g & 0x7FFFFFFFu;
+      uint32_t xi = c;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(xi, d, 64);
+        if (lane >= d) xi += y;
+      }
+      const bool wrej = __any((int)((g >> 31) & 1u));
+      if (lane == 63) {
+        sh.red[wid] = xi;
+        sh.red2[wid] = wrej ? 1u : 0u;
+      }
+      __syncthreads();
+      uint32_t wo = 0, all = 0, anyr = 0;
+#pragma unroll
+      for (int w = 0; w < FTPB / 64; ++w) {
+        if (w < wid) wo += sh.red[w];
+        all += sh.red[w];
+        anyr |= sh.red2[w];
+      }
+      if (tid < nt) sh.tpre[tid] = xi - c + wo;
+      if (tid == 0) {
+        sh.btot = all;
+        sh.anyrej = anyr;
+      }
+      __syncthreads();
+    }
+    const uint32_t b = sh.btot;
+    // 4. choice() draws for the resetters
+    uint32_t slow = sh.anyrej;
+    if (ncalls && b) {
+      if (!slow && b > (uint32_t)nt * RCOV)  // mass reset: extend call-1 coverage
+        slow = coverage_round(p, st, slots + nt, nt, G, QPT, tag0 + 1, (uint32_t)nt * RCOV, b - nt * RCOV, n1,
+                              thr1, sh);
+      if (!slow && ncalls == 2)  // agent words start right after the b goal words
+        slow = coverage_round(p, st, slots + 2 * nt, nt, G, QPT, tag0 + 2, b, b, (uint32_t)p.n_agent_valid,
+                              p.thr_agent, sh);
+      uint32_t w1 = b;
+      if (slow && ncalls == 2) {
+        if (tid < 64) {
+          const uint32_t a = scan_accepted(p, st, 0, n1, thr1, b - 1, b, nullptr);
+          if (tid == 0) sh.w1 = a;
+        }
+        __syncthreads();
+        w1 = sh.w1;
+      }
+#pragma unroll
+      for (int q = 0; q < QPT; ++q) {
+        const int tau = q * G + (int)blockIdx.x;
+        if (tau >= nt) continue;
+        const uint32_t tc = (uint32_t)(tot >> (16 * q)) & 0xFFFFu;
+        if (!tc) continue;  // block-uniform
+        const uint32_t P = sh.tpre[tau];
+        if (slow) {
+          if (tid < 64) {
+            if (rgoal) scan_accepted(p, st, 0, (uint32_t)p.n_goal_valid, p.thr_goal, P, P + tc, sh.pos);
+            if (ragent)
+              scan_accepted(p, st, rgoal ? w1 : 0, (uint32_t)p.n_agent_valid, p.thr_agent, P, P + tc,
+                            rgoal ? sh.pos2 : sh.pos);
+          }
+          __syncthreads();
+        }
+        if (fm[q]) {
+          const int env0 = tau * FEPB + tid * EPT;
+          uint32_t lr = (uint32_t)(excl_local >> (16 * q)) & 0xFFFFu;
+          void* ob = (uint8_t*)obs + (size_t)k * p.B * ow;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            if (!(fm[q] & (1u << i))) continue;
+            const uint32_t j = P + lr;
+            int goal = gl[q][i], agent = (int)(ae[q][i] & 0xFFFF);
+            if (rgoal) {
+              const uint32_t w = slow ? sh.pos[lr] : j;
+              goal = p.goal_valid[lemire_value(word_at(p, st, w), (uint32_t)p.n_goal_valid)];
+            }
+            if (ragent) {
+              const uint32_t w = slow ? (rgoal ? sh.pos2[lr] : sh.pos[lr]) : (rgoal ? w1 : 0u) + j;
+              agent = p.agent_valid[lemire_value(word_at(p, st, w), (uint32_t)p.n_agent_valid)];
+            }
+            gl[q][i] = goal;
+            ae[q][i] = (uint32_t)agent;
+            write_obs<OK>(p, env0 + i, agent, goal, ob);
+            ++lr;
+          }
+        }
+        if (slow) __syncthreads();  // sh.pos reused by the next tile
+      }
+      // words consumed this step
+      if (tid == 0) sh.wtot = slow ? 0xFFFFFFFFu : (uint32_t)ncalls * b;
+      __syncthreads();
+      if (sh.wtot == 0xFFFFFFFFu) {
+        if (tid < 64) {
+          const bool last_goal = ncalls == 1 && rgoal;
+          const uint32_t a = scan_accepted(p, st, ncalls == 2 ? w1 : 0u,
+                                           last_goal ? (uint32_t)p.n_goal_valid : (uint32_t)p.n_agent_valid,
+                                           last_goal ? p.thr_goal : p.thr_agent, b - 1, b, nullptr);
+          if (tid == 0) sh.wtot = a;
+        }
+        __syncthreads();
+      }
+    } else if (tid == 0) {
+      sh.wtot = 0;
+    }
+    // 5. next step's PCG64 state (computed identically by every block; thread 0 + broadcast)
+    if (tid == 0) {
+      const uint32_t wtot = sh.wtot;
+      uint32_t used, h, u = st.u0;
+      if (wtot == 0) {
+        used = 0; h = st.h0;
+      } else if (st.h0) {
+        used = wtot >> 1;
+        h = (wtot - 1) & 1;
+      } else {
+        used = (wtot + 1) >> 1;
+        h = wtot & 1;
+      }
+      const u128 s = pcg_jump(p.jt, apply_jump(*p.fjB, st.s0), used);
+      if (used) u = (uint32_t)(pcg_output(s) >> 32);
+      sh.ns_hi = hi64(s);
+      sh.ns_lo = lo64(s);
+      sh.nh = h;
+      sh.nu = u;
+    }
+    __syncthreads();
+    st.s0 = mk128(sh.ns_hi, sh.ns_lo);
+    st.h0 = sh.nh;
+    st.u0 = sh.nu;
+    if (k + 1 < K) {
+#pragma unroll
+      for (int q = 0; q < QPT; ++q)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a_cur[q][i] = a_nxt[q][i];
+    }
+    __syncthreads();  // sh reuse
+  }
+  // write the state back; block 0 publishes the RNG state and the step counter
+#pragma unroll
+  for (int q = 0; q < QPT; ++q) {
+    const int env0 = (q * G + (int)blockIdx.x) * FEPB + tid * EPT;
+    store4<uint32_t>(p.ae, env0, p.B, ae[q]);
+    if (rgoal) {
+      uint16_t gg[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) gg[i] = (uint16_t)gl[q][i];
+      store4<uint16_t>(p.goal, env0, p.B, gg);
+    }
+  }
+  if (blockIdx.x == 0 && tid == 0) {
+    C->s_hi = hi64(st.s0);
+    C->s_lo = lo64(st.s0);
+    C->has_u32 = st.h0;
+    C->uinteger = st.u0;
+    C->step = step_base + (uint32_t)K;
+  }
+  // metrics (1024-thread block)
+  {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+      rsum += __shfl_xor(rsum, d, 64);
+      eps += __shfl_xor(eps, d, 64);
+      lens += __shfl_xor(lens, d, 64);
+      nst += __shfl_xor(nst, d, 64);
+    }
+    __shared__ float m_r[FTPB / 64];
+    __shared__ uint32_t m_e[FTPB / 64], m_l[FTPB / 64], m_n[FTPB / 64];
+    if (lane == 0) { m_r[wid] = rsum; m_e[wid] = eps; m_l[wid] = lens; m_n[wid] = nst; }
+    __syncthreads();
+    if (tid == 0) {
+      float r = 0; uint32_t e = 0, l = 0, n = 0;
+      for (int w = 0; w < FTPB / 64; ++w) { r += m_r[w]; e += m_e[w]; l += m_l[w]; n += m_n[w]; }
+      MetricSlot& m = p.mslot[blockIdx.x];
+      m.return_sum += (double)r;
+      m.episodes += e;
+      m.length_sum += l;
+      m.env_steps += n;
+    }
+  }
+}
+
 // ------------------------------------------------------------------ kernels: counter modes ----
 // Philox: ctr = (env, step_lo, step_hi, 0x67706f21), key = seed-derived. One draw set per
 // env-step: x0,x1 -> 53-bit uniform; x2 -> goal index; x3 -> agent index (multiply-shift).
@@ -849,7 +1304,8 @@ struct GridBackend : EnvBackend {
   std::vector<int32_t> cells;
   std::vector<uint16_t> goal_valid_h, agent_valid_h;
   DevBuf b_move, b_thr, b_gv, b_av, b_hbase, b_doff, b_hvec, b_t1, b_t2, b_coords, b_window, b_jt, b_lt4, b_lt2,
-      b_tja, b_tjw, b_ae, b_goal, b_ctl, b_tcount, b_tlist, b_rflag, b_mslot;
+      b_tja, b_tjw, b_ae, b_goal, b_ctl, b_tcount, b_tlist, b_rflag, b_mslot, b_ftj, b_flt4, b_fjB, b_fslot;
+  int fused_G = 0, fused_qpt = 0;  // fused numpy rollout geometry (0 = not eligible)
   // replay pointers for the next step
   const uint64_t* rp_u = nullptr;
   const int32_t* rp_goal = nullptr;
@@ -903,6 +1359,26 @@ struct GridBackend : EnvBackend {
     return (int)v.size();
   }
   int metrics(double out[4]) override;
+  template <int OK>
+  int launch_fused(int K, const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc, hipStream_t s) {
+    timer.begin(s);
+    switch (fused_qpt) {
+      case 1:
+        hipLaunchKernelGGL((grid_rollout_numpy<OK, 1>), dim3(fused_G), dim3(FTPB), 0, s, d, K, (const int32_t*)act,
+                           obs, rew, term, trunc);
+        break;
+      case 2:
+        hipLaunchKernelGGL((grid_rollout_numpy<OK, 2>), dim3(fused_G), dim3(FTPB), 0, s, d, K, (const int32_t*)act,
+                           obs, rew, term, trunc);
+        break;
+      default:
+        hipLaunchKernelGGL((grid_rollout_numpy<OK, 4>), dim3(fused_G), dim3(FTPB), 0, s, d, K, (const int32_t*)act,
+                           obs, rew, term, trunc);
+    }
+    timer.end(s);
+    GP_HIP_CHECK(hipGetLastError());
+    return GP_OK;
+  }
 };
 
 int GridBackend::upload_rng() {
@@ -941,6 +1417,17 @@ int GridBackend::upload_rng() {
   }
   GP_HIP_CHECK(hipMemcpy(b_tja.p, ta.data(), ta.size() * sizeof(PcgJump), hipMemcpyHostToDevice));
   GP_HIP_CHECK(hipMemcpy(b_tjw.p, tw.data(), tw.size() * sizeof(PcgJump), hipMemcpyHostToDevice));
+  if (fused_G) {
+    std::vector<PcgJump> fl(FTPB), ft(d.fnt);
+    for (int t = 0; t < FTPB; ++t) fl[t] = pcg_jump_params((u128)(4 * t), rng.inc);
+    const PcgJump step_ftile = pcg_jump_params((u128)FEPB, rng.inc);
+    ft[0] = pcg_jump_params((u128)1, rng.inc);
+    for (int k = 1; k < d.fnt; ++k) ft[k] = compose(step_ftile, ft[k - 1]);
+    const PcgJump jb = pcg_jump_params((u128)B, rng.inc);
+    GP_HIP_CHECK(hipMemcpy(b_flt4.p, fl.data(), fl.size() * sizeof(PcgJump), hipMemcpyHostToDevice));
+    GP_HIP_CHECK(hipMemcpy(b_ftj.p, ft.data(), ft.size() * sizeof(PcgJump), hipMemcpyHostToDevice));
+    GP_HIP_CHECK(hipMemcpy(b_fjB.p, &jb, sizeof(PcgJump), hipMemcpyHostToDevice));
+  }
   return GP_OK;
 }
 
@@ -1026,6 +1513,7 @@ int GridBackend::step(const void* act, void* obs, float* rew, uint8_t* term, uin
   int e = dispatch_obs(d.obs_kind, [&](auto okc) -> int {
     constexpr int OK = decltype(okc)::value;
     if (rng_mode == GP_RNG_NUMPY) {
+      if (fused_G) return launch_fused<OK>(1, act, obs, rew, term, trunc, s);
       timer.begin(s);
       hipLaunchKernelGGL(grid_step_numpy<OK>, dim3(d.nblk), dim3(TPB), 0, s, d, (const int32_t*)act, obs, rew, term,
                          trunc);
@@ -1033,6 +1521,7 @@ int GridBackend::step(const void* act, void* obs, float* rew, uint8_t* term, uin
       timer2.begin(s);
       hipLaunchKernelGGL(grid_resolve_numpy<OK>, dim3(gp), dim3(TPB), 0, s, d, obs, 0, (uint32_t)B);
       timer2.end(s);
+      // keep the fused kernels' step counter meaningful for mixed use
     } else if (rng_mode == GP_RNG_PHILOX) {
       timer.begin(s);
       hipLaunchKernelGGL((grid_rollout_counter<OK, false>), dim3(d.nblk), dim3(TPB), 0, s, d, 1, philox_step,
@@ -1058,6 +1547,16 @@ int GridBackend::step(const void* act, void* obs, float* rew, uint8_t* term, uin
 
 int GridBackend::rollout(int K, const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc,
                          hipStream_t s) {
+  if (rng_mode == GP_RNG_NUMPY && fused_G) {
+    if (!has_reset) {
+      gp_set_error("rollout() before reset()");
+      return GP_E_STATE;
+    }
+    return dispatch_obs(d.obs_kind, [&](auto okc) -> int {
+      constexpr int OK = decltype(okc)::value;
+      return launch_fused<OK>(K, act, obs, rew, term, trunc, s);
+    });
+  }
   if (rng_mode != GP_RNG_PHILOX) return EnvBackend::rollout(K, act, obs, rew, term, trunc, s);
   if (!has_reset) {
     gp_set_error("rollout() before reset()");
@@ -1301,14 +1800,31 @@ int GridBackend::build(const gp_grid_config* cfg) {
       return GP_E_INVALID;
     }
   }
-  nslots = std::max(d.nblk, grid_persist);
+  // fused numpy rollout: one 1024-thread block per CU, <= 4 tiles of 4096 envs per block
+  d.fnt = (int)((B + FEPB - 1) / FEPB);
+  {
+    hipDeviceProp_t prop;
+    GP_HIP_CHECK(hipGetDeviceProperties(&prop, device));
+    int occ = 0;
+    GP_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, grid_rollout_numpy<GP_OBS_WINDOW, 4>, FTPB, 0));
+    const int G = std::min({prop.multiProcessorCount, FMAXG, d.fnt});
+    const int qpt = (d.fnt + G - 1) / G;
+    const char* off = getenv("GP_DISABLE_FUSED");  // testing knob: force the two-kernel numpy path
+    if (occ >= 1 && d.fnt <= FMAXT && qpt <= 4 && !(off && off[0] == '1')) {
+      fused_G = G;
+      fused_qpt = qpt <= 1 ? 1 : (qpt <= 2 ? 2 : 4);
+    }
+  }
+  nslots = std::max({d.nblk, grid_persist, fused_G});
   if ((e = b_jt.alloc(sizeof(PcgJump) * JT_LEVELS * JT_RADIX)) || (e = b_lt4.alloc(sizeof(PcgJump) * TPB)) ||
       (e = b_lt2.alloc(sizeof(PcgJump) * TPB)) || (e = b_tja.alloc(sizeof(PcgJump) * (size_t)d.nblk)) ||
       (e = b_tjw.alloc(sizeof(PcgJump) * (size_t)d.nblk)) || (e = b_ae.alloc(sizeof(uint32_t) * (B + 4))) ||
       (e = b_goal.alloc(sizeof(uint16_t) * (B + 8))) || (e = b_ctl.alloc(sizeof(GridCtl))) ||
       (e = b_tcount.alloc(sizeof(uint32_t) * (size_t)d.nblk)) ||
       (e = b_tlist.alloc(sizeof(uint16_t) * (size_t)d.nblk * EPB)) || (e = b_rflag.alloc(sizeof(uint32_t) * 256)) ||
-      (e = b_mslot.alloc(sizeof(MetricSlot) * (size_t)nslots)))
+      (e = b_mslot.alloc(sizeof(MetricSlot) * (size_t)nslots)) ||
+      (e = b_ftj.alloc(sizeof(PcgJump) * (size_t)std::max(d.fnt, 1))) || (e = b_flt4.alloc(sizeof(PcgJump) * FTPB)) ||
+      (e = b_fjB.alloc(sizeof(PcgJump))) || (e = b_fslot.alloc(sizeof(uint64_t) * 6 * (size_t)std::max(d.fnt, 1))))
     return e;
   d.move = b_move.as<uint16_t>();
   d.thr = b_thr.as<uint64_t>();
@@ -1333,6 +1849,10 @@ int GridBackend::build(const gp_grid_config* cfg) {
   d.tcount = b_tcount.as<uint32_t>();
   d.tlist = b_tlist.as<uint16_t>();
   d.rflag = b_rflag.as<uint32_t>();
+  d.ftj = b_ftj.as<PcgJump>();
+  d.flt4 = b_flt4.as<PcgJump>();
+  d.fjB = b_fjB.as<PcgJump>();
+  d.fslot = b_fslot.as<uint64_t>();
   // default seed: numpy's SeedSequence(0) until the caller seeds
   rng = pcg64_from_seed({0u}, {});
   return upload_rng();

@@ -289,3 +289,33 @@ def test_numpy_rollout_equals_stepwise(gpu_device):
         o2, r2, d2, t2, _ = e2.step(acts[k])
         assert torch.equal(o1[k], o2) and torch.equal(r1[k], r2) and torch.equal(t1[k], t2)
     assert e1.rng_state == e2.rng_state
+
+
+@pytest.mark.parametrize("name", ["fr_hansen_tl20", "fr_vgh_z3_randgoal", "rooms_2_goal_mdp_randgoal",
+                                  "rooms_4_grid3"])
+def test_two_kernel_numpy_path_bit_exact(name, gpu_device, monkeypatch):
+    """The non-fused numpy path (streaming step kernel + reset resolver), used above 4M envs."""
+    monkeypatch.setenv("GP_DISABLE_FUSED", "1")
+    meta, data = load_case(name)
+    env = make_env(meta)
+    acts = step_actions(meta)
+    np.testing.assert_array_equal(np_obs(reset_obs(env, meta["seed"])).astype(np.float64),
+                                  data["obs0"].astype(np.float64))
+    for t in range(meta["steps"]):
+        o, r, d, tr, _ = env.step(acts[t])
+        np.testing.assert_array_equal(np_obs(o).astype(np.float64), data["obs"][t].astype(np.float64),
+                                      err_msg=f"t={t}")
+        np.testing.assert_array_equal(tr.cpu().numpy(), data["trunc"][t])
+    assert rng_tuple(env.rng_state) == [int(x) for x in data["final_rng_state"]]
+
+
+def test_two_kernel_forced_rejection(gpu_device, monkeypatch):
+    monkeypatch.setenv("GP_DISABLE_FUSED", "1")
+    test_forced_rejection_slow_path_step(777, gpu_device)
+
+
+@pytest.mark.parametrize("B", [4096 * 256 + 5, 2_500_000])
+def test_fused_multi_tile_per_block(B, gpu_device):
+    """QPT > 1 (several 4096-env tiles per persistent block) vs the oracle, few steps."""
+    meta, _ = load_case("fr_hansen_tl20")
+    _run_vs_oracle(meta, B, 4, seed=17, action_seed=18)
