@@ -153,8 +153,9 @@ def main():
     env.set_profiling(False)
     kavg_ms = kms / max(nk, 1)
     ravg_ms = rms / max(nr, 1)
-    if args.mode == "philox":  # one fused launch = C steps; state read+written once per launch
-        bytes_per_launch = B * (ROLLOUT_BYTES_PER_ENV_STEP * C + 8)
+    steps_per_launch = prof_steps / max(nk, 1)
+    if steps_per_launch > 1.5:  # fused launch of several steps; state read+written once per launch
+        bytes_per_launch = B * (ROLLOUT_BYTES_PER_ENV_STEP * steps_per_launch + 8)
     else:
         bytes_per_launch = B * BYTES_PER_ENV_STEP
     achieved = bytes_per_launch / (kavg_ms * 1e-3) / 1e9
@@ -188,8 +189,10 @@ def main():
                    "parallelism": f"independent env shards x{world}", "steps_per_launch_call": C},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "grid_step_numpy<GP_OBS_HANSEN>" if args.mode == "numpy" else
+                     "kernel": ("grid_rollout_numpy<GP_OBS_HANSEN,1>" if steps_per_launch > 1.5 else
+                                "grid_step_numpy<GP_OBS_HANSEN>") if args.mode == "numpy" else
                                "grid_rollout_counter<GP_OBS_HANSEN,false>",
+                     "steps_per_launch": steps_per_launch,
                      "kernel_avg_us": kavg_ms * 1e3,
                      "bytes_per_launch": bytes_per_launch,
                      "kernel_launches_timed": nk,

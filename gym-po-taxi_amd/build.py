@@ -31,21 +31,24 @@ def up_to_date():
     return all(os.path.getmtime(d) <= t for d in deps())
 
 
-def build(force=False, debug=False, verbose=True):
-    if not force and up_to_date():
+def build(force=False, debug=False, verbose=True, stamps=False):
+    out = OUT.replace(".so", "_stamps.so") if stamps else OUT
+    if not force and not stamps and up_to_date():
         return OUT
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     cmd = [hipcc, f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-shared", "-O3",
-           "-Wno-unused-result", "-I", os.path.join(ROOT, "include"), "-o", OUT + ".tmp"] + sources()
+           "-Wno-unused-result", "-I", os.path.join(ROOT, "include"), "-o", out + ".tmp"] + sources()
+    if stamps:  # diagnostic build: s_memtime phase stamps in the fused kernel (never benchmarked)
+        cmd.insert(1, "-DGP_STAMPS")
     if debug:
         cmd[cmd.index("-O3")] = "-O1"
         cmd.append("-g")
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv, debug="--debug" in sys.argv)
+    build(force="--force" in sys.argv, debug="--debug" in sys.argv, stamps="--stamps" in sys.argv)

@@ -316,6 +316,14 @@ int gp_valid_cells(const gp_env* env, int which, int32_t* out, int cap) {
   return env->be->valid_cells(which, out, cap);
 }
 
+#ifdef GP_STAMPS
+// Diagnostic builds only (libgympo_amd_stamps.so): per-block per-step phase stamps of the fused kernel.
+int gp_debug_stamps(gp_env* env, unsigned long long* out, int cap) {
+  GP_REQUIRE_ENV();
+  return env->be->debug_stamps(out, cap);
+}
+#endif
+
 int gp_metrics(gp_env* env, double out[4]) {
   GP_REQUIRE_ENV();
   return env->be->metrics(out);

@@ -62,6 +62,7 @@ struct EnvBackend {
   }
   virtual int valid_cells(int which, int32_t* out, int cap) const { return 0; }
   virtual int metrics(double out[4]) = 0;
+  virtual int debug_stamps(unsigned long long* out, int cap) { return 0; }
   virtual int reset_distribution(double* out, int cap) const {
     gp_set_error("no reset distribution for this env kind");
     return GP_E_UNSUPPORTED;

@@ -90,6 +90,7 @@ struct GridDev {
   const PcgJump* flt4;      // [FTPB] jump by 4t
   const PcgJump* fjB;       // [1] jump by B
   uint64_t* fslot;          // [2][3][fnt] tagged granules
+  unsigned long long* dbg;  // GP_STAMPS diagnostic builds: [G][64][8] s_memtime stamps
   // philox / replay
   uint32_t key0, key1;
   const uint64_t* rp_u;
@@ -816,12 +817,37 @@ __device__ uint32_t coverage_round(const GridDev& p, const Stream& st, uint64_t*
   return __syncthreads_or((int)((g >> 31) & 1u)) ? 1u : 0u;
 }
 
+__device__ __forceinline__ PcgJump compose_jump(const PcgJump& j2, const PcgJump& j1) {  // j2 o j1
+  const u128 a = mk128(j2.a_hi, j2.a_lo) * mk128(j1.a_hi, j1.a_lo);
+  const u128 c = mk128(j2.a_hi, j2.a_lo) * mk128(j1.c_hi, j1.c_lo) + mk128(j2.c_hi, j2.c_lo);
+  return PcgJump{hi64(a), lo64(a), hi64(c), lo64(c)};
+}
+
+#ifdef GP_STAMPS
+#define STAMP(i)                                                                                  \
+  do {                                                                                            \
+    if (threadIdx.x == 0 && k < 64) {                                                             \
+      unsigned long long t_;                                                                      \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                   \
+      p_in.dbg[((size_t)blockIdx.x * 64 + k) * 8 + (i)] = t_;                                     \
+    }                                                                                             \
+  } while (0)
+#else
+#define STAMP(i) \
+  do {           \
+  } while (0)
+#endif
+
 template <int OK, int QPT>
-__global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p, int K, const int32_t* __restrict__ act,
+__global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, const int32_t* __restrict__ act,
                                                            void* __restrict__ obs, float* __restrict__ rew,
                                                            uint8_t* __restrict__ term, uint8_t* __restrict__ trunc) {
   __shared__ FusedShared sh;
   __shared__ uint64_t s_thr[64];
+  __shared__ PcgJump s_jt[JT_LEVELS * JT_RADIX];  // radix jump tables in LDS (resetter words, next state)
+  GridDev p = p_in;
+  for (int i = threadIdx.x; i < JT_LEVELS * JT_RADIX; i += FTPB) s_jt[i] = p_in.jt[i];
+  p.jt = s_jt;
   if (threadIdx.x < p.nact * p.nact) s_thr[threadIdx.x] = p.thr[threadIdx.x];
   GridCtl* C = p.ctl;
   const int G = (int)gridDim.x;
@@ -859,11 +885,16 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p, int K, con
   int32_t a_cur[QPT][4];
 #pragma unroll
   for (int q = 0; q < QPT; ++q) load4<int32_t>(act, (q * G + (int)blockIdx.x) * FEPB + tid * EPT, p.B, a_cur[q]);
+  // per-lane jump to the first action draw of this lane (step-invariant): (4t) o (tau*FEPB + 1)
+  PcgJump lj[QPT];
+#pragma unroll
+  for (int q = 0; q < QPT; ++q) lj[q] = compose_jump(p.flt4[tid], p.ftj[min(q * G + (int)blockIdx.x, nt - 1)]);
   float rsum = 0.f;
   uint32_t eps = 0, lens = 0, nst = 0;
   __syncthreads();
 
   for (int k = 0; k < K; ++k) {
+    STAMP(0);
     const uint32_t tag0 = (step_base + (uint32_t)k + 1u) * 4u;
     uint64_t* slots = p.fslot + (size_t)((step_base + (uint32_t)k) & 1u) * 3 * nt;
     // prefetch the next step's actions
@@ -891,7 +922,7 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p, int K, con
       const int env0 = tau * FEPB + tid * EPT;
       uint64_t k4[4];
       {
-        u128 s = apply_jump(p.flt4[tid], apply_jump(p.ftj[tau], st.s0));
+        u128 s = apply_jump(lj[q], st.s0);
         k4[0] = pcg_output(s) >> 11;
 #pragma unroll
         for (int i = 1; i < 4; ++i) {
@@ -936,6 +967,7 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p, int K, con
           if (!(fm[q] & (1u << i)) && env0 + i < p.B) write_obs<OK>(p, env0 + i, ag[i], gl[q][i], ob);
       }
     }
+    STAMP(1);
     // 2. per-tile reset counts (packed 16 bits per tile) and rejection bits -> granules
     uint64_t x = 0;
 #pragma unroll
@@ -974,6 +1006,7 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p, int K, con
         __hip_atomic_store(&slots[tau], gran(tag0, (rr >> tid) & 1u, (uint32_t)(tot >> (16 * tid)) & 0xFFFFu),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    STAMP(2);
     // 3. all-gather of the nt granules
     {
       const uint64_t g = gather_granule(p, slots, nt, tag0);
@@ -1005,6 +1038,7 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p, int K, con
       __syncthreads();
     }
     const uint32_t b = sh.btot;
+    STAMP(3);
     // 4. choice() draws for the resetters
     uint32_t slow = sh.anyrej;
     if (ncalls && b) {
@@ -1080,6 +1114,7 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p, int K, con
     } else if (tid == 0) {
       sh.wtot = 0;
     }
+    STAMP(4);
     // 5. next step's PCG64 state (computed identically by every block; thread 0 + broadcast)
     if (tid == 0) {
       const uint32_t wtot = sh.wtot;
@@ -1104,6 +1139,7 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p, int K, con
     st.s0 = mk128(sh.ns_hi, sh.ns_lo);
     st.h0 = sh.nh;
     st.u0 = sh.nu;
+    STAMP(5);
     if (k + 1 < K) {
 #pragma unroll
       for (int q = 0; q < QPT; ++q)
@@ -1304,7 +1340,7 @@ struct GridBackend : EnvBackend {
   std::vector<int32_t> cells;
   std::vector<uint16_t> goal_valid_h, agent_valid_h;
   DevBuf b_move, b_thr, b_gv, b_av, b_hbase, b_doff, b_hvec, b_t1, b_t2, b_coords, b_window, b_jt, b_lt4, b_lt2,
-      b_tja, b_tjw, b_ae, b_goal, b_ctl, b_tcount, b_tlist, b_rflag, b_mslot, b_ftj, b_flt4, b_fjB, b_fslot;
+      b_tja, b_tjw, b_ae, b_goal, b_ctl, b_tcount, b_tlist, b_rflag, b_mslot, b_ftj, b_flt4, b_fjB, b_fslot, b_dbg;
   int fused_G = 0, fused_qpt = 0;  // fused numpy rollout geometry (0 = not eligible)
   // replay pointers for the next step
   const uint64_t* rp_u = nullptr;
@@ -1359,6 +1395,14 @@ struct GridBackend : EnvBackend {
     return (int)v.size();
   }
   int metrics(double out[4]) override;
+#ifdef GP_STAMPS
+  int debug_stamps(unsigned long long* out, int cap) override {
+    GP_HIP_CHECK(hipDeviceSynchronize());
+    const int n = std::min(cap, 256 * 64 * 8);
+    GP_HIP_CHECK(hipMemcpy(out, d.dbg, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost));
+    return n;
+  }
+#endif
   template <int OK>
   int launch_fused(int K, const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc, hipStream_t s) {
     timer.begin(s);
@@ -1853,6 +1897,10 @@ int GridBackend::build(const gp_grid_config* cfg) {
   d.flt4 = b_flt4.as<PcgJump>();
   d.fjB = b_fjB.as<PcgJump>();
   d.fslot = b_fslot.as<uint64_t>();
+#ifdef GP_STAMPS
+  if ((e = b_dbg.alloc(sizeof(unsigned long long) * 256 * 64 * 8))) return e;
+  d.dbg = b_dbg.as<unsigned long long>();
+#endif
   // default seed: numpy's SeedSequence(0) until the caller seeds
   rng = pcg64_from_seed({0u}, {});
   return upload_rng();
