@@ -50,6 +50,14 @@ struct alignas(32) MetricSlot {
   unsigned long long episodes, length_sum, env_steps;
 };
 
+struct GridLdsTab {
+  int32_t off, bytes;
+};
+struct GridLds {  // where the fused kernel stages the lookup tables in dynamic LDS
+  int32_t total;
+  GridLdsTab move, hbase, hvec, t1, t2, coords, window, gv, av, doff;
+};
+
 struct GridDev {
   int32_t B, nblk;
   int32_t nact, ncells;
@@ -91,6 +99,7 @@ struct GridDev {
   const PcgJump* fjB;       // [1] jump by B
   uint64_t* fslot;          // [2][3][fnt] tagged granules
   unsigned long long* dbg;  // GP_STAMPS diagnostic builds: [G][64][8] s_memtime stamps
+  GridLds lds;
   // philox / replay
   uint32_t key0, key1;
   const uint64_t* rp_u;
@@ -712,33 +721,36 @@ __global__ __launch_bounds__(TPB) void grid_reset_init(GridDev p) {
 
 // ------------------------------------------------------------------ kernel: fused numpy rollout ----
 // K numpy-exact steps in ONE persistent launch. Block b (1024 threads, 4 envs each) owns the
-// 4096-env tiles tau = q*G + b (q < QPT); their state lives in registers for the whole launch.
-// Per step t:
-//   1. every env draws its action-failure u64 (stream position e+1 from the step's s0) and
-//      transitions; rewards/flags and the obs of non-resetting envs are stored at once.
+// 4096-env tiles tau = q*G + b (q < QPT); env state lives in registers for the whole launch.
+// Per step t (s0 = PCG64 state at the step start, B = num_envs):
+//   1. every env e draws u64 #(e) of random(B) from its lane state S_e = jump(s0, e+1) and
+//      transitions; rewards/flags and the obs of non-resetting envs are stored at once. Lookup
+//      tables live in LDS.
 //   2. each tile publishes one tagged 8-B granule {tag, Lemire-rejection bit, reset count}; the
-//      rejection bit covers a speculative window of RCOV word positions per tile.
+//      rejection bit covers a speculative window of RCOV choice() words per tile.
 //   3. every block all-gathers the nt granules (the only inter-block exchange): prefix of the
 //      reset counts (ranks of this block's resetters), total b, any rejection.
-//   4. resetters draw choice() words at positions rank (+b for the agent call) — extra check
-//      rounds extend the rejection coverage when b exceeds it (mass resets) or for the second
-//      call; a rejection anywhere switches to the exact stream walk (p ~ 1e-8 per word).
-//   5. every block derives the next step's PCG64 state from (s0, B, b) by itself.
-// Granule tags = (global step + 1) * 4 + round, so a granule from an earlier step or launch
-// never matches; slots alternate by step parity (a block publishes step t+2 only after every
-// block has published step t+1, i.e. finished reading step t's slots).
+//   4. resetters draw their choice() words (goal call, then agent call) at positions rank (+b).
+//      Extra check rounds extend the rejection coverage when b exceeds it (mass resets) or for
+//      the second call; a rejection anywhere switches to the exact stream walk (p ~ 1e-8/word).
+//   5. s0' = jump(s0, B + used(b)); every lane state advances by the same two affine jumps
+//      (J_B, then J_used), so the next step's draws need no per-lane table lookups.
+// Granule tags = (global step + 1) * 4 + round: a granule from an earlier step or launch never
+// matches; slots alternate by step parity (a block publishes step t+2 only after every block
+// has published step t+1, i.e. finished reading step t's slots).
 constexpr int FTPB = 1024;
 constexpr int FEPB = FTPB * EPT;  // 4096 envs per fused tile
-constexpr int RCOV = 64;          // speculative rejection-check words per tile per step
+constexpr int RCOV = 64;          // speculative rejection-check words per tile per step (33 u64 lanes)
 constexpr int FMAXG = 256;
 constexpr int FMAXT = 1024;       // max tiles (4M envs) for the fused path
+constexpr int LDS_TABLE_BUDGET = 96 * 1024;
 
 struct FusedShared {
-  uint32_t wsum_lo[FTPB / 64], wsum_hi[FTPB / 64];
+  uint32_t wsum_lo[FTPB / 64], wsum_hi[FTPB / 64], wrej[FTPB / 64];
   uint32_t red[FTPB / 64], red2[FTPB / 64];
   uint32_t tpre[FMAXT];             // exclusive prefix of the tile counts (all tiles)
-  uint32_t tcnt[4], trej[4];
   uint32_t btot, anyrej, w1, wtot, slow;
+  PcgJump ju;                       // this step's J_used
   uint64_t ns_hi, ns_lo;
   uint32_t nh, nu;
   uint32_t pos[FEPB];
@@ -749,9 +761,7 @@ __device__ __forceinline__ uint64_t gran(uint32_t tag, uint32_t rej, uint32_t co
   return ((uint64_t)tag << 32) | ((uint64_t)(rej & 1u) << 31) | (uint64_t)count;
 }
 
-// Publish-and-gather round: tile-owner threads have stored their granules; every thread
-// tid < nt polls granule tid until its tag matches, then the block reduces. Returns the
-// gathered (count, rej) of tile `tid` (0 for tid >= nt).
+// Every thread tid < nt polls granule tid until its tag matches. Returns it (0 for tid >= nt).
 __device__ __forceinline__ uint64_t gather_granule(const GridDev& p, const uint64_t* slots, int nt, uint32_t tag) {
   uint64_t g = 0;
   if ((int)threadIdx.x < nt) {
@@ -770,19 +780,6 @@ __device__ __forceinline__ uint64_t gather_granule(const GridDev& p, const uint6
   return g;
 }
 
-template <class T>
-__device__ __forceinline__ T fblock_sum(T v, uint32_t* red) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-  __syncthreads();
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = (uint32_t)v;
-  __syncthreads();
-  T s = 0;
-#pragma unroll
-  for (int w = 0; w < FTPB / 64; ++w) s += (T)red[w];
-  return s;
-}
-
 // Lemire check of `cnt` consecutive words from `w0` (one thread).
 __device__ __forceinline__ uint32_t check_words(const GridDev& p, const Stream& st, uint32_t w0, uint32_t cnt,
                                                 uint32_t n, uint32_t thr) {
@@ -797,8 +794,7 @@ __device__ __forceinline__ uint32_t check_words(const GridDev& p, const Stream& 
 // An extra coverage round: tile tau checks words [base + tau*R, base + (tau+1)*R) (R =
 // ceil(total / nt)); returns whether any word in [base, base + total) is rejected.
 __device__ uint32_t coverage_round(const GridDev& p, const Stream& st, uint64_t* slots, int nt, int G, int QPT,
-                                   uint32_t tag, uint32_t base, uint32_t total, uint32_t n, uint32_t thr,
-                                   FusedShared& sh) {
+                                   uint32_t tag, uint32_t base, uint32_t total, uint32_t n, uint32_t thr) {
   const uint32_t R = (total + nt - 1) / nt;
   const uint32_t per = (R + 63) / 64;  // words per checking lane (64 lanes per tile)
   for (int q = 0; q < QPT; ++q) {
@@ -823,6 +819,17 @@ __device__ __forceinline__ PcgJump compose_jump(const PcgJump& j2, const PcgJump
   return PcgJump{hi64(a), lo64(a), hi64(c), lo64(c)};
 }
 
+// Jump parameters for n steps from the radix tables (composition of <= JT_LEVELS entries).
+__device__ __forceinline__ PcgJump jump_params(const PcgJump* jt, uint32_t n) {
+  PcgJump j{0, 1, 0, 0};
+#pragma unroll
+  for (int L = 0; L < JT_LEVELS; ++L) {
+    const uint32_t d = (n >> (JT_RADIX_BITS * L)) & (JT_RADIX - 1);
+    if (d) j = compose_jump(jt[L * JT_RADIX + d], j);
+  }
+  return j;
+}
+
 #ifdef GP_STAMPS
 #define STAMP(i)                                                                                  \
   do {                                                                                            \
@@ -838,17 +845,39 @@ __device__ __forceinline__ PcgJump compose_jump(const PcgJump& j2, const PcgJump
   } while (0)
 #endif
 
+template <class T>
+__device__ __forceinline__ const T* lds_copy(char* dyn, const GridLdsTab& t, const T* src) {
+  if (t.bytes <= 0 || src == nullptr) return src;
+  const uint4* s = reinterpret_cast<const uint4*>(src);
+  uint4* d = reinterpret_cast<uint4*>(dyn + t.off);
+  for (int i = threadIdx.x; i < (t.bytes + 15) / 16; i += blockDim.x) d[i] = s[i];
+  return reinterpret_cast<const T*>(dyn + t.off);
+}
+
 template <int OK, int QPT>
 __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, const int32_t* __restrict__ act,
                                                            void* __restrict__ obs, float* __restrict__ rew,
                                                            uint8_t* __restrict__ term, uint8_t* __restrict__ trunc) {
   __shared__ FusedShared sh;
   __shared__ uint64_t s_thr[64];
-  __shared__ PcgJump s_jt[JT_LEVELS * JT_RADIX];  // radix jump tables in LDS (resetter words, next state)
+  __shared__ PcgJump s_jt[JT_LEVELS * JT_RADIX];
+  extern __shared__ __attribute__((aligned(16))) char dyn[];
   GridDev p = p_in;
   for (int i = threadIdx.x; i < JT_LEVELS * JT_RADIX; i += FTPB) s_jt[i] = p_in.jt[i];
   p.jt = s_jt;
   if (threadIdx.x < p.nact * p.nact) s_thr[threadIdx.x] = p.thr[threadIdx.x];
+  if (p.lds.total > 0) {
+    p.move = lds_copy(dyn, p.lds.move, p_in.move);
+    p.hbase = lds_copy(dyn, p.lds.hbase, p_in.hbase);
+    p.hvec = lds_copy(dyn, p.lds.hvec, p_in.hvec);
+    p.t1 = lds_copy(dyn, p.lds.t1, p_in.t1);
+    p.t2 = lds_copy(dyn, p.lds.t2, p_in.t2);
+    p.coords = lds_copy(dyn, p.lds.coords, p_in.coords);
+    p.window = lds_copy(dyn, p.lds.window, p_in.window);
+    p.goal_valid = lds_copy(dyn, p.lds.gv, p_in.goal_valid);
+    p.agent_valid = lds_copy(dyn, p.lds.av, p_in.agent_valid);
+    p.doff = lds_copy(dyn, p.lds.doff, p_in.doff);
+  }
   GridCtl* C = p.ctl;
   const int G = (int)gridDim.x;
   const int nt = p.fnt;
@@ -864,13 +893,17 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
   st.u0 = C->uinteger;
   st.U0 = (uint32_t)p.B;
   const uint32_t step_base = C->step;
+  const PcgJump jB = *p.fjB;
   const size_t ow = (size_t)p.obs_width * ((OK == GP_OBS_HANSEN_VEC || OK == GP_OBS_WINDOW) ? 1 : 4);
   // env state in registers
   uint32_t ae[QPT][4];
   int gl[QPT][4];
+  int32_t a_cur[QPT][4];
+  u128 S[QPT];  // lane draw state: jump(s0, e0 + 1)
 #pragma unroll
   for (int q = 0; q < QPT; ++q) {
-    const int env0 = (q * G + (int)blockIdx.x) * FEPB + tid * EPT;
+    const int tau = q * G + (int)blockIdx.x;
+    const int env0 = tau * FEPB + tid * EPT;
     load4<uint32_t>(p.ae, env0, p.B, ae[q]);
     if (rgoal) {
       uint16_t gg[4];
@@ -881,14 +914,16 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
 #pragma unroll
       for (int i = 0; i < 4; ++i) gl[q][i] = p.fixed_goal;
     }
+    load4<int32_t>(act, env0, p.B, a_cur[q]);
+    S[q] = apply_jump(compose_jump(p.flt4[tid], p.ftj[min(tau, nt - 1)]), st.s0);
   }
-  int32_t a_cur[QPT][4];
-#pragma unroll
-  for (int q = 0; q < QPT; ++q) load4<int32_t>(act, (q * G + (int)blockIdx.x) * FEPB + tid * EPT, p.B, a_cur[q]);
-  // per-lane jump to the first action draw of this lane (step-invariant): (4t) o (tau*FEPB + 1)
-  PcgJump lj[QPT];
-#pragma unroll
-  for (int q = 0; q < QPT; ++q) lj[q] = compose_jump(p.flt4[tid], p.ftj[min(q * G + (int)blockIdx.x, nt - 1)]);
+  // speculative-check lane state: wave q checks tile q*G+b; lane l holds u64 #(tau*32 - 1 + l)
+  // of the post-random(B) stream, i.e. jump(s0, B + tau*32 + l)
+  const int cq = wid;  // which of my tiles this wave checks (if wid < QPT)
+  const int ctau = cq * G + (int)blockIdx.x;
+  const bool checker = ncalls && wid < QPT && lane <= 32 && ctau < nt;
+  u128 CS = 0;
+  if (checker) CS = pcg_jump(p.jt, st.s0, (uint32_t)p.B + (uint32_t)ctau * (RCOV / 2) + (uint32_t)lane);
   float rsum = 0.f;
   uint32_t eps = 0, lens = 0, nst = 0;
   __syncthreads();
@@ -897,21 +932,26 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
     STAMP(0);
     const uint32_t tag0 = (step_base + (uint32_t)k + 1u) * 4u;
     uint64_t* slots = p.fslot + (size_t)((step_base + (uint32_t)k) & 1u) * 3 * nt;
-    // prefetch the next step's actions
     int32_t a_nxt[QPT][4];
     if (k + 1 < K) {
 #pragma unroll
       for (int q = 0; q < QPT; ++q)
         load4<int32_t>(act + (size_t)(k + 1) * p.B, (q * G + (int)blockIdx.x) * FEPB + tid * EPT, p.B, a_nxt[q]);
     }
-    // speculative Lemire check of this tile's RCOV window (call 1): 16 lanes x 4 words per tile
-    uint32_t srej[QPT];
-#pragma unroll
-    for (int q = 0; q < QPT; ++q) {
-      srej[q] = 0;
-      const int tau = q * G + (int)blockIdx.x;
-      if (ncalls && tid >= q * 16 && tid < q * 16 + RCOV / 4 && tau < nt)
-        srej[q] = check_words(p, st, (uint32_t)tau * RCOV + (uint32_t)(tid - q * 16) * 4, 4, n1, thr1);
+    // speculative Lemire check of this tile's RCOV-word window (call 1)
+    uint32_t crej = 0;
+    if (checker) {
+      const uint64_t x = pcg_output(CS);
+      const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+      if (!st.h0) {
+        if (lane >= 1) crej = (lemire_rejected(lo, n1, thr1) || lemire_rejected(hi, n1, thr1)) ? 1u : 0u;
+      } else if (lane == 0) {
+        crej = lemire_rejected(ctau == 0 ? st.u0 : hi, n1, thr1) ? 1u : 0u;
+      } else if (lane < 32) {
+        crej = (lemire_rejected(lo, n1, thr1) || lemire_rejected(hi, n1, thr1)) ? 1u : 0u;
+      } else {
+        crej = lemire_rejected(lo, n1, thr1) ? 1u : 0u;
+      }
     }
     // 1. transitions
     uint32_t fm[QPT];
@@ -922,7 +962,7 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
       const int env0 = tau * FEPB + tid * EPT;
       uint64_t k4[4];
       {
-        u128 s = apply_jump(lj[q], st.s0);
+        u128 s = S[q];
         k4[0] = pcg_output(s) >> 11;
 #pragma unroll
         for (int i = 1; i < 4; ++i) {
@@ -966,9 +1006,11 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
         for (int i = 0; i < 4; ++i)
           if (!(fm[q] & (1u << i)) && env0 + i < p.B) write_obs<OK>(p, env0 + i, ag[i], gl[q][i], ob);
       }
+      S[q] = apply_jump(jB, S[q]);  // half of the advance to the next step (J_B), off the critical path
     }
+    if (checker) CS = apply_jump(jB, CS);
     STAMP(1);
-    // 2. per-tile reset counts (packed 16 bits per tile) and rejection bits -> granules
+    // 2. per-tile reset counts (packed 16 bits per tile) -> granules
     uint64_t x = 0;
 #pragma unroll
     for (int q = 0; q < QPT; ++q) x |= (uint64_t)cnt[q] << (16 * q);
@@ -978,17 +1020,13 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
       const uint64_t y = ((uint64_t)__shfl_up((uint32_t)(x >> 32), d, 64) << 32) | __shfl_up((uint32_t)x, d, 64);
       if (lane >= d) x += y;
     }
+    const bool wrj = __any((int)crej);
     if (lane == 63) {
       sh.wsum_lo[wid] = (uint32_t)x;
       sh.wsum_hi[wid] = (uint32_t)(x >> 32);
     }
-    uint32_t rj = 0;
-#pragma unroll
-    for (int q = 0; q < QPT; ++q) rj |= srej[q] << q;
-    const unsigned long long rm = __ballot(rj != 0);
-    if (lane == 0) sh.red[wid] = 0;
+    if (lane == 0) sh.wrej[wid] = wrj ? 1u : 0u;
     __syncthreads();
-    if (rm) atomicOr(&sh.red[wid], rj);  // rare
     uint64_t woff = 0, tot = 0;
 #pragma unroll
     for (int w = 0; w < FTPB / 64; ++w) {
@@ -997,13 +1035,10 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
       tot += v;
     }
     const uint64_t excl_local = x - c_self + woff;  // my exclusive rank per tile (16-bit fields)
-    __syncthreads();
     if (tid < QPT) {
-      uint32_t rr = 0;
-      for (int w = 0; w < FTPB / 64; ++w) rr |= sh.red[w];
       const int tau = tid * G + (int)blockIdx.x;
       if (tau < nt)
-        __hip_atomic_store(&slots[tau], gran(tag0, (rr >> tid) & 1u, (uint32_t)(tot >> (16 * tid)) & 0xFFFFu),
+        __hip_atomic_store(&slots[tau], gran(tag0, sh.wrej[tid], (uint32_t)(tot >> (16 * tid)) & 0xFFFFu),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     STAMP(2);
@@ -1035,19 +1070,38 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
         sh.btot = all;
         sh.anyrej = anyr;
       }
+      // fast path (no rejection, full coverage, single call): J_used known right away
+      if (tid == 0 && !anyr && (ncalls == 0 || (ncalls == 1 && all <= (uint32_t)nt * RCOV))) {
+        const uint32_t wtot = (uint32_t)ncalls * all;
+        uint32_t used, h, u = st.u0;
+        if (wtot == 0) {
+          used = 0; h = st.h0;
+        } else if (st.h0) {
+          used = wtot >> 1; h = (wtot - 1) & 1;
+        } else {
+          used = (wtot + 1) >> 1; h = wtot & 1;
+        }
+        sh.ju = jump_params(p.jt, used);
+        sh.nh = h;
+        sh.nu = used ? 0xFFFFFFFFu : u;  // resolved after the jump (needs the new state's output)
+        sh.wtot = wtot;
+      } else if (tid == 0) {
+        sh.wtot = 0xFFFFFFFEu;  // not yet known
+      }
       __syncthreads();
     }
     const uint32_t b = sh.btot;
     STAMP(3);
     // 4. choice() draws for the resetters
     uint32_t slow = sh.anyrej;
+    const u128 SB = apply_jump(jB, st.s0);  // state after random(B): base of the word stream
     if (ncalls && b) {
       if (!slow && b > (uint32_t)nt * RCOV)  // mass reset: extend call-1 coverage
         slow = coverage_round(p, st, slots + nt, nt, G, QPT, tag0 + 1, (uint32_t)nt * RCOV, b - nt * RCOV, n1,
-                              thr1, sh);
+                              thr1);
       if (!slow && ncalls == 2)  // agent words start right after the b goal words
         slow = coverage_round(p, st, slots + 2 * nt, nt, G, QPT, tag0 + 2, b, b, (uint32_t)p.n_agent_valid,
-                              p.thr_agent, sh);
+                              p.thr_agent);
       uint32_t w1 = b;
       if (slow && ncalls == 2) {
         if (tid < 64) {
@@ -1098,54 +1152,50 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
         }
         if (slow) __syncthreads();  // sh.pos reused by the next tile
       }
-      // words consumed this step
-      if (tid == 0) sh.wtot = slow ? 0xFFFFFFFFu : (uint32_t)ncalls * b;
-      __syncthreads();
-      if (sh.wtot == 0xFFFFFFFFu) {
-        if (tid < 64) {
-          const bool last_goal = ncalls == 1 && rgoal;
-          const uint32_t a = scan_accepted(p, st, ncalls == 2 ? w1 : 0u,
-                                           last_goal ? (uint32_t)p.n_goal_valid : (uint32_t)p.n_agent_valid,
-                                           last_goal ? p.thr_goal : p.thr_agent, b - 1, b, nullptr);
-          if (tid == 0) sh.wtot = a;
-        }
+      if (sh.wtot == 0xFFFFFFFEu) {  // block-uniform: the slow / multi-call / extended cases
         __syncthreads();
+        if (tid < 64) {
+          uint32_t wtot;
+          if (!slow) {
+            wtot = (uint32_t)ncalls * b;
+          } else {
+            const bool last_goal = ncalls == 1 && rgoal;
+            wtot = scan_accepted(p, st, ncalls == 2 ? w1 : 0u,
+                                 last_goal ? (uint32_t)p.n_goal_valid : (uint32_t)p.n_agent_valid,
+                                 last_goal ? p.thr_goal : p.thr_agent, b - 1, b, nullptr);
+          }
+          if (tid == 0) {
+            uint32_t used, h, u = st.u0;
+            if (st.h0) {
+              used = wtot >> 1; h = (wtot - 1) & 1;
+            } else {
+              used = (wtot + 1) >> 1; h = wtot & 1;
+            }
+            sh.ju = jump_params(p.jt, used);
+            sh.nh = h;
+            sh.nu = used ? 0xFFFFFFFFu : u;
+            sh.wtot = wtot;
+          }
+        }
       }
-    } else if (tid == 0) {
-      sh.wtot = 0;
     }
     STAMP(4);
-    // 5. next step's PCG64 state (computed identically by every block; thread 0 + broadcast)
-    if (tid == 0) {
-      const uint32_t wtot = sh.wtot;
-      uint32_t used, h, u = st.u0;
-      if (wtot == 0) {
-        used = 0; h = st.h0;
-      } else if (st.h0) {
-        used = wtot >> 1;
-        h = (wtot - 1) & 1;
-      } else {
-        used = (wtot + 1) >> 1;
-        h = wtot & 1;
-      }
-      const u128 s = pcg_jump(p.jt, apply_jump(*p.fjB, st.s0), used);
-      if (used) u = (uint32_t)(pcg_output(s) >> 32);
-      sh.ns_hi = hi64(s);
-      sh.ns_lo = lo64(s);
-      sh.nh = h;
-      sh.nu = u;
-    }
     __syncthreads();
-    st.s0 = mk128(sh.ns_hi, sh.ns_lo);
+    // 5. advance: s0' = J_used(J_B(s0)); lanes apply J_used (J_B was applied in phase 1)
+    const PcgJump ju = sh.ju;
+    st.s0 = apply_jump(ju, SB);
     st.h0 = sh.nh;
-    st.u0 = sh.nu;
-    STAMP(5);
+    st.u0 = sh.nu == 0xFFFFFFFFu ? (uint32_t)(pcg_output(st.s0) >> 32) : sh.nu;
+#pragma unroll
+    for (int q = 0; q < QPT; ++q) S[q] = apply_jump(ju, S[q]);
+    if (checker) CS = apply_jump(ju, CS);
     if (k + 1 < K) {
 #pragma unroll
       for (int q = 0; q < QPT; ++q)
 #pragma unroll
         for (int i = 0; i < 4; ++i) a_cur[q][i] = a_nxt[q][i];
     }
+    STAMP(5);
     __syncthreads();  // sh reuse
   }
   // write the state back; block 0 publishes the RNG state and the step counter
@@ -1408,15 +1458,18 @@ struct GridBackend : EnvBackend {
     timer.begin(s);
     switch (fused_qpt) {
       case 1:
-        hipLaunchKernelGGL((grid_rollout_numpy<OK, 1>), dim3(fused_G), dim3(FTPB), 0, s, d, K, (const int32_t*)act,
+        hipLaunchKernelGGL((grid_rollout_numpy<OK, 1>), dim3(fused_G), dim3(FTPB), d.lds.total, s, d, K,
+                           (const int32_t*)act,
                            obs, rew, term, trunc);
         break;
       case 2:
-        hipLaunchKernelGGL((grid_rollout_numpy<OK, 2>), dim3(fused_G), dim3(FTPB), 0, s, d, K, (const int32_t*)act,
+        hipLaunchKernelGGL((grid_rollout_numpy<OK, 2>), dim3(fused_G), dim3(FTPB), d.lds.total, s, d, K,
+                           (const int32_t*)act,
                            obs, rew, term, trunc);
         break;
       default:
-        hipLaunchKernelGGL((grid_rollout_numpy<OK, 4>), dim3(fused_G), dim3(FTPB), 0, s, d, K, (const int32_t*)act,
+        hipLaunchKernelGGL((grid_rollout_numpy<OK, 4>), dim3(fused_G), dim3(FTPB), d.lds.total, s, d, K,
+                           (const int32_t*)act,
                            obs, rew, term, trunc);
     }
     timer.end(s);
@@ -1844,13 +1897,35 @@ int GridBackend::build(const gp_grid_config* cfg) {
       return GP_E_INVALID;
     }
   }
+  // LDS staging of the lookup tables for the fused kernel (when they fit)
+  {
+    int off = 0;
+    auto put = [&](GridLdsTab& t, size_t bytes) {
+      t.off = off;
+      t.bytes = (int)bytes;
+      off += (int)((bytes + 15) / 16 * 16);
+    };
+    const int k = cfg->obs_kind;
+    put(d.lds.move, (size_t)nc * nact * sizeof(uint16_t));
+    put(d.lds.hbase, k == GP_OBS_HANSEN ? (size_t)nc * sizeof(uint32_t) : 0);
+    put(d.lds.hvec, k == GP_OBS_HANSEN_VEC ? hvec.size() : 0);
+    put(d.lds.t1, t1.size() * sizeof(int32_t));
+    put(d.lds.t2, t2.size() * sizeof(int32_t));
+    put(d.lds.coords, (k == GP_OBS_COORDS || k == GP_OBS_WINDOW) ? coords.size() * sizeof(int16_t) : 0);
+    put(d.lds.window, window.size());
+    put(d.lds.gv, goal_valid_h.size() * sizeof(uint16_t));
+    put(d.lds.av, agent_valid_h.size() * sizeof(uint16_t));
+    put(d.lds.doff, doff.size() * sizeof(int32_t));
+    d.lds.total = off <= LDS_TABLE_BUDGET ? off : 0;
+  }
   // fused numpy rollout: one 1024-thread block per CU, <= 4 tiles of 4096 envs per block
   d.fnt = (int)((B + FEPB - 1) / FEPB);
   {
     hipDeviceProp_t prop;
     GP_HIP_CHECK(hipGetDeviceProperties(&prop, device));
     int occ = 0;
-    GP_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, grid_rollout_numpy<GP_OBS_WINDOW, 4>, FTPB, 0));
+    GP_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, grid_rollout_numpy<GP_OBS_WINDOW, 4>, FTPB,
+                                                             d.lds.total));
     const int G = std::min({prop.multiProcessorCount, FMAXG, d.fnt});
     const int qpt = (d.fnt + G - 1) / G;
     const char* off = getenv("GP_DISABLE_FUSED");  // testing knob: force the two-kernel numpy path
