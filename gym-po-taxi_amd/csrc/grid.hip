@@ -155,47 +155,82 @@ __device__ __forceinline__ void store4(T* __restrict__ p, int env0, int B, const
   }
 }
 
+// ------------------------------------------------------------------ lookup-table access ----
+// GTabs reads the tables from global memory (L1/L2 hot); LTabs from the fused kernel's LDS copy.
+struct GTabs {
+  const GridDev& p;
+  __device__ __forceinline__ uint16_t move(int i) const { return p.move[i]; }
+  __device__ __forceinline__ uint32_t hbase(int i) const { return p.hbase[i]; }
+  __device__ __forceinline__ int32_t doff(int i) const { return p.doff[i]; }
+  __device__ __forceinline__ uint8_t hvec(int i) const { return p.hvec[i]; }
+  __device__ __forceinline__ int32_t t1(int i) const { return p.t1[i]; }
+  __device__ __forceinline__ int32_t t2(int i) const { return p.t2[i]; }
+  __device__ __forceinline__ bool has_t2() const { return p.t2 != nullptr; }
+  __device__ __forceinline__ int16_t coords(int i) const { return p.coords[i]; }
+  __device__ __forceinline__ uint8_t window(int i) const { return p.window[i]; }
+  __device__ __forceinline__ uint16_t gv(int i) const { return p.goal_valid[i]; }
+  __device__ __forceinline__ uint16_t av(int i) const { return p.agent_valid[i]; }
+};
+struct LTabs {
+  const GridDev& p;
+  const char* dyn;
+  template <class T>
+  __device__ __forceinline__ T at(const GridLdsTab& t, int i) const {
+    return reinterpret_cast<const T*>(dyn + t.off)[i];
+  }
+  __device__ __forceinline__ uint16_t move(int i) const { return at<uint16_t>(p.lds.move, i); }
+  __device__ __forceinline__ uint32_t hbase(int i) const { return at<uint32_t>(p.lds.hbase, i); }
+  __device__ __forceinline__ int32_t doff(int i) const { return at<int32_t>(p.lds.doff, i); }
+  __device__ __forceinline__ uint8_t hvec(int i) const { return at<uint8_t>(p.lds.hvec, i); }
+  __device__ __forceinline__ int32_t t1(int i) const { return at<int32_t>(p.lds.t1, i); }
+  __device__ __forceinline__ int32_t t2(int i) const { return at<int32_t>(p.lds.t2, i); }
+  __device__ __forceinline__ bool has_t2() const { return p.lds.t2.bytes > 0; }
+  __device__ __forceinline__ int16_t coords(int i) const { return at<int16_t>(p.lds.coords, i); }
+  __device__ __forceinline__ uint8_t window(int i) const { return at<uint8_t>(p.lds.window, i); }
+  __device__ __forceinline__ uint16_t gv(int i) const { return at<uint16_t>(p.lds.gv, i); }
+  __device__ __forceinline__ uint16_t av(int i) const { return at<uint16_t>(p.lds.av, i); }
+};
+
 // ------------------------------------------------------------------ observation builders ----
 // GP_OBS_HANSEN:     hbase[agent] * goal_mult (msrooms.py:162-189 ternary / observations.py:44-71 binary)
 // GP_OBS_HANSEN_VEC: hvec[agent][i], goal -> goal_code    (msrooms.py:131-159 / observations.py:106-131)
 // GP_OBS_TABLE:      t1[agent] + t2[goal]                 (mdp / room scalars: rooms.py:23-48, msrooms.py:217-235)
 // GP_OBS_COORDS:     (z,)y,x of agent (+ goal)            (vector mdp: rooms.py:31-37, msrooms.py:218-224)
 // GP_OBS_WINDOW:     n x n window, goal -> 2              (observations.py:74-103)
-template <int OK>
-__device__ __forceinline__ void write_obs(const GridDev& p, int env, int agent, int goal, void* __restrict__ obs) {
+template <int OK, class TB>
+__device__ __forceinline__ void write_obs(const GridDev& p, const TB& tb, int env, int agent, int goal,
+                                          void* __restrict__ obs) {
   const bool gvalid = (unsigned)goal < (unsigned)p.ncells;
   if constexpr (OK == GP_OBS_HANSEN) {
     int mult = 1;
     if (gvalid) {
       int diff = goal - agent;
       for (int i = p.obs_dirs - 1; i >= 0; --i)
-        if (diff == p.doff[i]) mult = i + 1;
+        if (diff == tb.doff(i)) mult = i + 1;
     }
-    ((int32_t*)obs)[env] = (int32_t)p.hbase[agent] * mult;
+    ((int32_t*)obs)[env] = (int32_t)tb.hbase(agent) * mult;
   } else if constexpr (OK == GP_OBS_HANSEN_VEC) {
     uint8_t* o = (uint8_t*)obs + (size_t)env * p.obs_width;
     int diff = goal - agent;
     for (int i = 0; i < p.obs_dirs; ++i) {
-      uint8_t v = p.hvec[agent * p.obs_dirs + i];
-      if (p.obs_goal && gvalid && diff == p.doff[i]) v = (uint8_t)p.goal_code;
+      uint8_t v = tb.hvec(agent * p.obs_dirs + i);
+      if (p.obs_goal && gvalid && diff == tb.doff(i)) v = (uint8_t)p.goal_code;
       o[i] = v;
     }
   } else if constexpr (OK == GP_OBS_TABLE) {
-    int32_t v = p.t1[agent];
-    if (p.t2) v += p.t2[goal];
+    int32_t v = tb.t1(agent);
+    if (tb.has_t2()) v += tb.t2(goal);
     ((int32_t*)obs)[env] = v;
   } else if constexpr (OK == GP_OBS_COORDS) {
     int32_t* o = (int32_t*)obs + (size_t)env * p.obs_width;
-    const int16_t* ca = p.coords + agent * 3;
     int k = 0;
-    if (p.ndim == 3) o[k++] = ca[0];
-    o[k++] = ca[1];
-    o[k++] = ca[2];
+    if (p.ndim == 3) o[k++] = tb.coords(agent * 3);
+    o[k++] = tb.coords(agent * 3 + 1);
+    o[k++] = tb.coords(agent * 3 + 2);
     if (p.obs_goal) {
       int gz, gy, gx;
       if (gvalid) {
-        const int16_t* cg = p.coords + goal * 3;
-        gz = cg[0]; gy = cg[1]; gx = cg[2];
+        gz = tb.coords(goal * 3); gy = tb.coords(goal * 3 + 1); gx = tb.coords(goal * 3 + 2);
       } else {
         gz = p.goal_gz; gy = p.goal_gy; gx = p.goal_gx;
       }
@@ -206,20 +241,19 @@ __device__ __forceinline__ void write_obs(const GridDev& p, int env, int agent, 
   } else {  // GP_OBS_WINDOW
     const int n = p.obs_n, nn = n * n, h = n / 2;
     uint8_t* o = (uint8_t*)obs + (size_t)env * nn;
-    const uint8_t* w = p.window + (size_t)agent * nn;
-    for (int k = 0; k < nn; ++k) o[k] = w[k];
+    for (int k = 0; k < nn; ++k) o[k] = tb.window(agent * nn + k);
     if (gvalid) {
-      const int16_t* ca = p.coords + agent * 3;
-      const int16_t* cg = p.coords + goal * 3;
-      int dy = cg[1] - ca[1], dx = cg[2] - ca[2];
-      if (cg[0] == ca[0] && dy >= -h && dy <= n - 1 - h && dx >= -h && dx <= n - 1 - h) o[(dy + h) * n + (dx + h)] = 2;
+      const int az = tb.coords(agent * 3), ay = tb.coords(agent * 3 + 1), ax = tb.coords(agent * 3 + 2);
+      const int gz = tb.coords(goal * 3), gy = tb.coords(goal * 3 + 1), gx = tb.coords(goal * 3 + 2);
+      int dy = gy - ay, dx = gx - ax;
+      if (gz == az && dy >= -h && dy <= n - 1 - h && dx >= -h && dx <= n - 1 - h) o[(dy + h) * n + (dx + h)] = 2;
     }
   }
 }
 
-template <int OK>
-__device__ __forceinline__ void write_obs4(const GridDev& p, int env0, const int (&agent)[4], const int (&goal)[4],
-                                           void* __restrict__ obs) {
+template <int OK, class TB>
+__device__ __forceinline__ void write_obs4(const GridDev& p, const TB& tb, int env0, const int (&agent)[4],
+                                           const int (&goal)[4], void* __restrict__ obs) {
   if constexpr (OK == GP_OBS_HANSEN || OK == GP_OBS_TABLE) {
     int32_t v[4];
 #pragma unroll
@@ -230,18 +264,18 @@ __device__ __forceinline__ void write_obs4(const GridDev& p, int env0, const int
         if ((unsigned)g < (unsigned)p.ncells) {
           int diff = g - a;
           for (int d = p.obs_dirs - 1; d >= 0; --d)
-            if (diff == p.doff[d]) mult = d + 1;
+            if (diff == tb.doff(d)) mult = d + 1;
         }
-        v[i] = (int32_t)p.hbase[a] * mult;
+        v[i] = (int32_t)tb.hbase(a) * mult;
       } else {
-        v[i] = p.t1[a] + (p.t2 ? p.t2[g] : 0);
+        v[i] = tb.t1(a) + (tb.has_t2() ? tb.t2(g) : 0);
       }
     }
     store4<int32_t>((int32_t*)obs, env0, p.B, v);
   } else {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      if (env0 + i < p.B) write_obs<OK>(p, env0 + i, agent[i], goal[i], obs);
+      if (env0 + i < p.B) write_obs<OK>(p, tb, env0 + i, agent[i], goal[i], obs);
   }
 }
 
@@ -421,15 +455,16 @@ __device__ __forceinline__ uint32_t effective_action(const uint64_t* __restrict_
   return e;
 }
 
-__device__ __forceinline__ Trans transition(const GridDev& p, uint32_t ae, int goal, int a, uint64_t k53,
-                                            const uint64_t* thr) {
+template <class TB>
+__device__ __forceinline__ Trans transition(const GridDev& p, const TB& tb, uint32_t ae, int goal, int a,
+                                            uint64_t k53, const uint64_t* thr) {
   Trans t;
   const int agent = (int)(ae & 0xFFFF);
   t.elapsed = (int)(ae >> 16) + 1;
   if (a < 0) a += p.nact;               // numpy negative indexing of action_matrix[action]
   a = min(max(a, 0), p.nact - 1);       // (out-of-range actions raise in the reference; clamped here)
   const uint32_t eff = min(effective_action(thr, p.nact, a, k53), (uint32_t)p.nact - 1);
-  const uint16_t m = p.move[agent * p.nact + (int)eff];
+  const uint16_t m = tb.move(agent * p.nact + (int)eff);
   t.agent = m & 0x7FFF;
   const bool blocked = (m >> 15) != 0;
   t.goal = goal;
@@ -492,7 +527,7 @@ __global__ __launch_bounds__(TPB) void grid_step_numpy(GridDev p, const int32_t*
   uint32_t eps = 0, lens = 0, nst = 0;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const Trans t = transition(p, ae4[i], g4[i], a4[i], k4[i], s_thr);
+    const Trans t = transition(p, GTabs{p}, ae4[i], g4[i], a4[i], k4[i], s_thr);
     const bool valid = env0 + i < p.B;
     const bool f = valid && (t.term | t.trunc);
     r[i] = t.rew;
@@ -513,7 +548,7 @@ __global__ __launch_bounds__(TPB) void grid_step_numpy(GridDev p, const int32_t*
   store4<uint8_t>(term, env0, p.B, tm);
   store4<uint8_t>(trunc, env0, p.B, tr);
   store4<uint32_t>(p.ae, env0, p.B, nae);
-  write_obs4<OK>(p, env0, ag, gl, obs);
+  write_obs4<OK>(p, GTabs{p}, env0, ag, gl, obs);
   // compact this tile's resetters (ascending env order) for K2
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   uint32_t x = c;
@@ -665,7 +700,7 @@ __global__ __launch_bounds__(TPB) void grid_resolve_numpy(GridDev p, void* __res
       }
       if (rgoal) p.goal[env] = (uint16_t)goal;
       p.ae[env] = (uint32_t)agent;  // elapsed = 0
-      write_obs<OK>(p, env, agent, goal, obs);
+      write_obs<OK>(p, GTabs{p}, env, agent, goal, obs);
     }
     __syncthreads();
   }
@@ -846,12 +881,11 @@ __device__ __forceinline__ PcgJump jump_params(const PcgJump* jt, uint32_t n) {
 #endif
 
 template <class T>
-__device__ __forceinline__ const T* lds_copy(char* dyn, const GridLdsTab& t, const T* src) {
-  if (t.bytes <= 0 || src == nullptr) return src;
+__device__ __forceinline__ void lds_copy(char* dyn, const GridLdsTab& t, const T* src) {
+  if (t.bytes <= 0 || src == nullptr) return;
   const uint4* s = reinterpret_cast<const uint4*>(src);
   uint4* d = reinterpret_cast<uint4*>(dyn + t.off);
   for (int i = threadIdx.x; i < (t.bytes + 15) / 16; i += blockDim.x) d[i] = s[i];
-  return reinterpret_cast<const T*>(dyn + t.off);
 }
 
 template <int OK, int QPT>
@@ -860,24 +894,21 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
                                                            uint8_t* __restrict__ term, uint8_t* __restrict__ trunc) {
   __shared__ FusedShared sh;
   __shared__ uint64_t s_thr[64];
-  __shared__ PcgJump s_jt[JT_LEVELS * JT_RADIX];
   extern __shared__ __attribute__((aligned(16))) char dyn[];
-  GridDev p = p_in;
-  for (int i = threadIdx.x; i < JT_LEVELS * JT_RADIX; i += FTPB) s_jt[i] = p_in.jt[i];
-  p.jt = s_jt;
+  const GridDev& p = p_in;
   if (threadIdx.x < p.nact * p.nact) s_thr[threadIdx.x] = p.thr[threadIdx.x];
-  if (p.lds.total > 0) {
-    p.move = lds_copy(dyn, p.lds.move, p_in.move);
-    p.hbase = lds_copy(dyn, p.lds.hbase, p_in.hbase);
-    p.hvec = lds_copy(dyn, p.lds.hvec, p_in.hvec);
-    p.t1 = lds_copy(dyn, p.lds.t1, p_in.t1);
-    p.t2 = lds_copy(dyn, p.lds.t2, p_in.t2);
-    p.coords = lds_copy(dyn, p.lds.coords, p_in.coords);
-    p.window = lds_copy(dyn, p.lds.window, p_in.window);
-    p.goal_valid = lds_copy(dyn, p.lds.gv, p_in.goal_valid);
-    p.agent_valid = lds_copy(dyn, p.lds.av, p_in.agent_valid);
-    p.doff = lds_copy(dyn, p.lds.doff, p_in.doff);
-  }
+  // stage the lookup tables in LDS (the fused path is only taken when they fit)
+  lds_copy(dyn, p.lds.move, p.move);
+  lds_copy(dyn, p.lds.hbase, p.hbase);
+  lds_copy(dyn, p.lds.hvec, p.hvec);
+  lds_copy(dyn, p.lds.t1, p.t1);
+  lds_copy(dyn, p.lds.t2, p.t2);
+  lds_copy(dyn, p.lds.coords, p.coords);
+  lds_copy(dyn, p.lds.window, p.window);
+  lds_copy(dyn, p.lds.gv, p.goal_valid);
+  lds_copy(dyn, p.lds.av, p.agent_valid);
+  lds_copy(dyn, p.lds.doff, p.doff);
+  const LTabs tb{p_in, dyn};
   GridCtl* C = p.ctl;
   const int G = (int)gridDim.x;
   const int nt = p.fnt;
@@ -977,7 +1008,7 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
       cnt[q] = 0;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const Trans t = transition(p, ae[q][i], gl[q][i], a_cur[q][i], k4[i], s_thr);
+        const Trans t = transition(p, tb, ae[q][i], gl[q][i], a_cur[q][i], k4[i], s_thr);
         const bool valid = env0 + i < p.B;
         const bool f = valid && (t.term | t.trunc);
         r[i] = t.rew;
@@ -1000,11 +1031,11 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
       store4<uint8_t>(trunc + off, env0, p.B, tr);
       void* ob = (uint8_t*)obs + off * ow;
       if (fm[q] == 0 || ncalls == 0) {
-        write_obs4<OK>(p, env0, ag, gl[q], ob);
+        write_obs4<OK>(p, tb, env0, ag, gl[q], ob);
       } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          if (!(fm[q] & (1u << i)) && env0 + i < p.B) write_obs<OK>(p, env0 + i, ag[i], gl[q][i], ob);
+          if (!(fm[q] & (1u << i)) && env0 + i < p.B) write_obs<OK>(p, tb, env0 + i, ag[i], gl[q][i], ob);
       }
       S[q] = apply_jump(jB, S[q]);  // half of the advance to the next step (J_B), off the critical path
     }
@@ -1138,15 +1169,15 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
             int goal = gl[q][i], agent = (int)(ae[q][i] & 0xFFFF);
             if (rgoal) {
               const uint32_t w = slow ? sh.pos[lr] : j;
-              goal = p.goal_valid[lemire_value(word_at(p, st, w), (uint32_t)p.n_goal_valid)];
+              goal = tb.gv(lemire_value(word_at(p, st, w), (uint32_t)p.n_goal_valid));
             }
             if (ragent) {
               const uint32_t w = slow ? (rgoal ? sh.pos2[lr] : sh.pos[lr]) : (rgoal ? w1 : 0u) + j;
-              agent = p.agent_valid[lemire_value(word_at(p, st, w), (uint32_t)p.n_agent_valid)];
+              agent = tb.av(lemire_value(word_at(p, st, w), (uint32_t)p.n_agent_valid));
             }
             gl[q][i] = goal;
             ae[q][i] = (uint32_t)agent;
-            write_obs<OK>(p, env0 + i, agent, goal, ob);
+            write_obs<OK>(p, tb, env0 + i, agent, goal, ob);
             ++lr;
           }
         }
@@ -1258,7 +1289,7 @@ template <int OK>
 __device__ __forceinline__ void counter_env_step(const GridDev& p, const uint64_t* thr, uint32_t& ae, int& goal, int a,
                                                  uint64_t k53, uint32_t gi, uint32_t ai, float& r, uint8_t& tm,
                                                  uint8_t& tr, float& rsum, uint32_t& eps, uint32_t& lens) {
-  Trans t = transition(p, ae, goal, a, k53, thr);
+  Trans t = transition(p, GTabs{p}, ae, goal, a, k53, thr);
   int agent = t.agent, g = goal, el = t.elapsed;
   rsum += t.rew;
   if (t.term | t.trunc) {
@@ -1328,7 +1359,7 @@ __global__ __launch_bounds__(TPB) void grid_rollout_counter(GridDev p, int K, ui
     int ag[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) ag[i] = (int)(ae4[i] & 0xFFFF);
-    write_obs4<OK>(p, env0, ag, g4, (uint8_t*)obs + (size_t)k * p.B * ow);
+    write_obs4<OK>(p, GTabs{p}, env0, ag, g4, (uint8_t*)obs + (size_t)k * p.B * ow);
   }
   store4<uint32_t>(p.ae, env0, p.B, ae4);
   if (p.fixed_goal < 0) {
@@ -1357,7 +1388,7 @@ __global__ __launch_bounds__(TPB) void grid_reset_counter(GridDev p, uint64_t st
   const int a = p.fixed_agent >= 0 ? p.fixed_agent : (int)p.agent_valid[ai];
   p.ae[env] = (uint32_t)a;
   if (p.fixed_goal < 0) p.goal[env] = (uint16_t)g;
-  write_obs<OK>(p, env, a, g, obs);
+  write_obs<OK>(p, GTabs{p}, env, a, g, obs);
 }
 
 // ------------------------------------------------------------------ state access ----
@@ -1929,7 +1960,7 @@ int GridBackend::build(const gp_grid_config* cfg) {
     const int G = std::min({prop.multiProcessorCount, FMAXG, d.fnt});
     const int qpt = (d.fnt + G - 1) / G;
     const char* off = getenv("GP_DISABLE_FUSED");  // testing knob: force the two-kernel numpy path
-    if (occ >= 1 && d.fnt <= FMAXT && qpt <= 4 && !(off && off[0] == '1')) {
+    if (occ >= 1 && d.fnt <= FMAXT && qpt <= 4 && d.lds.total > 0 && !(off && off[0] == '1')) {
       fused_G = G;
       fused_qpt = qpt <= 1 ? 1 : (qpt <= 2 ? 2 : 4);
     }
