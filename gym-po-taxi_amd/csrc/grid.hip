@@ -880,6 +880,15 @@ __device__ __forceinline__ PcgJump jump_params(const PcgJump* jt, uint32_t n) {
   } while (0)
 #endif
 
+// Workgroup barrier that orders LDS only: __syncthreads() also drains every outstanding global
+// store of the wave (s_waitcnt vmcnt(0)), which would put the obs/reward store latency on the
+// fused kernel's per-step critical path. All fused-kernel barriers guard LDS (sh.*) only.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 template <class T>
 __device__ __forceinline__ void lds_copy(char* dyn, const GridLdsTab& t, const T* src) {
   if (t.bytes <= 0 || src == nullptr) return;
@@ -957,7 +966,7 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
   if (checker) CS = pcg_jump(p.jt, st.s0, (uint32_t)p.B + (uint32_t)ctau * (RCOV / 2) + (uint32_t)lane);
   float rsum = 0.f;
   uint32_t eps = 0, lens = 0, nst = 0;
-  __syncthreads();
+  lds_barrier();
 
   for (int k = 0; k < K; ++k) {
     STAMP(0);
@@ -1057,7 +1066,7 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
       sh.wsum_hi[wid] = (uint32_t)(x >> 32);
     }
     if (lane == 0) sh.wrej[wid] = wrj ? 1u : 0u;
-    __syncthreads();
+    lds_barrier();
     uint64_t woff = 0, tot = 0;
 #pragma unroll
     for (int w = 0; w < FTPB / 64; ++w) {
@@ -1088,7 +1097,7 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
         sh.red[wid] = xi;
         sh.red2[wid] = wrej ? 1u : 0u;
       }
-      __syncthreads();
+      lds_barrier();
       uint32_t wo = 0, all = 0, anyr = 0;
 #pragma unroll
       for (int w = 0; w < FTPB / 64; ++w) {
@@ -1101,8 +1110,8 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
         sh.btot = all;
         sh.anyrej = anyr;
       }
-      // fast path (no rejection, full coverage, single call): J_used known right away
-      if (tid == 0 && !anyr && (ncalls == 0 || (ncalls == 1 && all <= (uint32_t)nt * RCOV))) {
+      // fast path (no resets, or no rejection + full coverage + single call): J_used known right away
+      if (tid == 0 && (all == 0 || ncalls == 0 || (!anyr && ncalls == 1 && all <= (uint32_t)nt * RCOV))) {
         const uint32_t wtot = (uint32_t)ncalls * all;
         uint32_t used, h, u = st.u0;
         if (wtot == 0) {
@@ -1119,7 +1128,7 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
       } else if (tid == 0) {
         sh.wtot = 0xFFFFFFFEu;  // not yet known
       }
-      __syncthreads();
+      lds_barrier();
     }
     const uint32_t b = sh.btot;
     STAMP(3);
@@ -1139,7 +1148,7 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
           const uint32_t a = scan_accepted(p, st, 0, n1, thr1, b - 1, b, nullptr);
           if (tid == 0) sh.w1 = a;
         }
-        __syncthreads();
+        lds_barrier();
         w1 = sh.w1;
       }
 #pragma unroll
@@ -1156,7 +1165,7 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
               scan_accepted(p, st, rgoal ? w1 : 0, (uint32_t)p.n_agent_valid, p.thr_agent, P, P + tc,
                             rgoal ? sh.pos2 : sh.pos);
           }
-          __syncthreads();
+          lds_barrier();
         }
         if (fm[q]) {
           const int env0 = tau * FEPB + tid * EPT;
@@ -1181,10 +1190,10 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
             ++lr;
           }
         }
-        if (slow) __syncthreads();  // sh.pos reused by the next tile
+        if (slow) lds_barrier();  // sh.pos reused by the next tile
       }
       if (sh.wtot == 0xFFFFFFFEu) {  // block-uniform: the slow / multi-call / extended cases
-        __syncthreads();
+        lds_barrier();
         if (tid < 64) {
           uint32_t wtot;
           if (!slow) {
@@ -1211,7 +1220,7 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
       }
     }
     STAMP(4);
-    __syncthreads();
+    lds_barrier();
     // 5. advance: s0' = J_used(J_B(s0)); lanes apply J_used (J_B was applied in phase 1)
     const PcgJump ju = sh.ju;
     st.s0 = apply_jump(ju, SB);
@@ -1227,7 +1236,7 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
         for (int i = 0; i < 4; ++i) a_cur[q][i] = a_nxt[q][i];
     }
     STAMP(5);
-    __syncthreads();  // sh reuse
+    lds_barrier();  // sh reuse
   }
   // write the state back; block 0 publishes the RNG state and the step counter
 #pragma unroll
@@ -1260,7 +1269,7 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
     __shared__ float m_r[FTPB / 64];
     __shared__ uint32_t m_e[FTPB / 64], m_l[FTPB / 64], m_n[FTPB / 64];
     if (lane == 0) { m_r[wid] = rsum; m_e[wid] = eps; m_l[wid] = lens; m_n[wid] = nst; }
-    __syncthreads();
+    lds_barrier();
     if (tid == 0) {
       float r = 0; uint32_t e = 0, l = 0, n = 0;
       for (int w = 0; w < FTPB / 64; ++w) { r += m_r[w]; e += m_e[w]; l += m_l[w]; n += m_n[w]; }
