@@ -55,7 +55,7 @@ struct GridLdsTab {
 };
 struct GridLds {  // where the fused kernel stages the lookup tables in dynamic LDS
   int32_t total;
-  GridLdsTab move, hbase, hvec, t1, t2, coords, window, gv, av, doff;
+  GridLdsTab move, hbase, hvec, t1, t2, coords, window, gv, av, doff, jt;
 };
 
 struct GridDev {
@@ -93,13 +93,15 @@ struct GridDev {
   uint16_t* tlist;   // [nblk*EPB] local offsets of a tile's resetting envs, ascending
   uint32_t* rflag;   // [<=256] K2 per-block rejection flags, tagged with the epoch
   // fused numpy rollout
-  int32_t fnt;              // 4096-env tiles
+  int32_t fnt;              // 2048-env fused tiles
   const PcgJump* ftj;       // [fnt] jump by tau*FEPB + 1
   const PcgJump* flt4;      // [FTPB] jump by 4t
   const PcgJump* fjB;       // [1] jump by B
-  uint64_t* fslot;          // [2][3][fnt] tagged granules
+  uint64_t* fslot;          // [2][3][G] tagged block granules, then [2][fnt] tile words
   unsigned long long* dbg;  // GP_STAMPS diagnostic builds: [G][64][8] s_memtime stamps
   GridLds lds;
+  const GridDev* self;      // device copy of this struct (for out-of-line slow-path helpers)
+  int32_t diag;             // diagnostics (GP_DIAG env at build): bit0 = fused kernel skips output stores
   // philox / replay
   uint32_t key0, key1;
   const uint64_t* rp_u;
@@ -189,6 +191,7 @@ struct LTabs {
   __device__ __forceinline__ uint8_t window(int i) const { return at<uint8_t>(p.lds.window, i); }
   __device__ __forceinline__ uint16_t gv(int i) const { return at<uint16_t>(p.lds.gv, i); }
   __device__ __forceinline__ uint16_t av(int i) const { return at<uint16_t>(p.lds.av, i); }
+  __device__ __forceinline__ const PcgJump* jt() const { return reinterpret_cast<const PcgJump*>(dyn + p.lds.jt.off); }
 };
 
 // ------------------------------------------------------------------ observation builders ----
@@ -391,8 +394,9 @@ __device__ __forceinline__ T block_sum(T v, T* red) {
 // Slow path (a Lemire rejection somewhere): wave 0 walks the word stream from `wbase`,
 // recording the absolute positions of the accepted draws with rank in [jlo, jhi) into out.
 // Returns (to wave 0) the position after the last recorded draw.
-__device__ uint32_t scan_accepted(const GridDev& p, const Stream& st, uint32_t wbase, uint32_t n, uint32_t thr,
+__device__ __noinline__ uint32_t scan_accepted(const GridDev* __restrict__ gp, const Stream st, uint32_t wbase, uint32_t n, uint32_t thr,
                                   uint32_t jlo, uint32_t jhi, uint32_t* out) {
+  const GridDev& p = *gp;
   const int lane = threadIdx.x & 63;
   uint32_t acc = 0, pos = wbase, after = wbase;
   while (acc < jhi) {
@@ -661,7 +665,7 @@ __global__ __launch_bounds__(TPB) void grid_resolve_numpy(GridDev p, void* __res
   uint32_t w1 = btot;
   if (slow && ncalls == 2 && btot) {
     if (threadIdx.x < 64) {
-      const uint32_t a = scan_accepted(p, st, 0, (uint32_t)p.n_goal_valid, p.thr_goal, btot - 1, btot, nullptr);
+      const uint32_t a = scan_accepted(p.self, st, 0, (uint32_t)p.n_goal_valid, p.thr_goal, btot - 1, btot, nullptr);
       if (threadIdx.x == 0) sh.w1 = a;
     }
     __syncthreads();
@@ -673,9 +677,9 @@ __global__ __launch_bounds__(TPB) void grid_resolve_numpy(GridDev p, void* __res
     if (slow) {
       if (threadIdx.x < 64) {
         if (rgoal)
-          scan_accepted(p, st, 0, (uint32_t)p.n_goal_valid, p.thr_goal, P + b0, P + b0 + bl, sh.pos);
+          scan_accepted(p.self, st, 0, (uint32_t)p.n_goal_valid, p.thr_goal, P + b0, P + b0 + bl, sh.pos);
         if (ragent)
-          scan_accepted(p, st, rgoal ? w1 : 0, (uint32_t)p.n_agent_valid, p.thr_agent, P + b0, P + b0 + bl,
+          scan_accepted(p.self, st, rgoal ? w1 : 0, (uint32_t)p.n_agent_valid, p.thr_agent, P + b0, P + b0 + bl,
                         rgoal ? sh.pos2 : sh.pos);
       }
       __syncthreads();
@@ -714,7 +718,7 @@ __global__ __launch_bounds__(TPB) void grid_resolve_numpy(GridDev p, void* __res
         if (threadIdx.x < 64) {
           uint32_t a = ncalls == 2 ? w1 : 0u;
           const bool last_goal = ncalls == 1 && rgoal;
-          a = scan_accepted(p, st, a, last_goal ? (uint32_t)p.n_goal_valid : (uint32_t)p.n_agent_valid,
+          a = scan_accepted(p.self, st, a, last_goal ? (uint32_t)p.n_goal_valid : (uint32_t)p.n_agent_valid,
                             last_goal ? p.thr_goal : p.thr_agent, btot - 1, btot, nullptr);
           if (threadIdx.x == 0) sh.bcast = a;
         }
@@ -755,69 +759,146 @@ __global__ __launch_bounds__(TPB) void grid_reset_init(GridDev p) {
 }
 
 // ------------------------------------------------------------------ kernel: fused numpy rollout ----
-// K numpy-exact steps in ONE persistent launch. Block b (1024 threads, 4 envs each) owns the
-// 4096-env tiles tau = q*G + b (q < QPT); env state lives in registers for the whole launch.
-// Per step t (s0 = PCG64 state at the step start, B = num_envs):
-//   1. every env e draws u64 #(e) of random(B) from its lane state S_e = jump(s0, e+1) and
-//      transitions; rewards/flags and the obs of non-resetting envs are stored at once. Lookup
-//      tables live in LDS.
-//   2. each tile publishes one tagged 8-B granule {tag, Lemire-rejection bit, reset count}; the
-//      rejection bit covers a speculative window of RCOV choice() words per tile.
-//   3. every block all-gathers the nt granules (the only inter-block exchange): prefix of the
-//      reset counts (ranks of this block's resetters), total b, any rejection.
-//   4. resetters draw their choice() words (goal call, then agent call) at positions rank (+b).
-//      Extra check rounds extend the rejection coverage when b exceeds it (mass resets) or for
-//      the second call; a rejection anywhere switches to the exact stream walk (p ~ 1e-8/word).
-//   5. s0' = jump(s0, B + used(b)); every lane state advances by the same two affine jumps
-//      (J_B, then J_used), so the next step's draws need no per-lane table lookups.
-// Granule tags = (global step + 1) * 4 + round: a granule from an earlier step or launch never
-// matches; slots alternate by step parity (a block publishes step t+2 only after every block
-// has published step t+1, i.e. finished reading step t's slots).
-constexpr int FTPB = 1024;
-constexpr int FEPB = FTPB * EPT;  // 4096 envs per fused tile
-constexpr int RCOV = 64;          // speculative rejection-check words per tile per step (33 u64 lanes)
-constexpr int FMAXG = 256;
-constexpr int FMAXT = 1024;       // max tiles (4M envs) for the fused path
+// K numpy-exact steps in ONE persistent launch. Block b (512 threads = 8 waves, 4 envs per
+// thread) owns the 2048-env tiles tau = q*G + b (q < QPT); env state lives in registers for the
+// whole launch and the lookup tables in LDS. Per step (s0 = PCG64 state at the step start):
+//   1. every env e draws u64 #e of random(B) from its lane state S_e = jump(s0, e+1) and
+//      transitions (critical path: nothing else happens before the publish).
+//   2. per-wave reset counts by ballot bit-planes -> LDS -> barrier B1 -> thread 0 publishes ONE
+//      tagged 8-B granule per block {tag, Lemire-rejection bit, 12-bit reset count per tile}.
+//      The rejection bit covers a speculative window of RCOV choice() words per tile, checked
+//      by a spare wave per tile.
+//   3. wave 0 all-gathers the G block granules (4 per lane, the only inter-block exchange),
+//      scans them (DPP) into this block's tile prefixes, the total b and the rejection flag, and
+//      in the common case already derives the next state s0' = J_used(J_B(s0)). Meanwhile the
+//      other waves store rewards / flags / the obs of non-resetting envs (wave 0 stores its own
+//      after the gather, so its polling loads never wait behind its stores).
+//   4. barrier B2; resetters draw their choice() words (goal call, then agent call) at word
+//      position prefix + rank (+b). Extra check rounds extend the rejection coverage when b
+//      exceeds it (mass resets) or for the second call; a rejection anywhere switches to the
+//      exact stream walk (p ~ 1e-8/word).
+//   5. every lane state advances by J_used (J_B was applied in step 3's slack).
+// Granule tags = ((global step + 1) * 4 + round) mod 2^15; slots alternate by step parity (a
+// block publishes step t+2 only after every block has published step t+1, i.e. finished
+// reading step t's slots), so a stale granule never carries the expected tag.
+constexpr int FENVW = 8;                 // env waves per block (2 per SIMD)
+constexpr int FTPB = (FENVW + 1) * 64;   // + one control wave
+constexpr int FWAVES = FENVW + 1;
+constexpr int FEPB = FENVW * 64 * EPT;   // 2048 envs per fused tile
+constexpr int RCOV = 62;                 // speculative rejection-check words per tile per step (32 u64 lanes)
+constexpr int FMAXG = 256;        // blocks: wave 0 gathers 4 granules per lane
+constexpr int FMAXQ = 4;          // tiles per block (12-bit counts: 4 per granule)
+constexpr int FMAXT = FMAXG * FMAXQ;
 constexpr int LDS_TABLE_BUDGET = 96 * 1024;
+constexpr uint32_t TAG_MASK = 0x7FFFu;
 
 struct FusedShared {
-  uint32_t wsum_lo[FTPB / 64], wsum_hi[FTPB / 64], wrej[FTPB / 64];
-  uint32_t red[FTPB / 64], red2[FTPB / 64];
-  uint32_t tpre[FMAXT];             // exclusive prefix of the tile counts (all tiles)
-  uint32_t btot, anyrej, w1, wtot, slow;
-  PcgJump ju;                       // this step's J_used
-  uint64_t ns_hi, ns_lo;
-  uint32_t nh, nu;
-  uint32_t pos[FEPB];
+  uint32_t wcnt[FMAXQ][FENVW];   // per-env-wave reset counts of each tile
+  uint32_t wrej;                 // speculative-check rejection (control wave)
+  uint32_t tpre[FMAXQ];          // global exclusive prefix of this block's tiles
+  uint32_t btot, anyrej, known, flag, w1;
+  uint64_t ju[4];                // lane-state advance J_used o J_B (a_hi, a_lo, c_hi, c_lo)
+  uint4 thr4[16];                // action-failure thresholds >> 21 (hi 32 bits), [a][j]
+  uint64_t ns_hi, ns_lo;         // next step's s0
+  uint32_t nh, nu;               // next step's has_uint32 / uinteger
+  uint32_t pos[FEPB];            // slow path: accepted-word positions of one tile's resetters
   uint32_t pos2[FEPB];
 };
 
-__device__ __forceinline__ uint64_t gran(uint32_t tag, uint32_t rej, uint32_t count) {
-  return ((uint64_t)tag << 32) | ((uint64_t)(rej & 1u) << 31) | (uint64_t)count;
+__device__ __forceinline__ uint64_t bgran(uint32_t tag, uint32_t rej, uint64_t counts) {
+  return ((uint64_t)(tag & TAG_MASK) << 49) | ((uint64_t)(rej & 1u) << 48) | counts;
+}
+__device__ __forceinline__ uint32_t gcount(uint64_t g, int q) { return (uint32_t)(g >> (12 * q)) & 0xFFFu; }
+// Per-tile word published by the aggregator: {tag, rejection bit, b (24 bits), tile prefix (24 bits)}.
+__device__ __forceinline__ uint64_t tword(uint32_t tag, uint32_t rej, uint32_t b, uint32_t pre) {
+  return ((uint64_t)(tag & TAG_MASK) << 49) | ((uint64_t)(rej & 1u) << 48) | ((uint64_t)(b & 0xFFFFFFu) << 24) |
+         (uint64_t)(pre & 0xFFFFFFu);
 }
 
-// Every thread tid < nt polls granule tid until its tag matches. Returns it (0 for tid >= nt).
-__device__ __forceinline__ uint64_t gather_granule(const GridDev& p, const uint64_t* slots, int nt, uint32_t tag) {
-  uint64_t g = 0;
-  if ((int)threadIdx.x < nt) {
-    g = __hip_atomic_load(&slots[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    uint32_t spins = 0;
-    while ((uint32_t)(g >> 32) != tag) {
-      __builtin_amdgcn_s_sleep(1);
-      g = __hip_atomic_load(&slots[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (++spins > SPIN_LIMIT) {
-        atomicOr(&p.ctl->err, 1u);
-        g = gran(tag, 0, 0);
-        break;
-      }
-    }
+// Wave-64 inclusive prefix sum (DPP row shifts + row broadcasts).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false); // row_bcast:15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false); // row_bcast:31
+  return x;
+}
+
+// Exclusive wave prefix and wave total of a per-lane count in [0, 7] (three ballot bit-planes).
+__device__ __forceinline__ void wave_count_prefix(uint32_t c, uint32_t& excl, uint32_t& tot) {
+  const uint64_t b0 = __ballot(c & 1u), b1 = __ballot(c & 2u), b2 = __ballot(c & 4u);
+  const uint32_t lt0 = __builtin_amdgcn_mbcnt_hi((uint32_t)(b0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b0, 0u));
+  const uint32_t lt1 = __builtin_amdgcn_mbcnt_hi((uint32_t)(b1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b1, 0u));
+  const uint32_t lt2 = __builtin_amdgcn_mbcnt_hi((uint32_t)(b2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b2, 0u));
+  excl = lt0 + 2u * lt1 + 4u * lt2;
+  tot = (uint32_t)__builtin_popcountll(b0) + 2u * (uint32_t)__builtin_popcountll(b1) +
+        4u * (uint32_t)__builtin_popcountll(b2);
+}
+
+// Orders a wave's own LDS writes before its later LDS reads by other lanes (no block barrier).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+}
+
+// The choice() draws of one resetter: Lemire values of word wg (goal call, mode bit 0, n = ng)
+// and word wa (agent call, mode bit 1, n = na) -> goal index | agent index << 16. Out of line:
+// it is the only place the fused kernel needs a full jump from s0 per lane.
+__device__ __forceinline__ uint32_t draw_cells(const PcgJump* jt, u128 s0, u128 inc, uint32_t h0, uint32_t u0,
+                                            uint32_t U0, uint32_t wg, uint32_t wa, uint32_t mode, uint32_t ng,
+                                            uint32_t na) {
+  auto word = [&](uint32_t w) -> uint32_t {
+    if (h0 && w == 0) return u0;
+    const uint32_t ww = w - h0;
+    const uint64_t x = pcg_output(pcg_jump(jt, s0, U0 + (ww >> 1) + 1));
+    return (ww & 1) ? (uint32_t)(x >> 32) : (uint32_t)x;
+  };
+  uint32_t v = 0;
+  if (mode & 1u) v |= lemire_value(word(wg), ng);
+  if (mode & 2u) v |= lemire_value(word(wa), na) << 16;
+  return v;
+}
+
+// Wave 0: poll the G block granules of one round (lane l holds blocks 4l..4l+3) until every one
+// carries `tag`. Granules of blocks >= G read as 0.
+__device__ __forceinline__ void gather_blocks(const GridDev& p, const uint64_t* slots, int G, uint32_t tag,
+                                              uint64_t (&g)[4]) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t want = (uint64_t)(tag & TAG_MASK);
+  uint32_t pend = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    g[j] = 0;
+    if (lane * 4 + j < G) pend |= 1u << j;
   }
-  return g;
+  uint32_t spins = 0;
+  while (true) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (pend & (1u << j))
+        g[j] = __hip_atomic_load(&slots[lane * 4 + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if ((pend & (1u << j)) && (g[j] >> 49) == want) pend &= ~(1u << j);
+    if (!__any((int)pend)) break;
+    if (++spins > SPIN_LIMIT) {
+      if (pend) atomicOr(&p.ctl->err, 1u);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (pend & (1u << j)) g[j] = want << 49;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
 }
 
 // Lemire check of `cnt` consecutive words from `w0` (one thread).
-__device__ __forceinline__ uint32_t check_words(const GridDev& p, const Stream& st, uint32_t w0, uint32_t cnt,
+__device__ __noinline__ uint32_t check_words(const GridDev* __restrict__ gp, const Stream st, uint32_t w0, uint32_t cnt,
                                                 uint32_t n, uint32_t thr) {
+  const GridDev& p = *gp;
   if (!cnt) return 0;
   WordIter it;
   it.init(p, st, w0);
@@ -827,25 +908,37 @@ __device__ __forceinline__ uint32_t check_words(const GridDev& p, const Stream& 
 }
 
 // An extra coverage round: tile tau checks words [base + tau*R, base + (tau+1)*R) (R =
-// ceil(total / nt)); returns whether any word in [base, base + total) is rejected.
-__device__ uint32_t coverage_round(const GridDev& p, const Stream& st, uint64_t* slots, int nt, int G, int QPT,
-                                   uint32_t tag, uint32_t base, uint32_t total, uint32_t n, uint32_t thr) {
+// ceil(total / nt)) with wave q checking tile q of the block; returns whether any word in
+// [base, base + total) is rejected (grid-wide, via one more granule exchange).
+__device__ __noinline__ uint32_t coverage_round(const GridDev* __restrict__ gp, const Stream st, uint64_t* slots, int nt, int G, int QPT,
+                                   uint32_t tag, uint32_t base, uint32_t total, uint32_t n, uint32_t thr,
+                                   FusedShared& sh) {
+  const GridDev& p = *gp;
   const uint32_t R = (total + nt - 1) / nt;
   const uint32_t per = (R + 63) / 64;  // words per checking lane (64 lanes per tile)
-  for (int q = 0; q < QPT; ++q) {
-    const int tau = q * G + (int)blockIdx.x;
-    uint32_t r = 0;
-    if (tau < nt && (int)threadIdx.x >= q * 64 && (int)threadIdx.x < (q + 1) * 64) {
-      const uint32_t l = threadIdx.x - q * 64;
-      const uint32_t lo = tau * R + l * per, hi = min(min(lo + per, (uint32_t)(tau + 1) * R), total);
-      if (lo < hi) r = check_words(p, st, base + lo, hi - lo, n, thr);
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint32_t r = 0;
+  if (wid < QPT) {
+    const int tau = wid * G + (int)blockIdx.x;
+    if (tau < nt) {
+      const uint32_t lo = tau * R + lane * per, hi = min(min(lo + per, (uint32_t)(tau + 1) * R), total);
+      if (lo < hi) r = check_words(gp, st, base + lo, hi - lo, n, thr);
     }
-    const uint32_t any = __syncthreads_or((int)r) ? 1u : 0u;
-    if (threadIdx.x == 0 && tau < nt)
-      __hip_atomic_store(&slots[tau], gran(tag, any, 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  const uint64_t g = gather_granule(p, slots, nt, tag);
-  return __syncthreads_or((int)((g >> 31) & 1u)) ? 1u : 0u;
+  const uint32_t any = __syncthreads_or((int)r) ? 1u : 0u;
+  if (threadIdx.x == 0)
+    __hip_atomic_store(&slots[blockIdx.x], bgran(tag, any, 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (wid == FENVW) {  // the control wave
+    uint64_t g[4];
+    gather_blocks(p, slots, G, tag, g);
+    uint32_t rj = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) rj |= (uint32_t)(g[j] >> 48) & 1u;
+    const bool a = __any((int)rj);
+    if (lane == 0) sh.flag = a ? 1u : 0u;
+  }
+  __syncthreads();
+  return sh.flag;
 }
 
 __device__ __forceinline__ PcgJump compose_jump(const PcgJump& j2, const PcgJump& j1) {  // j2 o j1
@@ -857,24 +950,68 @@ __device__ __forceinline__ PcgJump compose_jump(const PcgJump& j2, const PcgJump
 // Jump parameters for n steps from the radix tables (composition of <= JT_LEVELS entries).
 __device__ __forceinline__ PcgJump jump_params(const PcgJump* jt, uint32_t n) {
   PcgJump j{0, 1, 0, 0};
+  bool first = true;
 #pragma unroll
   for (int L = 0; L < JT_LEVELS; ++L) {
     const uint32_t d = (n >> (JT_RADIX_BITS * L)) & (JT_RADIX - 1);
-    if (d) j = compose_jump(jt[L * JT_RADIX + d], j);
+    if (d) {
+      j = first ? jt[L * JT_RADIX + d] : compose_jump(jt[L * JT_RADIX + d], j);
+      first = false;
+    }
   }
   return j;
+}
+
+// numpy next_uint32 bookkeeping after `wtot` 32-bit words: u64 draws used and the new buffer flag.
+__device__ __forceinline__ void words_to_draws(uint32_t wtot, uint32_t h0, uint32_t& used, uint32_t& h) {
+  if (wtot == 0) {
+    used = 0; h = h0;
+  } else if (h0) {
+    used = wtot >> 1; h = (wtot - 1) & 1;  // ceil((wtot-1)/2)
+  } else {
+    used = (wtot + 1) >> 1; h = wtot & 1;  // ceil(wtot/2)
+  }
+}
+
+// Publish (to LDS) the next step's state: s0' = J_used(SB), buffered half. One lane writes.
+__device__ __forceinline__ void publish_next(const PcgJump* jt_lds, FusedShared& sh, const u128 SB, const PcgJump jB,
+                                            uint32_t wtot, uint32_t h0, uint32_t u0, bool writer) {
+  uint32_t used, h;
+  words_to_draws(wtot, h0, used, h);
+  const PcgJump ju = jump_params(jt_lds, used);
+  const u128 s = apply_jump(ju, SB);
+  // numpy keeps the last buffered half in `uinteger` even after it has been consumed
+  const uint32_t u = used ? (uint32_t)(pcg_output(s) >> 32) : u0;
+  const PcgJump jt = used ? compose_jump(ju, jB) : jB;  // lane states advance by J_used o J_B
+  if (writer) {
+    sh.ju[0] = jt.a_hi; sh.ju[1] = jt.a_lo; sh.ju[2] = jt.c_hi; sh.ju[3] = jt.c_lo;
+    sh.ns_hi = hi64(s); sh.ns_lo = lo64(s);
+    sh.nh = h; sh.nu = u;
+  }
 }
 
 #ifdef GP_STAMPS
 #define STAMP(i)                                                                                  \
   do {                                                                                            \
-    if (threadIdx.x == 0 && k < 64) {                                                             \
+    if (threadIdx.x == ((i) == 3 ? FENVW * 64 : 0) && k < 64) {                                   \
       unsigned long long t_;                                                                      \
-      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                   \
+      asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");               \
+      p_in.dbg[((size_t)blockIdx.x * 64 + k) * 8 + (i)] = t_;                                     \
+    }                                                                                             \
+  } while (0)
+// wall-clock (100 MHz, chip-synchronous) stamp by the calling lane
+#define RSTAMP(i)                                                                                 \
+  do {                                                                                            \
+    if (k < 64) {                                                                                 \
+      unsigned long long t_;                                                                      \
+      asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");               \
       p_in.dbg[((size_t)blockIdx.x * 64 + k) * 8 + (i)] = t_;                                     \
     }                                                                                             \
   } while (0)
 #else
+#define RSTAMP(i) \
+  do {            \
+  } while (0)
 #define STAMP(i) \
   do {           \
   } while (0)
@@ -882,7 +1019,7 @@ __device__ __forceinline__ PcgJump jump_params(const PcgJump* jt, uint32_t n) {
 
 // Workgroup barrier that orders LDS only: __syncthreads() also drains every outstanding global
 // store of the wave (s_waitcnt vmcnt(0)), which would put the obs/reward store latency on the
-// fused kernel's per-step critical path. All fused-kernel barriers guard LDS (sh.*) only.
+// fused kernel's per-step critical path. All fused-kernel barriers below guard LDS (sh.*) only.
 __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
   __builtin_amdgcn_s_barrier();
@@ -897,31 +1034,351 @@ __device__ __forceinline__ void lds_copy(char* dyn, const GridLdsTab& t, const T
   for (int i = threadIdx.x; i < (t.bytes + 15) / 16; i += blockDim.x) d[i] = s[i];
 }
 
-template <int OK, int QPT>
-__global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, const int32_t* __restrict__ act,
-                                                           void* __restrict__ obs, float* __restrict__ rew,
-                                                           uint8_t* __restrict__ term, uint8_t* __restrict__ trunc) {
-  __shared__ FusedShared sh;
-  __shared__ uint64_t s_thr[64];
-  extern __shared__ __attribute__((aligned(16))) char dyn[];
+// Phase 4 of a fused step (both roles; every barrier here is block-uniform): the resetters'
+// choice() draws. CTRL = the control wave (coverage exchanges, stream walks, J_used of the
+// unusual cases); otherwise an env wave with its env state.
+template <int OK, int QPT, bool CTRL>
+__device__ __forceinline__ void fused_resets(const GridDev& p, FusedShared& sh, const LTabs& tb, const Stream& st,
+                                             const u128 SB, const PcgJump& jB, uint64_t* slots, uint32_t tag0,
+                                             void* ob, uint32_t (&ae)[QPT][4], int (&gl)[QPT][4],
+                                             const uint32_t (&fm)[QPT], const uint32_t (&excl)[QPT],
+                                             const uint32_t (&wex)[QPT], const uint32_t (&wt)[QPT]) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int G = (int)gridDim.x, nt = p.fnt;
+  const bool rgoal = p.fixed_goal < 0, ragent = p.fixed_agent < 0;
+  const int ncalls = (int)rgoal + (int)ragent;
+  const uint32_t n1 = rgoal ? (uint32_t)p.n_goal_valid : (uint32_t)p.n_agent_valid;
+  const uint32_t thr1 = rgoal ? p.thr_goal : p.thr_agent;
+  const uint32_t b = sh.btot;
+  if (!(ncalls && b)) return;
+  uint32_t slow = sh.anyrej;
+  if (!slow && b > (uint32_t)nt * RCOV)  // mass reset: extend call-1 coverage
+    slow = coverage_round(p.self, st, slots + G, nt, G, QPT, tag0 + 1, (uint32_t)nt * RCOV, b - nt * RCOV, n1, thr1, sh);
+  if (!slow && ncalls == 2)  // agent words start right after the b goal words
+    slow = coverage_round(p.self, st, slots + 2 * G, nt, G, QPT, tag0 + 2, b, b, (uint32_t)p.n_agent_valid, p.thr_agent,
+                          sh);
+  uint32_t w1 = b;
+  if (slow && ncalls == 2) {
+    if constexpr (CTRL) {
+      const uint32_t a = scan_accepted(p.self, st, 0, n1, thr1, b - 1, b, nullptr);
+      if (lane == 0) sh.w1 = a;
+    }
+    lds_barrier();
+    w1 = sh.w1;
+  }
+  const uint32_t mode = (rgoal ? 1u : 0u) | (ragent ? 2u : 0u);
+  const uint32_t ng = (uint32_t)p.n_goal_valid, na = (uint32_t)p.n_agent_valid;
+  if (!slow) {
+    if constexpr (!CTRL) {
+      // fast path: the wave's resetters are compacted in LDS, one draw per lane per pass
+      uint32_t* rj = sh.pos + wid * 256;
+      uint32_t* rv = sh.pos2 + wid * 256;
+      uint32_t R = 0, cb[QPT];
+#pragma unroll
+      for (int q = 0; q < QPT; ++q) {
+        cb[q] = R + wex[q];
+        R += wt[q];
+      }
+      for (uint32_t c0 = 0; c0 < R; c0 += 256) {
+#pragma unroll
+        for (int q = 0; q < QPT; ++q) {
+          uint32_t m = fm[q], c = cb[q], lr = excl[q];
+          const uint32_t P = sh.tpre[q];
+          while (m) {
+            if (c - c0 < 256u) rj[c - c0] = P + lr;
+            m &= m - 1;
+            ++c;
+            ++lr;
+          }
+        }
+        wave_lds_sync();
+        const uint32_t nr = min(R - c0, 256u);
+        for (uint32_t l = lane; l < nr; l += 64) {
+          const uint32_t j = rj[l];
+          rv[l] = draw_cells(tb.jt(), st.s0, st.inc, st.h0, st.u0, st.U0, j, (rgoal ? w1 : 0u) + j, mode, ng, na);
+        }
+        wave_lds_sync();
+#pragma unroll
+        for (int q = 0; q < QPT; ++q) {
+          const int env0 = (q * G + (int)blockIdx.x) * FEPB + tid * EPT;
+          uint32_t c = cb[q];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            if (!(fm[q] & (1u << i))) continue;
+            if (c - c0 < 256u) {
+              const uint32_t v = rv[c - c0];
+              const int goal = rgoal ? (int)tb.gv((int)(v & 0xFFFFu)) : gl[q][i];
+              const int agent = ragent ? (int)tb.av((int)(v >> 16)) : (int)(ae[q][i] & 0xFFFFu);
+              gl[q][i] = goal;
+              ae[q][i] = (uint32_t)agent;
+              write_obs<OK>(p, tb, env0 + i, agent, goal, ob);
+            }
+            ++c;
+          }
+        }
+        wave_lds_sync();  // rj/rv reused by the next pass
+      }
+    }
+  } else {
+    // slow path (a rejection somewhere): the control wave walks the stream tile by tile
+#pragma unroll
+    for (int q = 0; q < QPT; ++q) {
+      const int tau = q * G + (int)blockIdx.x;
+      if (tau >= nt) continue;  // block-uniform
+      const uint32_t P = sh.tpre[q];
+      if constexpr (CTRL) {
+        uint32_t tc = 0;
+#pragma unroll
+        for (int w = 0; w < FENVW; ++w) tc += sh.wcnt[q][w];
+        if (tc) {
+          if (rgoal) scan_accepted(p.self, st, 0, ng, p.thr_goal, P, P + tc, sh.pos);
+          if (ragent) scan_accepted(p.self, st, rgoal ? w1 : 0, na, p.thr_agent, P, P + tc, rgoal ? sh.pos2 : sh.pos);
+        }
+      }
+      lds_barrier();
+      if constexpr (!CTRL) {
+        if (fm[q]) {
+          const int env0 = tau * FEPB + tid * EPT;
+          uint32_t lr = excl[q];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            if (!(fm[q] & (1u << i))) continue;
+            const uint32_t wg = sh.pos[lr], wa = rgoal ? sh.pos2[lr] : sh.pos[lr];
+            const uint32_t v = draw_cells(tb.jt(), st.s0, st.inc, st.h0, st.u0, st.U0, wg, wa, mode, ng, na);
+            const int goal = rgoal ? (int)tb.gv((int)(v & 0xFFFFu)) : gl[q][i];
+            const int agent = ragent ? (int)tb.av((int)(v >> 16)) : (int)(ae[q][i] & 0xFFFFu);
+            gl[q][i] = goal;
+            ae[q][i] = (uint32_t)agent;
+            write_obs<OK>(p, tb, env0 + i, agent, goal, ob);
+            ++lr;
+          }
+        }
+      }
+      lds_barrier();  // sh.pos reused by the next tile
+    }
+  }
+  if (!sh.known) {  // block-uniform: the slow / multi-call / extended cases
+    if constexpr (CTRL) {
+      uint32_t wtot;
+      if (!slow) {
+        wtot = (uint32_t)ncalls * b;
+      } else {
+        const bool last_goal = ncalls == 1 && rgoal;
+        wtot = scan_accepted(p.self, st, ncalls == 2 ? w1 : 0u, last_goal ? ng : na, last_goal ? p.thr_goal : p.thr_agent,
+                             b - 1, b, nullptr);
+      }
+      publish_next(tb.jt(), sh, SB, jB, wtot, st.h0, st.u0, lane == 0);
+    }
+    lds_barrier();
+  }
+}
+
+// Effective action of env with action a and 53-bit uniform k: #{j : k > thr[a][j]} (integer form
+// of action_utils.py:84-90), on the high 32 bits with an exact 64-bit fallback on a tie.
+template <int NA>
+__device__ __forceinline__ uint32_t fused_effective_action(const FusedShared& sh, const uint64_t* s_thr, int a,
+                                                           uint64_t k) {
+  const uint32_t khi = (uint32_t)(k >> 21);
+  uint32_t e = 0;
+  bool tie = false;
+#pragma unroll
+  for (int h = 0; h < NA / 4; ++h) {
+    const uint4 t = sh.thr4[a * (NA / 4) + h];
+    e += (khi > t.x) + (khi > t.y) + (khi > t.z) + (khi > t.w);
+    tie |= (khi == t.x) | (khi == t.y) | (khi == t.z) | (khi == t.w);
+  }
+  if (tie) {
+    e = 0;
+#pragma unroll
+    for (int j = 0; j < NA; ++j) e += (k > s_thr[a * NA + j]) ? 1u : 0u;
+  }
+  return min(e, (uint32_t)NA - 1);
+}
+
+// The env waves of the fused kernel.
+template <int OK, int QPT, int NA>
+__device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, const uint64_t* s_thr,
+                                          const LTabs& tb, int K, const int32_t* __restrict__ act,
+                                          void* __restrict__ obs, float* __restrict__ rew,
+                                          uint8_t* __restrict__ term, uint8_t* __restrict__ trunc, float& rsum,
+                                          uint32_t& eps, uint32_t& lens, uint32_t& nst) {
   const GridDev& p = p_in;
-  if (threadIdx.x < p.nact * p.nact) s_thr[threadIdx.x] = p.thr[threadIdx.x];
-  // stage the lookup tables in LDS (the fused path is only taken when they fit)
-  lds_copy(dyn, p.lds.move, p.move);
-  lds_copy(dyn, p.lds.hbase, p.hbase);
-  lds_copy(dyn, p.lds.hvec, p.hvec);
-  lds_copy(dyn, p.lds.t1, p.t1);
-  lds_copy(dyn, p.lds.t2, p.t2);
-  lds_copy(dyn, p.lds.coords, p.coords);
-  lds_copy(dyn, p.lds.window, p.window);
-  lds_copy(dyn, p.lds.gv, p.goal_valid);
-  lds_copy(dyn, p.lds.av, p.agent_valid);
-  lds_copy(dyn, p.lds.doff, p.doff);
-  const LTabs tb{p_in, dyn};
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const GridCtl* C = p.ctl;
+  const int G = (int)gridDim.x;
+  const int nt = p.fnt;
+  const int B = p.B;
+  const bool rgoal = p.fixed_goal < 0;
+  const int ncalls = (int)rgoal + (int)(p.fixed_agent < 0);
+  const int fixed_agent = p.fixed_agent, fixed_goal = p.fixed_goal, tlim = p.time_limit;
+  const float r_step = p.r_step, r_wall = p.r_wall, r_goal = p.r_goal;
+  Stream st;
+  st.s0 = mk128(C->s_hi, C->s_lo);
+  st.inc = mk128(C->inc_hi, C->inc_lo);
+  st.h0 = C->has_u32;
+  st.u0 = C->uinteger;
+  st.U0 = (uint32_t)B;
+  const uint32_t step_base = C->step;
+  const size_t ow = (size_t)p.obs_width * ((OK == GP_OBS_HANSEN_VEC || OK == GP_OBS_WINDOW) ? 1 : 4);
+  const PcgJump jB_unused{0, 1, 0, 0};
+  uint32_t ae[QPT][4];
+  int gl[QPT][4];
+  int32_t a_cur[QPT][4];
+  u128 S[QPT];  // lane draw state: jump(s0, e0 + 1)
+#pragma unroll
+  for (int q = 0; q < QPT; ++q) {
+    const int tau = q * G + (int)blockIdx.x;
+    const int env0 = tau * FEPB + tid * EPT;
+    load4<uint32_t>(p.ae, env0, B, ae[q]);
+    if (rgoal) {
+      uint16_t gg[4];
+      load4<uint16_t>(p.goal, env0, B, gg);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) gl[q][i] = gg[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) gl[q][i] = fixed_goal;
+    }
+    load4<int32_t>(act, env0, B, a_cur[q]);
+    S[q] = apply_jump(compose_jump(p.flt4[tid], p.ftj[min(tau, nt - 1)]), st.s0);
+  }
+  for (int k = 0; k < K; ++k) {
+    STAMP(0);
+    const uint32_t tag0 = (step_base + (uint32_t)k + 1u) * 4u;
+    uint64_t* slots = p.fslot + (size_t)((step_base + (uint32_t)k) & 1u) * 3 * G;
+    int32_t a_nxt[QPT][4];
+    if (k + 1 < K) {
+#pragma unroll
+      for (int q = 0; q < QPT; ++q)
+        load4<int32_t>(act + (size_t)(k + 1) * B, (q * G + (int)blockIdx.x) * FEPB + tid * EPT, B, a_nxt[q]);
+    }
+    // ---- 1. draws + transitions (the critical path) ----
+    float r[QPT][4];
+    uint32_t fm[QPT], tmm[QPT], trm[QPT], excl[QPT], wex[QPT], wt[QPT];
+#pragma unroll
+    for (int q = 0; q < QPT; ++q) {
+      const int env0 = (q * G + (int)blockIdx.x) * FEPB + tid * EPT;
+      fm[q] = tmm[q] = trm[q] = 0;
+      u128 s = S[q];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (i) s = pcg_step(s, st.inc);
+        const uint64_t k53 = pcg_output(s) >> 11;
+        int a = a_cur[q][i];
+        if (a < 0) a += NA;                 // numpy negative indexing of action_matrix[action]
+        a = min(max(a, 0), NA - 1);         // (out-of-range actions raise in the reference; clamped here)
+        const uint32_t eff = fused_effective_action<NA>(sh, s_thr, a, k53);
+        const uint32_t s_ae = ae[q][i];
+        const int agent = (int)(s_ae & 0xFFFFu);
+        const uint32_t m = tb.move(agent * NA + (int)eff);
+        const int na_ = (int)(m & 0x7FFFu);
+        const bool blocked = (m >> 15) != 0;
+        const uint32_t el = (s_ae >> 16) + 1u;
+        const bool tm_ = na_ == gl[q][i];
+        const bool tr_ = el > (uint32_t)tlim;
+        const bool valid = env0 + i < B;
+        const bool f = valid && (tm_ || tr_);
+        const float rw = tm_ ? r_goal : (blocked ? r_wall : r_step);
+        r[q][i] = rw;
+        tmm[q] |= (uint32_t)tm_ << i;
+        trm[q] |= (uint32_t)tr_ << i;
+        fm[q] |= (uint32_t)f << i;
+        const int ag = f && fixed_agent >= 0 ? fixed_agent : na_;
+        ae[q][i] = (uint32_t)ag | ((f ? 0u : el) << 16);
+        if (f && fixed_goal >= 0) gl[q][i] = fixed_goal;
+        if (valid) {
+          rsum += rw;
+          nst += 1;
+        }
+        if (f) {
+          eps += 1;
+          lens += el;
+        }
+      }
+      wave_count_prefix((uint32_t)__builtin_popcount(fm[q]), wex[q], wt[q]);
+      if (lane == 0) sh.wcnt[q][wid] = wt[q];
+    }
+    STAMP(1);
+    lds_barrier();  // B1: per-wave reset counts are in LDS
+    STAMP(2);
+#pragma unroll
+    for (int q = 0; q < QPT; ++q) {
+      uint32_t woff = 0;
+#pragma unroll
+      for (int w = 0; w < FENVW; ++w) woff += w < wid ? sh.wcnt[q][w] : 0u;
+      excl[q] = wex[q] + woff;
+    }
+    // ---- 3. this step's outputs (overlap the exchange) ----
+    const size_t off = (size_t)k * B;
+    void* ob = (uint8_t*)obs + off * ow;
+    if (!(p.diag & 1)) {
+#pragma unroll
+      for (int q = 0; q < QPT; ++q) {
+        const int env0 = (q * G + (int)blockIdx.x) * FEPB + tid * EPT;
+        uint8_t tm[4], tr[4];
+        int ag[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          tm[i] = (uint8_t)((tmm[q] >> i) & 1u);
+          tr[i] = (uint8_t)((trm[q] >> i) & 1u);
+          ag[i] = (int)(ae[q][i] & 0xFFFFu);
+        }
+        store4<float>(rew + off, env0, B, r[q]);
+        store4<uint8_t>(term + off, env0, B, tm);
+        store4<uint8_t>(trunc + off, env0, B, tr);
+        if (fm[q] == 0 || ncalls == 0) {
+          write_obs4<OK>(p, tb, env0, ag, gl[q], ob);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (!(fm[q] & (1u << i)) && env0 + i < B) write_obs<OK>(p, tb, env0 + i, ag[i], gl[q][i], ob);
+        }
+      }
+    }
+    lds_barrier();  // B2: the exchange result is in LDS
+    STAMP(4);
+    // ---- 4. the resetters' draws ----
+    fused_resets<OK, QPT, false>(p, sh, tb, st, st.s0, jB_unused, slots, tag0, ob, ae, gl, fm, excl, wex, wt);
+    // ---- 5. advance: lane states jump by J_used o J_B ----
+    {
+      const PcgJump jt{sh.ju[0], sh.ju[1], sh.ju[2], sh.ju[3]};
+      st.s0 = mk128(sh.ns_hi, sh.ns_lo);
+      st.h0 = sh.nh;
+      st.u0 = sh.nu;
+#pragma unroll
+      for (int q = 0; q < QPT; ++q) S[q] = apply_jump(jt, S[q]);
+    }
+    if (k + 1 < K) {
+#pragma unroll
+      for (int q = 0; q < QPT; ++q)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a_cur[q][i] = a_nxt[q][i];
+    }
+    STAMP(5);
+  }
+#pragma unroll
+  for (int q = 0; q < QPT; ++q) {
+    const int env0 = (q * G + (int)blockIdx.x) * FEPB + tid * EPT;
+    store4<uint32_t>(p.ae, env0, B, ae[q]);
+    if (rgoal) {
+      uint16_t gg[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) gg[i] = (uint16_t)gl[q][i];
+      store4<uint16_t>(p.goal, env0, B, gg);
+    }
+  }
+}
+
+// The control wave of the fused kernel: speculative rejection checks, the granule exchange, the
+// next PCG64 state; publishes the RNG state at the end (block 0).
+template <int OK, int QPT>
+__device__ __forceinline__ void fused_ctrl(const GridDev& p_in, FusedShared& sh, const LTabs& tb, int K) {
+  constexpr int NC = (QPT + 1) / 2;  // checker states per lane (32 lanes per tile)
+  const GridDev& p = p_in;
+  const int tid = threadIdx.x, lane = tid & 63;
   GridCtl* C = p.ctl;
   const int G = (int)gridDim.x;
   const int nt = p.fnt;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const bool rgoal = p.fixed_goal < 0, ragent = p.fixed_agent < 0;
   const int ncalls = (int)rgoal + (int)ragent;
   const uint32_t n1 = rgoal ? (uint32_t)p.n_goal_valid : (uint32_t)p.n_agent_valid;
@@ -934,351 +1391,213 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
   st.U0 = (uint32_t)p.B;
   const uint32_t step_base = C->step;
   const PcgJump jB = *p.fjB;
-  const size_t ow = (size_t)p.obs_width * ((OK == GP_OBS_HANSEN_VEC || OK == GP_OBS_WINDOW) ? 1 : 4);
-  // env state in registers
-  uint32_t ae[QPT][4];
-  int gl[QPT][4];
-  int32_t a_cur[QPT][4];
-  u128 S[QPT];  // lane draw state: jump(s0, e0 + 1)
+  // lane l checks tile q = 2c + (l >> 5); lane ll = l & 31 holds u64 #(tau*31 - 1 + ll) of the
+  // post-random(B) stream, i.e. jump(s0, B + tau*31 + ll)
+  u128 CS[NC];
+  bool chk[NC];
+  int ctau[NC];
 #pragma unroll
-  for (int q = 0; q < QPT; ++q) {
-    const int tau = q * G + (int)blockIdx.x;
-    const int env0 = tau * FEPB + tid * EPT;
-    load4<uint32_t>(p.ae, env0, p.B, ae[q]);
-    if (rgoal) {
-      uint16_t gg[4];
-      load4<uint16_t>(p.goal, env0, p.B, gg);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) gl[q][i] = gg[i];
-    } else {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) gl[q][i] = p.fixed_goal;
-    }
-    load4<int32_t>(act, env0, p.B, a_cur[q]);
-    S[q] = apply_jump(compose_jump(p.flt4[tid], p.ftj[min(tau, nt - 1)]), st.s0);
+  for (int c = 0; c < NC; ++c) {
+    const int q = 2 * c + (lane >> 5);
+    ctau[c] = q * G + (int)blockIdx.x;
+    chk[c] = ncalls && q < QPT && ctau[c] < nt;
+    CS[c] = chk[c] ? pcg_jump(p.jt, st.s0, (uint32_t)p.B + (uint32_t)ctau[c] * (RCOV / 2) + (uint32_t)(lane & 31))
+                   : (u128)0;
   }
-  // speculative-check lane state: wave q checks tile q*G+b; lane l holds u64 #(tau*32 - 1 + l)
-  // of the post-random(B) stream, i.e. jump(s0, B + tau*32 + l)
-  const int cq = wid;  // which of my tiles this wave checks (if wid < QPT)
-  const int ctau = cq * G + (int)blockIdx.x;
-  const bool checker = ncalls && wid < QPT && lane <= 32 && ctau < nt;
-  u128 CS = 0;
-  if (checker) CS = pcg_jump(p.jt, st.s0, (uint32_t)p.B + (uint32_t)ctau * (RCOV / 2) + (uint32_t)lane);
-  float rsum = 0.f;
-  uint32_t eps = 0, lens = 0, nst = 0;
-  lds_barrier();
-
+  uint32_t dummy_u[QPT][4];
+  int dummy_i[QPT][4];
+  const uint32_t dummy_c[QPT] = {};
   for (int k = 0; k < K; ++k) {
-    STAMP(0);
     const uint32_t tag0 = (step_base + (uint32_t)k + 1u) * 4u;
-    uint64_t* slots = p.fslot + (size_t)((step_base + (uint32_t)k) & 1u) * 3 * nt;
-    int32_t a_nxt[QPT][4];
-    if (k + 1 < K) {
-#pragma unroll
-      for (int q = 0; q < QPT; ++q)
-        load4<int32_t>(act + (size_t)(k + 1) * p.B, (q * G + (int)blockIdx.x) * FEPB + tid * EPT, p.B, a_nxt[q]);
-    }
-    // speculative Lemire check of this tile's RCOV-word window (call 1)
+    uint64_t* slots = p.fslot + (size_t)((step_base + (uint32_t)k) & 1u) * 3 * G;
+    // speculative Lemire check of the RCOV-word windows of this block's tiles (call 1)
     uint32_t crej = 0;
-    if (checker) {
-      const uint64_t x = pcg_output(CS);
+    const uint32_t ll = lane & 31;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      if (!chk[c]) continue;
+      const uint64_t x = pcg_output(CS[c]);
       const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+      bool rj;
       if (!st.h0) {
-        if (lane >= 1) crej = (lemire_rejected(lo, n1, thr1) || lemire_rejected(hi, n1, thr1)) ? 1u : 0u;
-      } else if (lane == 0) {
-        crej = lemire_rejected(ctau == 0 ? st.u0 : hi, n1, thr1) ? 1u : 0u;
-      } else if (lane < 32) {
-        crej = (lemire_rejected(lo, n1, thr1) || lemire_rejected(hi, n1, thr1)) ? 1u : 0u;
+        rj = ll >= 1 && (lemire_rejected(lo, n1, thr1) || lemire_rejected(hi, n1, thr1));
+      } else if (ll == 0) {
+        rj = lemire_rejected(ctau[c] == 0 ? st.u0 : hi, n1, thr1);
+      } else if (ll < 31) {
+        rj = lemire_rejected(lo, n1, thr1) || lemire_rejected(hi, n1, thr1);
       } else {
-        crej = lemire_rejected(lo, n1, thr1) ? 1u : 0u;
+        rj = lemire_rejected(lo, n1, thr1);
       }
+      crej |= rj ? 1u : 0u;
     }
-    // 1. transitions
-    uint32_t fm[QPT];
-    uint32_t cnt[QPT];
-#pragma unroll
-    for (int q = 0; q < QPT; ++q) {
-      const int tau = q * G + (int)blockIdx.x;
-      const int env0 = tau * FEPB + tid * EPT;
-      uint64_t k4[4];
-      {
-        u128 s = S[q];
-        k4[0] = pcg_output(s) >> 11;
-#pragma unroll
-        for (int i = 1; i < 4; ++i) {
-          s = pcg_step(s, st.inc);
-          k4[i] = pcg_output(s) >> 11;
-        }
-      }
-      float r[4];
-      uint8_t tm[4], tr[4];
-      int ag[4];
-      fm[q] = 0;
-      cnt[q] = 0;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const Trans t = transition(p, tb, ae[q][i], gl[q][i], a_cur[q][i], k4[i], s_thr);
-        const bool valid = env0 + i < p.B;
-        const bool f = valid && (t.term | t.trunc);
-        r[i] = t.rew;
-        tm[i] = t.term;
-        tr[i] = t.trunc;
-        ag[i] = f && p.fixed_agent >= 0 ? p.fixed_agent : t.agent;
-        ae[q][i] = (uint32_t)ag[i] | ((uint32_t)(f ? 0 : t.elapsed) << 16);
-        if (f && p.fixed_goal >= 0) gl[q][i] = p.fixed_goal;
-        fm[q] |= (f ? 1u : 0u) << i;
-        cnt[q] += f;
-        if (valid) {
-          rsum += t.rew;
-          nst += 1;
-          if (f) { eps += 1; lens += (uint32_t)t.elapsed; }
-        }
-      }
-      const size_t off = (size_t)k * p.B;
-      store4<float>(rew + off, env0, p.B, r);
-      store4<uint8_t>(term + off, env0, p.B, tm);
-      store4<uint8_t>(trunc + off, env0, p.B, tr);
-      void* ob = (uint8_t*)obs + off * ow;
-      if (fm[q] == 0 || ncalls == 0) {
-        write_obs4<OK>(p, tb, env0, ag, gl[q], ob);
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (!(fm[q] & (1u << i)) && env0 + i < p.B) write_obs<OK>(p, tb, env0 + i, ag[i], gl[q][i], ob);
-      }
-      S[q] = apply_jump(jB, S[q]);  // half of the advance to the next step (J_B), off the critical path
-    }
-    if (checker) CS = apply_jump(jB, CS);
-    STAMP(1);
-    // 2. per-tile reset counts (packed 16 bits per tile) -> granules
-    uint64_t x = 0;
-#pragma unroll
-    for (int q = 0; q < QPT; ++q) x |= (uint64_t)cnt[q] << (16 * q);
-    const uint64_t c_self = x;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint64_t y = ((uint64_t)__shfl_up((uint32_t)(x >> 32), d, 64) << 32) | __shfl_up((uint32_t)x, d, 64);
-      if (lane >= d) x += y;
-    }
-    const bool wrj = __any((int)crej);
-    if (lane == 63) {
-      sh.wsum_lo[wid] = (uint32_t)x;
-      sh.wsum_hi[wid] = (uint32_t)(x >> 32);
-    }
-    if (lane == 0) sh.wrej[wid] = wrj ? 1u : 0u;
-    lds_barrier();
-    uint64_t woff = 0, tot = 0;
-#pragma unroll
-    for (int w = 0; w < FTPB / 64; ++w) {
-      const uint64_t v = ((uint64_t)sh.wsum_hi[w] << 32) | sh.wsum_lo[w];
-      if (w < wid) woff += v;
-      tot += v;
-    }
-    const uint64_t excl_local = x - c_self + woff;  // my exclusive rank per tile (16-bit fields)
-    if (tid < QPT) {
-      const int tau = tid * G + (int)blockIdx.x;
-      if (tau < nt)
-        __hip_atomic_store(&slots[tau], gran(tag0, sh.wrej[tid], (uint32_t)(tot >> (16 * tid)) & 0xFFFFu),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    STAMP(2);
-    // 3. all-gather of the nt granules
-    {
-      const uint64_t g = gather_granule(p, slots, nt, tag0);
-      const uint32_t c = (uint32_t)g & 0x7FFFFFFFu;
-      uint32_t xi = c;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(xi, d, 64);
-        if (lane >= d) xi += y;
-      }
-      const bool wrej = __any((int)((g >> 31) & 1u));
-      if (lane == 63) {
-        sh.red[wid] = xi;
-        sh.red2[wid] = wrej ? 1u : 0u;
-      }
-      lds_barrier();
-      uint32_t wo = 0, all = 0, anyr = 0;
-#pragma unroll
-      for (int w = 0; w < FTPB / 64; ++w) {
-        if (w < wid) wo += sh.red[w];
-        all += sh.red[w];
-        anyr |= sh.red2[w];
-      }
-      if (tid < nt) sh.tpre[tid] = xi - c + wo;
-      if (tid == 0) {
-        sh.btot = all;
-        sh.anyrej = anyr;
-      }
-      // fast path (no resets, or no rejection + full coverage + single call): J_used known right away
-      if (tid == 0 && (all == 0 || ncalls == 0 || (!anyr && ncalls == 1 && all <= (uint32_t)nt * RCOV))) {
-        const uint32_t wtot = (uint32_t)ncalls * all;
-        uint32_t used, h, u = st.u0;
-        if (wtot == 0) {
-          used = 0; h = st.h0;
-        } else if (st.h0) {
-          used = wtot >> 1; h = (wtot - 1) & 1;
-        } else {
-          used = (wtot + 1) >> 1; h = wtot & 1;
-        }
-        sh.ju = jump_params(p.jt, used);
-        sh.nh = h;
-        sh.nu = used ? 0xFFFFFFFFu : u;  // resolved after the jump (needs the new state's output)
-        sh.wtot = wtot;
-      } else if (tid == 0) {
-        sh.wtot = 0xFFFFFFFEu;  // not yet known
-      }
-      lds_barrier();
-    }
-    const uint32_t b = sh.btot;
-    STAMP(3);
-    // 4. choice() draws for the resetters
-    uint32_t slow = sh.anyrej;
+    const uint32_t wrej = __any((int)crej) ? 1u : 0u;
     const u128 SB = apply_jump(jB, st.s0);  // state after random(B): base of the word stream
-    if (ncalls && b) {
-      if (!slow && b > (uint32_t)nt * RCOV)  // mass reset: extend call-1 coverage
-        slow = coverage_round(p, st, slots + nt, nt, G, QPT, tag0 + 1, (uint32_t)nt * RCOV, b - nt * RCOV, n1,
-                              thr1);
-      if (!slow && ncalls == 2)  // agent words start right after the b goal words
-        slow = coverage_round(p, st, slots + 2 * nt, nt, G, QPT, tag0 + 2, b, b, (uint32_t)p.n_agent_valid,
-                              p.thr_agent);
-      uint32_t w1 = b;
-      if (slow && ncalls == 2) {
-        if (tid < 64) {
-          const uint32_t a = scan_accepted(p, st, 0, n1, thr1, b - 1, b, nullptr);
-          if (tid == 0) sh.w1 = a;
-        }
-        lds_barrier();
-        w1 = sh.w1;
-      }
+    lds_barrier();  // B1
+    // ---- 2. publish this block's granule ----
+    uint32_t tq = 0;
+    if (lane < QPT) {
+#pragma unroll
+      for (int w = 0; w < FENVW; ++w) tq += sh.wcnt[lane][w];
+    }
+    uint64_t counts = 0;
+#pragma unroll
+    for (int q = 0; q < QPT; ++q) counts |= (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)tq, q) << (12 * q);
+    if (lane == 0) {
+      __hip_atomic_store(&slots[blockIdx.x], bgran(tag0, wrej, counts), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      RSTAMP(6);
+    }
+    // ---- 3. exchange: block 0 aggregates and publishes one tagged word per tile
+    // {rejection, b, tile prefix}; every other block polls only its own QPT words ----
+    uint64_t* tw = p.fslot + (size_t)6 * G + (size_t)((step_base + (uint32_t)k) & 1u) * nt;
+    uint32_t b, anyr;
+    if (blockIdx.x == 0) {
+      uint64_t g[4];
+      gather_blocks(p, slots, G, tag0, g);
+      uint32_t rj = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) rj |= (uint32_t)(g[j] >> 48) & 1u;
+      anyr = __any((int)rj) ? 1u : 0u;
+      uint32_t pre[QPT][4];
+      uint32_t acc = 0;
 #pragma unroll
       for (int q = 0; q < QPT; ++q) {
-        const int tau = q * G + (int)blockIdx.x;
-        if (tau >= nt) continue;
-        const uint32_t tc = (uint32_t)(tot >> (16 * q)) & 0xFFFFu;
-        if (!tc) continue;  // block-uniform
-        const uint32_t P = sh.tpre[tau];
-        if (slow) {
-          if (tid < 64) {
-            if (rgoal) scan_accepted(p, st, 0, (uint32_t)p.n_goal_valid, p.thr_goal, P, P + tc, sh.pos);
-            if (ragent)
-              scan_accepted(p, st, rgoal ? w1 : 0, (uint32_t)p.n_agent_valid, p.thr_agent, P, P + tc,
-                            rgoal ? sh.pos2 : sh.pos);
-          }
-          lds_barrier();
-        }
-        if (fm[q]) {
-          const int env0 = tau * FEPB + tid * EPT;
-          uint32_t lr = (uint32_t)(excl_local >> (16 * q)) & 0xFFFFu;
-          void* ob = (uint8_t*)obs + (size_t)k * p.B * ow;
+        uint32_t v = 0;
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            if (!(fm[q] & (1u << i))) continue;
-            const uint32_t j = P + lr;
-            int goal = gl[q][i], agent = (int)(ae[q][i] & 0xFFFF);
-            if (rgoal) {
-              const uint32_t w = slow ? sh.pos[lr] : j;
-              goal = tb.gv(lemire_value(word_at(p, st, w), (uint32_t)p.n_goal_valid));
-            }
-            if (ragent) {
-              const uint32_t w = slow ? (rgoal ? sh.pos2[lr] : sh.pos[lr]) : (rgoal ? w1 : 0u) + j;
-              agent = tb.av(lemire_value(word_at(p, st, w), (uint32_t)p.n_agent_valid));
-            }
-            gl[q][i] = goal;
-            ae[q][i] = (uint32_t)agent;
-            write_obs<OK>(p, tb, env0 + i, agent, goal, ob);
-            ++lr;
-          }
-        }
-        if (slow) lds_barrier();  // sh.pos reused by the next tile
-      }
-      if (sh.wtot == 0xFFFFFFFEu) {  // block-uniform: the slow / multi-call / extended cases
-        lds_barrier();
-        if (tid < 64) {
-          uint32_t wtot;
-          if (!slow) {
-            wtot = (uint32_t)ncalls * b;
-          } else {
-            const bool last_goal = ncalls == 1 && rgoal;
-            wtot = scan_accepted(p, st, ncalls == 2 ? w1 : 0u,
-                                 last_goal ? (uint32_t)p.n_goal_valid : (uint32_t)p.n_agent_valid,
-                                 last_goal ? p.thr_goal : p.thr_agent, b - 1, b, nullptr);
-          }
-          if (tid == 0) {
-            uint32_t used, h, u = st.u0;
-            if (st.h0) {
-              used = wtot >> 1; h = (wtot - 1) & 1;
-            } else {
-              used = (wtot + 1) >> 1; h = wtot & 1;
-            }
-            sh.ju = jump_params(p.jt, used);
-            sh.nh = h;
-            sh.nu = used ? 0xFFFFFFFFu : u;
-            sh.wtot = wtot;
-          }
-        }
-      }
-    }
-    STAMP(4);
-    lds_barrier();
-    // 5. advance: s0' = J_used(J_B(s0)); lanes apply J_used (J_B was applied in phase 1)
-    const PcgJump ju = sh.ju;
-    st.s0 = apply_jump(ju, SB);
-    st.h0 = sh.nh;
-    st.u0 = sh.nu == 0xFFFFFFFFu ? (uint32_t)(pcg_output(st.s0) >> 32) : sh.nu;
+        for (int j = 0; j < 4; ++j) v += gcount(g[j], q);
+        const uint32_t incl = wave_incl_scan(v);
+        uint32_t run = acc + incl - v;
 #pragma unroll
-    for (int q = 0; q < QPT; ++q) S[q] = apply_jump(ju, S[q]);
-    if (checker) CS = apply_jump(ju, CS);
-    if (k + 1 < K) {
+        for (int j = 0; j < 4; ++j) {
+          pre[q][j] = run;
+          run += gcount(g[j], q);
+        }
+        acc += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+      }
+      b = acc;
 #pragma unroll
       for (int q = 0; q < QPT; ++q)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) a_cur[q][i] = a_nxt[q][i];
-    }
-    STAMP(5);
-    lds_barrier();  // sh reuse
-  }
-  // write the state back; block 0 publishes the RNG state and the step counter
+        for (int j = 0; j < 4; ++j) {
+          const int blk = lane * 4 + j, tau = q * G + blk;
+          if (blk < G && tau < nt)
+            __hip_atomic_store(&tw[tau], tword(tag0, anyr, b, pre[q][j]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      if (lane == 0) {
 #pragma unroll
-  for (int q = 0; q < QPT; ++q) {
-    const int env0 = (q * G + (int)blockIdx.x) * FEPB + tid * EPT;
-    store4<uint32_t>(p.ae, env0, p.B, ae[q]);
-    if (rgoal) {
-      uint16_t gg[4];
+        for (int q = 0; q < QPT; ++q) sh.tpre[q] = pre[q][0];
+      }
+    } else {
+      uint64_t w = 0;
+      const int tau = lane * G + (int)blockIdx.x;
+      if (lane < QPT && tau < nt) {
+        const uint64_t want = (uint64_t)(tag0 & TAG_MASK);
+        uint32_t spins = 0;
+        w = __hip_atomic_load(&tw[tau], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while ((w >> 49) != want) {
+          __builtin_amdgcn_s_sleep(1);
+          w = __hip_atomic_load(&tw[tau], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (++spins > SPIN_LIMIT) {
+            atomicOr(&p.ctl->err, 1u);
+            w = want << 49;
+            break;
+          }
+        }
+        sh.tpre[lane] = (uint32_t)w & 0xFFFFFFu;
+      }
+      const uint64_t w0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(w >> 32), 0) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)w, 0);
+      b = (uint32_t)(w0 >> 24) & 0xFFFFFFu;
+      anyr = (uint32_t)(w0 >> 48) & 1u;
+    }
+    const bool known = b == 0 || ncalls == 0 || (!anyr && ncalls == 1 && b <= (uint32_t)nt * RCOV);
+    if (known) publish_next(tb.jt(), sh, SB, jB, ncalls ? b : 0u, st.h0, st.u0, lane == 0);
+    if (lane == 0) {
+      sh.btot = b;
+      sh.anyrej = anyr;
+      sh.known = known ? 1u : 0u;
+      RSTAMP(7);
+    }
+    STAMP(3);
+    lds_barrier();  // B2
+    // ---- 4. coverage exchanges / stream walks of the unusual cases ----
+    fused_resets<OK, QPT, true>(p, sh, tb, st, SB, jB, slots, tag0, nullptr, dummy_u, dummy_i, dummy_c, dummy_c,
+                                dummy_c, dummy_c);
+    // ---- 5. advance ----
+    {
+      const PcgJump jt{sh.ju[0], sh.ju[1], sh.ju[2], sh.ju[3]};
+      st.s0 = mk128(sh.ns_hi, sh.ns_lo);
+      st.h0 = sh.nh;
+      st.u0 = sh.nu;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) gg[i] = (uint16_t)gl[q][i];
-      store4<uint16_t>(p.goal, env0, p.B, gg);
+      for (int c = 0; c < NC; ++c)
+        if (chk[c]) CS[c] = apply_jump(jt, CS[c]);
     }
   }
-  if (blockIdx.x == 0 && tid == 0) {
+  if (blockIdx.x == 0 && lane == 0) {
     C->s_hi = hi64(st.s0);
     C->s_lo = lo64(st.s0);
     C->has_u32 = st.h0;
     C->uinteger = st.u0;
     C->step = step_base + (uint32_t)K;
   }
-  // metrics (1024-thread block)
-  {
+}
+
+template <int OK, int QPT, int NA>
+__global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, const int32_t* __restrict__ act,
+                                                           void* __restrict__ obs, float* __restrict__ rew,
+                                                           uint8_t* __restrict__ term, uint8_t* __restrict__ trunc) {
+  __shared__ FusedShared sh;
+  __shared__ uint64_t s_thr[64];
+  extern __shared__ __attribute__((aligned(16))) char dyn[];
+  const GridDev& p = p_in;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if (tid < NA * NA) {
+    const uint64_t t = p.thr[tid];
+    s_thr[tid] = t;
+    reinterpret_cast<uint32_t*>(sh.thr4)[tid] = (t >> 21) > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)(t >> 21);
+  }
+  // stage the lookup tables in LDS (the fused path is only taken when they fit)
+  lds_copy(dyn, p.lds.move, p.move);
+  lds_copy(dyn, p.lds.hbase, p.hbase);
+  lds_copy(dyn, p.lds.hvec, p.hvec);
+  lds_copy(dyn, p.lds.t1, p.t1);
+  lds_copy(dyn, p.lds.t2, p.t2);
+  lds_copy(dyn, p.lds.coords, p.coords);
+  lds_copy(dyn, p.lds.window, p.window);
+  lds_copy(dyn, p.lds.gv, p.goal_valid);
+  lds_copy(dyn, p.lds.av, p.agent_valid);
+  lds_copy(dyn, p.lds.doff, p.doff);
+  lds_copy(dyn, p.lds.jt, p.jt);
+  const LTabs tb{p_in, dyn};
+  __syncthreads();
+  float rsum = 0.f;
+  uint32_t eps = 0, lens = 0, nst = 0;
+  if (wid == FENVW) {
+    __builtin_amdgcn_s_setprio(3);  // the exchange is on every step's critical path
+    fused_ctrl<OK, QPT>(p, sh, tb, K);
+  } else {
+    fused_env<OK, QPT, NA>(p, sh, s_thr, tb, K, act, obs, rew, term, trunc, rsum, eps, lens, nst);
+  }
+  // metrics (the control wave contributes zeros)
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-      rsum += __shfl_xor(rsum, d, 64);
-      eps += __shfl_xor(eps, d, 64);
-      lens += __shfl_xor(lens, d, 64);
-      nst += __shfl_xor(nst, d, 64);
-    }
-    __shared__ float m_r[FTPB / 64];
-    __shared__ uint32_t m_e[FTPB / 64], m_l[FTPB / 64], m_n[FTPB / 64];
-    if (lane == 0) { m_r[wid] = rsum; m_e[wid] = eps; m_l[wid] = lens; m_n[wid] = nst; }
-    lds_barrier();
-    if (tid == 0) {
-      float r = 0; uint32_t e = 0, l = 0, n = 0;
-      for (int w = 0; w < FTPB / 64; ++w) { r += m_r[w]; e += m_e[w]; l += m_l[w]; n += m_n[w]; }
-      MetricSlot& m = p.mslot[blockIdx.x];
-      m.return_sum += (double)r;
-      m.episodes += e;
-      m.length_sum += l;
-      m.env_steps += n;
-    }
+  for (int d = 32; d >= 1; d >>= 1) {
+    rsum += __shfl_xor(rsum, d, 64);
+    eps += __shfl_xor(eps, d, 64);
+    lens += __shfl_xor(lens, d, 64);
+    nst += __shfl_xor(nst, d, 64);
+  }
+  __shared__ float m_r[FWAVES];
+  __shared__ uint32_t m_e[FWAVES], m_l[FWAVES], m_n[FWAVES];
+  if (lane == 0) { m_r[wid] = rsum; m_e[wid] = eps; m_l[wid] = lens; m_n[wid] = nst; }
+  __syncthreads();
+  if (tid == 0) {
+    float rr = 0; uint32_t e = 0, l = 0, n = 0;
+    for (int w = 0; w < FWAVES; ++w) { rr += m_r[w]; e += m_e[w]; l += m_l[w]; n += m_n[w]; }
+    MetricSlot& m = p.mslot[blockIdx.x];
+    m.return_sum += (double)rr;
+    m.episodes += e;
+    m.length_sum += l;
+    m.env_steps += n;
   }
 }
 
@@ -1430,7 +1749,7 @@ struct GridBackend : EnvBackend {
   std::vector<int32_t> cells;
   std::vector<uint16_t> goal_valid_h, agent_valid_h;
   DevBuf b_move, b_thr, b_gv, b_av, b_hbase, b_doff, b_hvec, b_t1, b_t2, b_coords, b_window, b_jt, b_lt4, b_lt2,
-      b_tja, b_tjw, b_ae, b_goal, b_ctl, b_tcount, b_tlist, b_rflag, b_mslot, b_ftj, b_flt4, b_fjB, b_fslot, b_dbg;
+      b_tja, b_tjw, b_ae, b_goal, b_ctl, b_tcount, b_tlist, b_rflag, b_mslot, b_ftj, b_flt4, b_fjB, b_fslot, b_dbg, b_self;
   int fused_G = 0, fused_qpt = 0;  // fused numpy rollout geometry (0 = not eligible)
   // replay pointers for the next step
   const uint64_t* rp_u = nullptr;
@@ -1493,24 +1812,22 @@ struct GridBackend : EnvBackend {
     return n;
   }
 #endif
+  template <int OK, int QPT>
+  void launch_fused_q(int K, const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc, hipStream_t s) {
+    if (d.nact == 4)
+      hipLaunchKernelGGL((grid_rollout_numpy<OK, QPT, 4>), dim3(fused_G), dim3(FTPB), d.lds.total, s, d, K,
+                         (const int32_t*)act, obs, rew, term, trunc);
+    else
+      hipLaunchKernelGGL((grid_rollout_numpy<OK, QPT, 8>), dim3(fused_G), dim3(FTPB), d.lds.total, s, d, K,
+                         (const int32_t*)act, obs, rew, term, trunc);
+  }
   template <int OK>
   int launch_fused(int K, const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc, hipStream_t s) {
     timer.begin(s);
     switch (fused_qpt) {
-      case 1:
-        hipLaunchKernelGGL((grid_rollout_numpy<OK, 1>), dim3(fused_G), dim3(FTPB), d.lds.total, s, d, K,
-                           (const int32_t*)act,
-                           obs, rew, term, trunc);
-        break;
-      case 2:
-        hipLaunchKernelGGL((grid_rollout_numpy<OK, 2>), dim3(fused_G), dim3(FTPB), d.lds.total, s, d, K,
-                           (const int32_t*)act,
-                           obs, rew, term, trunc);
-        break;
-      default:
-        hipLaunchKernelGGL((grid_rollout_numpy<OK, 4>), dim3(fused_G), dim3(FTPB), d.lds.total, s, d, K,
-                           (const int32_t*)act,
-                           obs, rew, term, trunc);
+      case 1: launch_fused_q<OK, 1>(K, act, obs, rew, term, trunc, s); break;
+      case 2: launch_fused_q<OK, 2>(K, act, obs, rew, term, trunc, s); break;
+      default: launch_fused_q<OK, 4>(K, act, obs, rew, term, trunc, s);
     }
     timer.end(s);
     GP_HIP_CHECK(hipGetLastError());
@@ -1520,6 +1837,7 @@ struct GridBackend : EnvBackend {
 
 int GridBackend::upload_rng() {
   GP_HIP_CHECK(hipDeviceSynchronize());
+  if (d.self) GP_HIP_CHECK(hipMemcpy(const_cast<GridDev*>(d.self), &d, sizeof(GridDev), hipMemcpyHostToDevice));
   GridCtl c;
   GP_HIP_CHECK(hipMemcpy(&c, d.ctl, sizeof(c), hipMemcpyDeviceToHost));
   c.s_hi = hi64(rng.state);
@@ -1956,15 +2274,20 @@ int GridBackend::build(const gp_grid_config* cfg) {
     put(d.lds.gv, goal_valid_h.size() * sizeof(uint16_t));
     put(d.lds.av, agent_valid_h.size() * sizeof(uint16_t));
     put(d.lds.doff, doff.size() * sizeof(int32_t));
+    put(d.lds.jt, sizeof(PcgJump) * JT_LEVELS * JT_RADIX);
     d.lds.total = off <= LDS_TABLE_BUDGET ? off : 0;
   }
-  // fused numpy rollout: one 1024-thread block per CU, <= 4 tiles of 4096 envs per block
+  // fused numpy rollout: one 512-thread block per CU, <= 4 tiles of 2048 envs per block
   d.fnt = (int)((B + FEPB - 1) / FEPB);
+  {
+    const char* dg = getenv("GP_DIAG");
+    d.diag = dg ? atoi(dg) : 0;
+  }
   {
     hipDeviceProp_t prop;
     GP_HIP_CHECK(hipGetDeviceProperties(&prop, device));
     int occ = 0;
-    GP_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, grid_rollout_numpy<GP_OBS_WINDOW, 4>, FTPB,
+    GP_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, grid_rollout_numpy<GP_OBS_WINDOW, 4, 8>, FTPB,
                                                              d.lds.total));
     const int G = std::min({prop.multiProcessorCount, FMAXG, d.fnt});
     const int qpt = (d.fnt + G - 1) / G;
@@ -1983,7 +2306,7 @@ int GridBackend::build(const gp_grid_config* cfg) {
       (e = b_tlist.alloc(sizeof(uint16_t) * (size_t)d.nblk * EPB)) || (e = b_rflag.alloc(sizeof(uint32_t) * 256)) ||
       (e = b_mslot.alloc(sizeof(MetricSlot) * (size_t)nslots)) ||
       (e = b_ftj.alloc(sizeof(PcgJump) * (size_t)std::max(d.fnt, 1))) || (e = b_flt4.alloc(sizeof(PcgJump) * FTPB)) ||
-      (e = b_fjB.alloc(sizeof(PcgJump))) || (e = b_fslot.alloc(sizeof(uint64_t) * 6 * (size_t)std::max(d.fnt, 1))))
+      (e = b_fjB.alloc(sizeof(PcgJump))) || (e = b_fslot.alloc(sizeof(uint64_t) * 8 * (size_t)std::max(d.fnt, 1))))
     return e;
   d.move = b_move.as<uint16_t>();
   d.thr = b_thr.as<uint64_t>();
@@ -2016,6 +2339,8 @@ int GridBackend::build(const gp_grid_config* cfg) {
   if ((e = b_dbg.alloc(sizeof(unsigned long long) * 256 * 64 * 8))) return e;
   d.dbg = b_dbg.as<unsigned long long>();
 #endif
+  if ((e = b_self.alloc(sizeof(GridDev)))) return e;
+  d.self = b_self.as<GridDev>();
   // default seed: numpy's SeedSequence(0) until the caller seeds
   rng = pcg64_from_seed({0u}, {});
   return upload_rng();

@@ -1,8 +1,9 @@
 """Phase breakdown of the fused numpy rollout kernel from a GP_STAMPS diagnostic build.
 
-    python gym-po-taxi_amd/build.py --stamps && GYM_PO_AMD_LIB=.../libgympo_amd_stamps.so python tools/stamps.py
-Stamps: 0 step start, 1 transitions+stores issued, 2 granule published, 3 all-gather done,
-4 resetters resolved, 5 next state broadcast. Reports median cycles per phase over blocks/steps.
+    python gym-po-taxi_amd/build.py --stamps && python tools/stamps.py [B]
+All stamps are s_memrealtime (100 MHz, synchronous across XCDs), per block and step:
+0 step start (env wave 0), 1 transitions done, 2 B1 passed, 3 exchange done (control wave),
+4 B2 passed, 5 step end, 6 granule published (control wave), 7 exchange done (control wave).
 """
 import ctypes
 import os
@@ -31,14 +32,27 @@ fn.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int
 buf = (ctypes.c_ulonglong * (256 * 64 * 8))()
 n = fn(env._handle, buf, 256 * 64 * 8)
 a = np.frombuffer(buf, dtype=np.uint64).reshape(256, 64, 8).astype(np.int64)
-G = min(256, (B + 4095) // 4096)
-a = a[:G, 1:K - 1]
-d = np.diff(a[:, :, :6], axis=2)
-names = ["transitions+stores", "scan+publish", "all-gather", "resolve", "next-state"]
-for i, nm in enumerate(names):
-    print(f"{nm:20s} median {np.median(d[:, :, i]):8.0f} cyc  p90 {np.percentile(d[:, :, i], 90):8.0f}")
-step = a[:, 1:, 0] - a[:, :-1, 0]
-print(f"{'step total':20s} median {np.median(step):8.0f} cyc")
-# skew between blocks at publish time
-pub = a[:, :, 2]
-print(f"publish skew across blocks (max-min) median {np.median(pub.max(0) - pub.min(0)):.0f} cyc")
+G = min(256, (B + 2047) // 2048)
+a = a[:G, 2:K - 2] * 10  # ns
+def rep(name, d):
+    per_step_max = d.max(0)
+    print(f"{name:34s} median {np.median(d):7.0f} ns  p90 {np.percentile(d, 90):7.0f}  "
+          f"max-over-blocks (median over steps) {np.median(per_step_max):7.0f}")
+rep("transitions (0->1)", a[:, :, 1] - a[:, :, 0])
+rep("B1 wait (1->2)", a[:, :, 2] - a[:, :, 1])
+rep("B1 -> exchange done (2->7)", a[:, :, 7] - a[:, :, 2])
+rep("exchange done -> B2 (7->4)", a[:, :, 4] - a[:, :, 7])
+rep("resets+advance (4->5)", a[:, :, 5] - a[:, :, 4])
+rep("step (0->next 0)", a[:, 1:, 0] - a[:, :-1, 0])
+pub, done = a[:, :, 6], a[:, :, 7]
+print(f"publish spread across blocks (max-min)   median {np.median(pub.max(0) - pub.min(0)):.0f} ns")
+print(f"exchange done - last publish             median {np.median(done - pub.max(0)[None, :]):.0f} ns")
+print(f"step start spread across blocks          median {np.median(a[:, :, 0].max(0) - a[:, :, 0].min(0)):.0f} ns")
+slow = pub.argmax(0)
+print("slowest publisher per step:", slow[:24].tolist())
+t01 = (a[:, :, 1] - a[:, :, 0])
+print("slowest transitions block per step:", t01.argmax(0)[:24].tolist())
+b0 = 0
+print("block 0 phases (ns) step 10:", np.diff(a[b0, 10, [0, 1, 2, 7, 4, 5]]).tolist())
+bs = int(slow[10])
+print(f"block {bs} phases (ns) step 10:", np.diff(a[bs, 10, [0, 1, 2, 7, 4, 5]]).tolist())
