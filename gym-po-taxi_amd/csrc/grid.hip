@@ -101,7 +101,6 @@ struct GridDev {
   unsigned long long* dbg;  // GP_STAMPS diagnostic builds: [G][64][8] s_memtime stamps
   GridLds lds;
   const GridDev* self;      // device copy of this struct (for out-of-line slow-path helpers)
-  int32_t diag;             // diagnostics (GP_DIAG env at build): bit0 = fused kernel skips output stores
   // philox / replay
   uint32_t key0, key1;
   const uint64_t* rp_u;
@@ -801,8 +800,10 @@ struct FusedShared {
   uint4 thr4[16];                // action-failure thresholds >> 21 (hi 32 bits), [a][j]
   uint64_t ns_hi, ns_lo;         // next step's s0
   uint32_t nh, nu;               // next step's has_uint32 / uinteger
+  uint32_t drawn;                // the control wave drew this step's resetter cells before B2
   uint32_t pos[FEPB];            // slow path: accepted-word positions of one tile's resetters
   uint32_t pos2[FEPB];
+  uint32_t cell[FMAXQ * FEPB];   // resetter cells (goal | agent << 16) by tile and rank
 };
 
 __device__ __forceinline__ uint64_t bgran(uint32_t tag, uint32_t rej, uint64_t counts) {
@@ -993,7 +994,7 @@ __device__ __forceinline__ void publish_next(const PcgJump* jt_lds, FusedShared&
 #ifdef GP_STAMPS
 #define STAMP(i)                                                                                  \
   do {                                                                                            \
-    if (threadIdx.x == ((i) == 3 ? FENVW * 64 : 0) && k < 64) {                                   \
+    if (threadIdx.x == 0 && k < 64) {                                                             \
       unsigned long long t_;                                                                      \
       asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");               \
       p_in.dbg[((size_t)blockIdx.x * 64 + k) * 8 + (i)] = t_;                                     \
@@ -1037,13 +1038,55 @@ __device__ __forceinline__ void lds_copy(char* dyn, const GridLdsTab& t, const T
 // Phase 4 of a fused step (both roles; every barrier here is block-uniform): the resetters'
 // choice() draws. CTRL = the control wave (coverage exchanges, stream walks, J_used of the
 // unusual cases); otherwise an env wave with its env state.
+// Control wave: the cells (goal | agent << 16) of this block's resetters, rank r of tile q ->
+// sh.cell[q*FEPB + r]. Word positions: fast path P_q + r (goal call) and w1 + P_q + r (agent
+// call); slow path (only_q >= 0: one tile) from the stream walk's position lists pg / pa.
+template <int QPT>
+__device__ __forceinline__ void ctrl_draw_cells(const GridDev& p, FusedShared& sh, const LTabs& tb, const u128 SB,
+                                                const Stream& st, uint32_t w1, const uint32_t* pg, const uint32_t* pa,
+                                                int only_q) {
+  const int lane = threadIdx.x & 63;
+  const bool rgoal = p.fixed_goal < 0, ragent = p.fixed_agent < 0;
+  const uint32_t mode = (rgoal ? 1u : 0u) | (ragent ? 2u : 0u);
+  const uint32_t ng = (uint32_t)p.n_goal_valid, na = (uint32_t)p.n_agent_valid;
+  uint32_t tc[QPT], cum[QPT + 1];
+  cum[0] = 0;
+#pragma unroll
+  for (int q = 0; q < QPT; ++q) {
+    uint32_t t = 0;
+#pragma unroll
+    for (int w = 0; w < FENVW; ++w) t += sh.wcnt[q][w];
+    const int tau = q * (int)gridDim.x + (int)blockIdx.x;
+    tc[q] = (tau < p.fnt && (only_q < 0 || only_q == q)) ? t : 0u;
+    cum[q + 1] = cum[q] + tc[q];
+  }
+  for (uint32_t idx = lane; idx < cum[QPT]; idx += 64) {
+    int q = 0;
+#pragma unroll
+    for (int j = 1; j < QPT; ++j) q += idx >= cum[j] ? 1 : 0;
+    const uint32_t r = idx - cum[q];
+    uint32_t wg, wa;
+    if (pg) {
+      wg = pg[r];
+      wa = pa[r];
+    } else {
+      wg = sh.tpre[q] + r;
+      wa = (rgoal ? w1 : 0u) + wg;
+    }
+    const uint32_t v = draw_cells(tb.jt(), SB, st.inc, st.h0, st.u0, 0u, wg, wa, mode, ng, na);
+    const uint32_t goal = rgoal ? (uint32_t)tb.gv((int)(v & 0xFFFFu)) : (uint32_t)p.fixed_goal;
+    const uint32_t agent = ragent ? (uint32_t)tb.av((int)(v >> 16)) : (uint32_t)p.fixed_agent;
+    sh.cell[q * FEPB + r] = goal | (agent << 16);
+  }
+}
+
+
 template <int OK, int QPT, bool CTRL>
 __device__ __forceinline__ void fused_resets(const GridDev& p, FusedShared& sh, const LTabs& tb, const Stream& st,
                                              const u128 SB, const PcgJump& jB, uint64_t* slots, uint32_t tag0,
                                              void* ob, uint32_t (&ae)[QPT][4], int (&gl)[QPT][4],
-                                             const uint32_t (&fm)[QPT], const uint32_t (&excl)[QPT],
-                                             const uint32_t (&wex)[QPT], const uint32_t (&wt)[QPT]) {
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+                                             const uint32_t (&fm)[QPT], const uint32_t (&excl)[QPT]) {
+  const int tid = threadIdx.x, lane = tid & 63;
   const int G = (int)gridDim.x, nt = p.fnt;
   const bool rgoal = p.fixed_goal < 0, ragent = p.fixed_agent < 0;
   const int ncalls = (int)rgoal + (int)ragent;
@@ -1051,12 +1094,37 @@ __device__ __forceinline__ void fused_resets(const GridDev& p, FusedShared& sh, 
   const uint32_t thr1 = rgoal ? p.thr_goal : p.thr_agent;
   const uint32_t b = sh.btot;
   if (!(ncalls && b)) return;
+  // env waves: take the resetters' cells the control wave drew for tile q
+  auto consume = [&](int q) {
+    if constexpr (!CTRL) {
+      if (fm[q]) {
+        const int env0 = (q * G + (int)blockIdx.x) * FEPB + tid * EPT;
+        uint32_t r = excl[q];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (!(fm[q] & (1u << i))) continue;
+          const uint32_t c = sh.cell[q * FEPB + r];
+          const int goal = (int)(c & 0xFFFFu), agent = (int)(c >> 16);
+          gl[q][i] = goal;
+          ae[q][i] = (uint32_t)agent;
+          write_obs<OK>(p, tb, env0 + i, agent, goal, ob);
+          ++r;
+        }
+      }
+    }
+  };
+  if (sh.drawn) {  // common case: drawn before B2
+#pragma unroll
+    for (int q = 0; q < QPT; ++q) consume(q);
+    return;
+  }
   uint32_t slow = sh.anyrej;
   if (!slow && b > (uint32_t)nt * RCOV)  // mass reset: extend call-1 coverage
-    slow = coverage_round(p.self, st, slots + G, nt, G, QPT, tag0 + 1, (uint32_t)nt * RCOV, b - nt * RCOV, n1, thr1, sh);
-  if (!slow && ncalls == 2)  // agent words start right after the b goal words
-    slow = coverage_round(p.self, st, slots + 2 * G, nt, G, QPT, tag0 + 2, b, b, (uint32_t)p.n_agent_valid, p.thr_agent,
+    slow = coverage_round(p.self, st, slots + G, nt, G, QPT, tag0 + 1, (uint32_t)nt * RCOV, b - nt * RCOV, n1, thr1,
                           sh);
+  if (!slow && ncalls == 2)  // agent words start right after the b goal words
+    slow = coverage_round(p.self, st, slots + 2 * G, nt, G, QPT, tag0 + 2, b, b, (uint32_t)p.n_agent_valid,
+                          p.thr_agent, sh);
   uint32_t w1 = b;
   if (slow && ncalls == 2) {
     if constexpr (CTRL) {
@@ -1066,95 +1134,32 @@ __device__ __forceinline__ void fused_resets(const GridDev& p, FusedShared& sh, 
     lds_barrier();
     w1 = sh.w1;
   }
-  const uint32_t mode = (rgoal ? 1u : 0u) | (ragent ? 2u : 0u);
-  const uint32_t ng = (uint32_t)p.n_goal_valid, na = (uint32_t)p.n_agent_valid;
   if (!slow) {
-    if constexpr (!CTRL) {
-      // fast path: the wave's resetters are compacted in LDS, one draw per lane per pass
-      uint32_t* rj = sh.pos + wid * 256;
-      uint32_t* rv = sh.pos2 + wid * 256;
-      uint32_t R = 0, cb[QPT];
+    if constexpr (CTRL) ctrl_draw_cells<QPT>(p, sh, tb, SB, st, w1, nullptr, nullptr, -1);
+    lds_barrier();
 #pragma unroll
-      for (int q = 0; q < QPT; ++q) {
-        cb[q] = R + wex[q];
-        R += wt[q];
-      }
-      for (uint32_t c0 = 0; c0 < R; c0 += 256) {
-#pragma unroll
-        for (int q = 0; q < QPT; ++q) {
-          uint32_t m = fm[q], c = cb[q], lr = excl[q];
-          const uint32_t P = sh.tpre[q];
-          while (m) {
-            if (c - c0 < 256u) rj[c - c0] = P + lr;
-            m &= m - 1;
-            ++c;
-            ++lr;
-          }
-        }
-        wave_lds_sync();
-        const uint32_t nr = min(R - c0, 256u);
-        for (uint32_t l = lane; l < nr; l += 64) {
-          const uint32_t j = rj[l];
-          rv[l] = draw_cells(tb.jt(), st.s0, st.inc, st.h0, st.u0, st.U0, j, (rgoal ? w1 : 0u) + j, mode, ng, na);
-        }
-        wave_lds_sync();
-#pragma unroll
-        for (int q = 0; q < QPT; ++q) {
-          const int env0 = (q * G + (int)blockIdx.x) * FEPB + tid * EPT;
-          uint32_t c = cb[q];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            if (!(fm[q] & (1u << i))) continue;
-            if (c - c0 < 256u) {
-              const uint32_t v = rv[c - c0];
-              const int goal = rgoal ? (int)tb.gv((int)(v & 0xFFFFu)) : gl[q][i];
-              const int agent = ragent ? (int)tb.av((int)(v >> 16)) : (int)(ae[q][i] & 0xFFFFu);
-              gl[q][i] = goal;
-              ae[q][i] = (uint32_t)agent;
-              write_obs<OK>(p, tb, env0 + i, agent, goal, ob);
-            }
-            ++c;
-          }
-        }
-        wave_lds_sync();  // rj/rv reused by the next pass
-      }
-    }
+    for (int q = 0; q < QPT; ++q) consume(q);
   } else {
     // slow path (a rejection somewhere): the control wave walks the stream tile by tile
 #pragma unroll
     for (int q = 0; q < QPT; ++q) {
       const int tau = q * G + (int)blockIdx.x;
       if (tau >= nt) continue;  // block-uniform
-      const uint32_t P = sh.tpre[q];
       if constexpr (CTRL) {
+        const uint32_t P = sh.tpre[q];
         uint32_t tc = 0;
 #pragma unroll
         for (int w = 0; w < FENVW; ++w) tc += sh.wcnt[q][w];
         if (tc) {
-          if (rgoal) scan_accepted(p.self, st, 0, ng, p.thr_goal, P, P + tc, sh.pos);
-          if (ragent) scan_accepted(p.self, st, rgoal ? w1 : 0, na, p.thr_agent, P, P + tc, rgoal ? sh.pos2 : sh.pos);
+          if (rgoal) scan_accepted(p.self, st, 0, n1, p.thr_goal, P, P + tc, sh.pos);
+          if (ragent)
+            scan_accepted(p.self, st, rgoal ? w1 : 0, (uint32_t)p.n_agent_valid, p.thr_agent, P, P + tc,
+                          rgoal ? sh.pos2 : sh.pos);
         }
+        ctrl_draw_cells<QPT>(p, sh, tb, SB, st, w1, sh.pos, rgoal ? sh.pos2 : sh.pos, q);
       }
       lds_barrier();
-      if constexpr (!CTRL) {
-        if (fm[q]) {
-          const int env0 = tau * FEPB + tid * EPT;
-          uint32_t lr = excl[q];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            if (!(fm[q] & (1u << i))) continue;
-            const uint32_t wg = sh.pos[lr], wa = rgoal ? sh.pos2[lr] : sh.pos[lr];
-            const uint32_t v = draw_cells(tb.jt(), st.s0, st.inc, st.h0, st.u0, st.U0, wg, wa, mode, ng, na);
-            const int goal = rgoal ? (int)tb.gv((int)(v & 0xFFFFu)) : gl[q][i];
-            const int agent = ragent ? (int)tb.av((int)(v >> 16)) : (int)(ae[q][i] & 0xFFFFu);
-            gl[q][i] = goal;
-            ae[q][i] = (uint32_t)agent;
-            write_obs<OK>(p, tb, env0 + i, agent, goal, ob);
-            ++lr;
-          }
-        }
-      }
-      lds_barrier();  // sh.pos reused by the next tile
+      consume(q);
     }
   }
   if (!sh.known) {  // block-uniform: the slow / multi-call / extended cases
@@ -1164,14 +1169,15 @@ __device__ __forceinline__ void fused_resets(const GridDev& p, FusedShared& sh, 
         wtot = (uint32_t)ncalls * b;
       } else {
         const bool last_goal = ncalls == 1 && rgoal;
-        wtot = scan_accepted(p.self, st, ncalls == 2 ? w1 : 0u, last_goal ? ng : na, last_goal ? p.thr_goal : p.thr_agent,
-                             b - 1, b, nullptr);
+        wtot = scan_accepted(p.self, st, ncalls == 2 ? w1 : 0u, last_goal ? n1 : (uint32_t)p.n_agent_valid,
+                             last_goal ? p.thr_goal : p.thr_agent, b - 1, b, nullptr);
       }
       publish_next(tb.jt(), sh, SB, jB, wtot, st.h0, st.u0, lane == 0);
     }
     lds_barrier();
   }
 }
+
 
 // Effective action of env with action a and 53-bit uniform k: #{j : k > thr[a][j]} (integer form
 // of action_utils.py:84-90), on the high 32 bits with an exact 64-bit fallback on a tie.
@@ -1311,34 +1317,29 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
     // ---- 3. this step's outputs (overlap the exchange) ----
     const size_t off = (size_t)k * B;
     void* ob = (uint8_t*)obs + off * ow;
-    if (!(p.diag & 1)) {
 #pragma unroll
-      for (int q = 0; q < QPT; ++q) {
-        const int env0 = (q * G + (int)blockIdx.x) * FEPB + tid * EPT;
-        uint8_t tm[4], tr[4];
-        int ag[4];
+    for (int q = 0; q < QPT; ++q) {
+      const int env0 = (q * G + (int)blockIdx.x) * FEPB + tid * EPT;
+      uint8_t tm[4], tr[4];
+      int ag[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          tm[i] = (uint8_t)((tmm[q] >> i) & 1u);
-          tr[i] = (uint8_t)((trm[q] >> i) & 1u);
-          ag[i] = (int)(ae[q][i] & 0xFFFFu);
-        }
-        store4<float>(rew + off, env0, B, r[q]);
-        store4<uint8_t>(term + off, env0, B, tm);
-        store4<uint8_t>(trunc + off, env0, B, tr);
-        if (fm[q] == 0 || ncalls == 0) {
-          write_obs4<OK>(p, tb, env0, ag, gl[q], ob);
-        } else {
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (!(fm[q] & (1u << i)) && env0 + i < B) write_obs<OK>(p, tb, env0 + i, ag[i], gl[q][i], ob);
-        }
+      for (int i = 0; i < 4; ++i) {
+        tm[i] = (uint8_t)((tmm[q] >> i) & 1u);
+        tr[i] = (uint8_t)((trm[q] >> i) & 1u);
+        ag[i] = (int)(ae[q][i] & 0xFFFFu);
       }
+      store4<float>(rew + off, env0, B, r[q]);
+      store4<uint8_t>(term + off, env0, B, tm);
+      store4<uint8_t>(trunc + off, env0, B, tr);
+      // one vector store for all 4 envs (uniform store count per step: no vmcnt(0) at merges);
+      // a resetter's obs is provisional here and rewritten in phase 4
+      write_obs4<OK>(p, tb, env0, ag, gl[q], ob);
     }
     lds_barrier();  // B2: the exchange result is in LDS
     STAMP(4);
     // ---- 4. the resetters' draws ----
-    fused_resets<OK, QPT, false>(p, sh, tb, st, st.s0, jB_unused, slots, tag0, ob, ae, gl, fm, excl, wex, wt);
+    fused_resets<OK, QPT, false>(p, sh, tb, st, st.s0, jB_unused, slots, tag0, ob, ae, gl, fm, excl);
+    STAMP(3);
     // ---- 5. advance: lane states jump by J_used o J_B ----
     {
       const PcgJump jt{sh.ju[0], sh.ju[1], sh.ju[2], sh.ju[3]};
@@ -1449,7 +1450,7 @@ __device__ __forceinline__ void fused_ctrl(const GridDev& p_in, FusedShared& sh,
     // ---- 3. exchange: block 0 aggregates and publishes one tagged word per tile
     // {rejection, b, tile prefix}; every other block polls only its own QPT words ----
     uint64_t* tw = p.fslot + (size_t)6 * G + (size_t)((step_base + (uint32_t)k) & 1u) * nt;
-    uint32_t b, anyr;
+    uint32_t b, anyr, mypre = 0;  // lane q < QPT: global prefix of tile q
     if (blockIdx.x == 0) {
       uint64_t g[4];
       gather_blocks(p, slots, G, tag0, g);
@@ -1482,9 +1483,10 @@ __device__ __forceinline__ void fused_ctrl(const GridDev& p_in, FusedShared& sh,
           if (blk < G && tau < nt)
             __hip_atomic_store(&tw[tau], tword(tag0, anyr, b, pre[q][j]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-      if (lane == 0) {
 #pragma unroll
-        for (int q = 0; q < QPT; ++q) sh.tpre[q] = pre[q][0];
+      for (int q = 0; q < QPT; ++q) {
+        const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)pre[q][0], 0);
+        if (lane == q) mypre = v;
       }
     } else {
       uint64_t w = 0;
@@ -1502,7 +1504,7 @@ __device__ __forceinline__ void fused_ctrl(const GridDev& p_in, FusedShared& sh,
             break;
           }
         }
-        sh.tpre[lane] = (uint32_t)w & 0xFFFFFFu;
+        mypre = (uint32_t)w & 0xFFFFFFu;
       }
       const uint64_t w0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(w >> 32), 0) << 32) |
                           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)w, 0);
@@ -1510,18 +1512,21 @@ __device__ __forceinline__ void fused_ctrl(const GridDev& p_in, FusedShared& sh,
       anyr = (uint32_t)(w0 >> 48) & 1u;
     }
     const bool known = b == 0 || ncalls == 0 || (!anyr && ncalls == 1 && b <= (uint32_t)nt * RCOV);
+    const bool drawn = known && ncalls == 1 && b > 0;
+    if (lane < QPT) sh.tpre[lane] = mypre;
+    wave_lds_sync();
+    if (drawn) ctrl_draw_cells<QPT>(p, sh, tb, SB, st, 0u, nullptr, nullptr, -1);  // before B2
     if (known) publish_next(tb.jt(), sh, SB, jB, ncalls ? b : 0u, st.h0, st.u0, lane == 0);
     if (lane == 0) {
       sh.btot = b;
       sh.anyrej = anyr;
       sh.known = known ? 1u : 0u;
+      sh.drawn = drawn ? 1u : 0u;
       RSTAMP(7);
     }
-    STAMP(3);
     lds_barrier();  // B2
     // ---- 4. coverage exchanges / stream walks of the unusual cases ----
-    fused_resets<OK, QPT, true>(p, sh, tb, st, SB, jB, slots, tag0, nullptr, dummy_u, dummy_i, dummy_c, dummy_c,
-                                dummy_c, dummy_c);
+    fused_resets<OK, QPT, true>(p, sh, tb, st, SB, jB, slots, tag0, nullptr, dummy_u, dummy_i, dummy_c, dummy_c);
     // ---- 5. advance ----
     {
       const PcgJump jt{sh.ju[0], sh.ju[1], sh.ju[2], sh.ju[3]};
@@ -2279,10 +2284,6 @@ int GridBackend::build(const gp_grid_config* cfg) {
   }
   // fused numpy rollout: one 512-thread block per CU, <= 4 tiles of 2048 envs per block
   d.fnt = (int)((B + FEPB - 1) / FEPB);
-  {
-    const char* dg = getenv("GP_DIAG");
-    d.diag = dg ? atoi(dg) : 0;
-  }
   {
     hipDeviceProp_t prop;
     GP_HIP_CHECK(hipGetDeviceProperties(&prop, device));

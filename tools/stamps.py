@@ -2,7 +2,7 @@
 
     python gym-po-taxi_amd/build.py --stamps && python tools/stamps.py [B]
 All stamps are s_memrealtime (100 MHz, synchronous across XCDs), per block and step:
-0 step start (env wave 0), 1 transitions done, 2 B1 passed, 3 exchange done (control wave),
+0 step start (env wave 0), 1 transitions done, 2 B1 passed, 3 resets done (env wave 0),
 4 B2 passed, 5 step end, 6 granule published (control wave), 7 exchange done (control wave).
 """
 import ctypes
@@ -42,7 +42,8 @@ rep("transitions (0->1)", a[:, :, 1] - a[:, :, 0])
 rep("B1 wait (1->2)", a[:, :, 2] - a[:, :, 1])
 rep("B1 -> exchange done (2->7)", a[:, :, 7] - a[:, :, 2])
 rep("exchange done -> B2 (7->4)", a[:, :, 4] - a[:, :, 7])
-rep("resets+advance (4->5)", a[:, :, 5] - a[:, :, 4])
+rep("resets (4->3)", a[:, :, 3] - a[:, :, 4])
+rep("advance (3->5)", a[:, :, 5] - a[:, :, 3])
 rep("step (0->next 0)", a[:, 1:, 0] - a[:, :-1, 0])
 pub, done = a[:, :, 6], a[:, :, 7]
 print(f"publish spread across blocks (max-min)   median {np.median(pub.max(0) - pub.min(0)):.0f} ns")
