@@ -55,7 +55,7 @@ struct GridLdsTab {
 };
 struct GridLds {  // where the fused kernel stages the lookup tables in dynamic LDS
   int32_t total;
-  GridLdsTab move, hbase, hvec, t1, t2, coords, window, gv, av, doff, jt;
+  GridLdsTab move, hbase, hvec, t1, t2, coords, window, gv, av, doff, jt, jt8;
 };
 
 struct GridDev {
@@ -101,6 +101,8 @@ struct GridDev {
   unsigned long long* dbg;  // GP_STAMPS diagnostic builds: [G][64][8] s_memtime stamps
   GridLds lds;
   const GridDev* self;      // device copy of this struct (for out-of-line slow-path helpers)
+  const PcgJump* jt8;       // [2][256] radix-256 jumps: d and 256*d steps (fused kernel: jumps < 2^16)
+  int32_t xmode;            // fused exchange: 0 = block-0 aggregator + per-tile words, 1 = all-gather
   // philox / replay
   uint32_t key0, key1;
   const uint64_t* rp_u;
@@ -191,6 +193,7 @@ struct LTabs {
   __device__ __forceinline__ uint16_t gv(int i) const { return at<uint16_t>(p.lds.gv, i); }
   __device__ __forceinline__ uint16_t av(int i) const { return at<uint16_t>(p.lds.av, i); }
   __device__ __forceinline__ const PcgJump* jt() const { return reinterpret_cast<const PcgJump*>(dyn + p.lds.jt.off); }
+  __device__ __forceinline__ const PcgJump* jt8() const { return reinterpret_cast<const PcgJump*>(dyn + p.lds.jt8.off); }
 };
 
 // ------------------------------------------------------------------ observation builders ----
@@ -796,7 +799,8 @@ struct FusedShared {
   uint32_t wrej;                 // speculative-check rejection (control wave)
   uint32_t tpre[FMAXQ];          // global exclusive prefix of this block's tiles
   uint32_t btot, anyrej, known, flag, w1;
-  uint64_t ju[4];                // lane-state advance J_used o J_B (a_hi, a_lo, c_hi, c_lo)
+  uint64_t ju[4];                // this step's J_used (a_hi, a_lo, c_hi, c_lo)
+  uint64_t jB[4];                // J_B: jump by num_envs
   uint4 thr4[16];                // action-failure thresholds >> 21 (hi 32 bits), [a][j]
   uint64_t ns_hi, ns_lo;         // next step's s0
   uint32_t nh, nu;               // next step's has_uint32 / uinteger
@@ -845,23 +849,6 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
 }
 
-// The choice() draws of one resetter: Lemire values of word wg (goal call, mode bit 0, n = ng)
-// and word wa (agent call, mode bit 1, n = na) -> goal index | agent index << 16. Out of line:
-// it is the only place the fused kernel needs a full jump from s0 per lane.
-__device__ __forceinline__ uint32_t draw_cells(const PcgJump* jt, u128 s0, u128 inc, uint32_t h0, uint32_t u0,
-                                            uint32_t U0, uint32_t wg, uint32_t wa, uint32_t mode, uint32_t ng,
-                                            uint32_t na) {
-  auto word = [&](uint32_t w) -> uint32_t {
-    if (h0 && w == 0) return u0;
-    const uint32_t ww = w - h0;
-    const uint64_t x = pcg_output(pcg_jump(jt, s0, U0 + (ww >> 1) + 1));
-    return (ww & 1) ? (uint32_t)(x >> 32) : (uint32_t)x;
-  };
-  uint32_t v = 0;
-  if (mode & 1u) v |= lemire_value(word(wg), ng);
-  if (mode & 2u) v |= lemire_value(word(wa), na) << 16;
-  return v;
-}
 
 // Wave 0: poll the G block granules of one round (lane l holds blocks 4l..4l+3) until every one
 // carries `tag`. Granules of blocks >= G read as 0.
@@ -963,6 +950,38 @@ __device__ __forceinline__ PcgJump jump_params(const PcgJump* jt, uint32_t n) {
   return j;
 }
 
+// Jump by n steps: two radix-256 entries (both loads issued up front) for n < 2^16, else the
+// radix-64 tables.
+__device__ __forceinline__ u128 jump_small(const PcgJump* t8, const PcgJump* t64, u128 s, uint32_t n) {
+  if (n < 65536u) {
+    const PcgJump j0 = t8[n & 255u], j1 = t8[256u + (n >> 8)];
+    return apply_jump(j1, apply_jump(j0, s));
+  }
+  return pcg_jump(t64, s, n);
+}
+__device__ __forceinline__ PcgJump jparams_small(const PcgJump* t8, const PcgJump* t64, uint32_t n) {
+  if (n < 65536u) return compose_jump(t8[256u + (n >> 8)], t8[n & 255u]);
+  return jump_params(t64, n);
+}
+
+// The choice() draws of one resetter: Lemire values of word wg (goal call, mode bit 0, n = ng)
+// and word wa (agent call, mode bit 1, n = na) -> goal index | agent index << 16. Out of line:
+// it is the only place the fused kernel needs a full jump from s0 per lane.
+__device__ __forceinline__ uint32_t draw_cells(const PcgJump* jt8, const PcgJump* jt, u128 SB, uint32_t h0,
+                                            uint32_t u0, uint32_t wg, uint32_t wa, uint32_t mode, uint32_t ng,
+                                            uint32_t na) {
+  auto word = [&](uint32_t w) -> uint32_t {
+    if (h0 && w == 0) return u0;
+    const uint32_t ww = w - h0;
+    const uint64_t x = pcg_output(jump_small(jt8, jt, SB, (ww >> 1) + 1));
+    return (ww & 1) ? (uint32_t)(x >> 32) : (uint32_t)x;
+  };
+  uint32_t v = 0;
+  if (mode & 1u) v |= lemire_value(word(wg), ng);
+  if (mode & 2u) v |= lemire_value(word(wa), na) << 16;
+  return v;
+}
+
 // numpy next_uint32 bookkeeping after `wtot` 32-bit words: u64 draws used and the new buffer flag.
 __device__ __forceinline__ void words_to_draws(uint32_t wtot, uint32_t h0, uint32_t& used, uint32_t& h) {
   if (wtot == 0) {
@@ -975,17 +994,16 @@ __device__ __forceinline__ void words_to_draws(uint32_t wtot, uint32_t h0, uint3
 }
 
 // Publish (to LDS) the next step's state: s0' = J_used(SB), buffered half. One lane writes.
-__device__ __forceinline__ void publish_next(const PcgJump* jt_lds, FusedShared& sh, const u128 SB, const PcgJump jB,
-                                            uint32_t wtot, uint32_t h0, uint32_t u0, bool writer) {
+__device__ __forceinline__ void publish_next(const LTabs& tb, FusedShared& sh, const u128 SB, uint32_t wtot,
+                                            uint32_t h0, uint32_t u0, bool writer) {
   uint32_t used, h;
   words_to_draws(wtot, h0, used, h);
-  const PcgJump ju = jump_params(jt_lds, used);
-  const u128 s = apply_jump(ju, SB);
+  const PcgJump ju = jparams_small(tb.jt8(), tb.jt(), used);
+  const u128 s = jump_small(tb.jt8(), tb.jt(), SB, used);
   // numpy keeps the last buffered half in `uinteger` even after it has been consumed
   const uint32_t u = used ? (uint32_t)(pcg_output(s) >> 32) : u0;
-  const PcgJump jt = used ? compose_jump(ju, jB) : jB;  // lane states advance by J_used o J_B
   if (writer) {
-    sh.ju[0] = jt.a_hi; sh.ju[1] = jt.a_lo; sh.ju[2] = jt.c_hi; sh.ju[3] = jt.c_lo;
+    sh.ju[0] = ju.a_hi; sh.ju[1] = ju.a_lo; sh.ju[2] = ju.c_hi; sh.ju[3] = ju.c_lo;
     sh.ns_hi = hi64(s); sh.ns_lo = lo64(s);
     sh.nh = h; sh.nu = u;
   }
@@ -997,7 +1015,7 @@ __device__ __forceinline__ void publish_next(const PcgJump* jt_lds, FusedShared&
     if (threadIdx.x == 0 && k < 64) {                                                             \
       unsigned long long t_;                                                                      \
       asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");               \
-      p_in.dbg[((size_t)blockIdx.x * 64 + k) * 8 + (i)] = t_;                                     \
+      p_in.dbg[((size_t)blockIdx.x * 64 + k) * 16 + (i)] = t_;                                    \
     }                                                                                             \
   } while (0)
 // wall-clock (100 MHz, chip-synchronous) stamp by the calling lane
@@ -1006,7 +1024,7 @@ __device__ __forceinline__ void publish_next(const PcgJump* jt_lds, FusedShared&
     if (k < 64) {                                                                                 \
       unsigned long long t_;                                                                      \
       asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");               \
-      p_in.dbg[((size_t)blockIdx.x * 64 + k) * 8 + (i)] = t_;                                     \
+      p_in.dbg[((size_t)blockIdx.x * 64 + k) * 16 + (i)] = t_;                                    \
     }                                                                                             \
   } while (0)
 #else
@@ -1073,7 +1091,7 @@ __device__ __forceinline__ void ctrl_draw_cells(const GridDev& p, FusedShared& s
       wg = sh.tpre[q] + r;
       wa = (rgoal ? w1 : 0u) + wg;
     }
-    const uint32_t v = draw_cells(tb.jt(), SB, st.inc, st.h0, st.u0, 0u, wg, wa, mode, ng, na);
+    const uint32_t v = draw_cells(tb.jt8(), tb.jt(), SB, st.h0, st.u0, wg, wa, mode, ng, na);
     const uint32_t goal = rgoal ? (uint32_t)tb.gv((int)(v & 0xFFFFu)) : (uint32_t)p.fixed_goal;
     const uint32_t agent = ragent ? (uint32_t)tb.av((int)(v >> 16)) : (uint32_t)p.fixed_agent;
     sh.cell[q * FEPB + r] = goal | (agent << 16);
@@ -1084,8 +1102,9 @@ __device__ __forceinline__ void ctrl_draw_cells(const GridDev& p, FusedShared& s
 template <int OK, int QPT, bool CTRL>
 __device__ __forceinline__ void fused_resets(const GridDev& p, FusedShared& sh, const LTabs& tb, const Stream& st,
                                              const u128 SB, const PcgJump& jB, uint64_t* slots, uint32_t tag0,
-                                             void* ob, uint32_t (&ae)[QPT][4], int (&gl)[QPT][4],
-                                             const uint32_t (&fm)[QPT], const uint32_t (&excl)[QPT]) {
+                                             uint32_t (&ae)[QPT][4], int (&gl)[QPT][4], const uint32_t (&fm)[QPT],
+                                             const uint32_t (&excl)[QPT], uint32_t (&pc)[QPT][4],
+                                             uint32_t (&pfm)[QPT]) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int G = (int)gridDim.x, nt = p.fnt;
   const bool rgoal = p.fixed_goal < 0, ragent = p.fixed_agent < 0;
@@ -1097,20 +1116,23 @@ __device__ __forceinline__ void fused_resets(const GridDev& p, FusedShared& sh, 
   // env waves: take the resetters' cells the control wave drew for tile q
   auto consume = [&](int q) {
     if constexpr (!CTRL) {
-      if (fm[q]) {
-        const int env0 = (q * G + (int)blockIdx.x) * FEPB + tid * EPT;
-        uint32_t r = excl[q];
+      // the resetters' new cells (independent LDS loads); their obs are written in the next step's
+      // output phase, off the critical path (pc / pfm)
+      uint32_t r = excl[q];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          if (!(fm[q] & (1u << i))) continue;
-          const uint32_t c = sh.cell[q * FEPB + r];
-          const int goal = (int)(c & 0xFFFFu), agent = (int)(c >> 16);
-          gl[q][i] = goal;
-          ae[q][i] = (uint32_t)agent;
-          write_obs<OK>(p, tb, env0 + i, agent, goal, ob);
-          ++r;
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t bit = (fm[q] >> i) & 1u;
+        pc[q][i] = sh.cell[q * FEPB + min(r, (uint32_t)FEPB - 1u)];
+        r += bit;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if ((fm[q] >> i) & 1u) {
+          gl[q][i] = (int)(pc[q][i] & 0xFFFFu);
+          ae[q][i] = pc[q][i] >> 16;
         }
       }
+      pfm[q] = fm[q];
     }
   };
   if (sh.drawn) {  // common case: drawn before B2
@@ -1172,7 +1194,7 @@ __device__ __forceinline__ void fused_resets(const GridDev& p, FusedShared& sh, 
         wtot = scan_accepted(p.self, st, ncalls == 2 ? w1 : 0u, last_goal ? n1 : (uint32_t)p.n_agent_valid,
                              last_goal ? p.thr_goal : p.thr_agent, b - 1, b, nullptr);
       }
-      publish_next(tb.jt(), sh, SB, jB, wtot, st.h0, st.u0, lane == 0);
+      publish_next(tb, sh, SB, wtot, st.h0, st.u0, lane == 0);
     }
     lds_barrier();
   }
@@ -1199,6 +1221,22 @@ __device__ __forceinline__ uint32_t fused_effective_action(const FusedShared& sh
     for (int j = 0; j < NA; ++j) e += (k > s_thr[a * NA + j]) ? 1u : 0u;
   }
   return min(e, (uint32_t)NA - 1);
+}
+
+// The obs of the previous step's resetters (their provisional obs were stored with the step's
+// outputs): written during the next step's exchange wait.
+template <int OK, int QPT>
+__device__ __forceinline__ void flush_reset_obs(const GridDev& p, const LTabs& tb, void* ob, int tid,
+                                                const uint32_t (&pc)[QPT][4], uint32_t (&pfm)[QPT]) {
+#pragma unroll
+  for (int q = 0; q < QPT; ++q) {
+    if (!pfm[q]) continue;
+    const int env0 = (q * (int)gridDim.x + (int)blockIdx.x) * FEPB + tid * EPT;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if ((pfm[q] >> i) & 1u) write_obs<OK>(p, tb, env0 + i, (int)(pc[q][i] >> 16), (int)(pc[q][i] & 0xFFFFu), ob);
+    pfm[q] = 0;
+  }
 }
 
 // The env waves of the fused kernel.
@@ -1231,10 +1269,12 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
   int gl[QPT][4];
   int32_t a_cur[QPT][4];
   u128 S[QPT];  // lane draw state: jump(s0, e0 + 1)
+  uint32_t pc[QPT][4], pfm[QPT];  // previous step's resetters: new cells (goal | agent << 16), masks
 #pragma unroll
   for (int q = 0; q < QPT; ++q) {
     const int tau = q * G + (int)blockIdx.x;
     const int env0 = tau * FEPB + tid * EPT;
+    pfm[q] = 0;
     load4<uint32_t>(p.ae, env0, B, ae[q]);
     if (rgoal) {
       uint16_t gg[4];
@@ -1335,12 +1375,18 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
       // a resetter's obs is provisional here and rewritten in phase 4
       write_obs4<OK>(p, tb, env0, ag, gl[q], ob);
     }
+    if (k > 0) flush_reset_obs<OK, QPT>(p, tb, (uint8_t*)obs + (off - B) * ow, tid, pc, pfm);
+    {
+      const PcgJump jB{sh.jB[0], sh.jB[1], sh.jB[2], sh.jB[3]};
+#pragma unroll
+      for (int q = 0; q < QPT; ++q) S[q] = apply_jump(jB, S[q]);  // first half of the advance (J_B)
+    }
     lds_barrier();  // B2: the exchange result is in LDS
     STAMP(4);
     // ---- 4. the resetters' draws ----
-    fused_resets<OK, QPT, false>(p, sh, tb, st, st.s0, jB_unused, slots, tag0, ob, ae, gl, fm, excl);
+    fused_resets<OK, QPT, false>(p, sh, tb, st, st.s0, jB_unused, slots, tag0, ae, gl, fm, excl, pc, pfm);
     STAMP(3);
-    // ---- 5. advance: lane states jump by J_used o J_B ----
+    // ---- 5. advance: lane states jump by J_used (J_B was applied while waiting for the exchange) ----
     {
       const PcgJump jt{sh.ju[0], sh.ju[1], sh.ju[2], sh.ju[3]};
       st.s0 = mk128(sh.ns_hi, sh.ns_lo);
@@ -1357,6 +1403,7 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
     }
     STAMP(5);
   }
+  if (K > 0) flush_reset_obs<OK, QPT>(p, tb, (uint8_t*)obs + (size_t)(K - 1) * B * ow, tid, pc, pfm);
 #pragma unroll
   for (int q = 0; q < QPT; ++q) {
     const int env0 = (q * G + (int)blockIdx.x) * FEPB + tid * EPT;
@@ -1408,6 +1455,7 @@ __device__ __forceinline__ void fused_ctrl(const GridDev& p_in, FusedShared& sh,
   uint32_t dummy_u[QPT][4];
   int dummy_i[QPT][4];
   const uint32_t dummy_c[QPT] = {};
+  uint32_t dummy_p[QPT] = {};
   for (int k = 0; k < K; ++k) {
     const uint32_t tag0 = (step_base + (uint32_t)k + 1u) * 4u;
     uint64_t* slots = p.fslot + (size_t)((step_base + (uint32_t)k) & 1u) * 3 * G;
@@ -1447,13 +1495,17 @@ __device__ __forceinline__ void fused_ctrl(const GridDev& p_in, FusedShared& sh,
       __hip_atomic_store(&slots[blockIdx.x], bgran(tag0, wrej, counts), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       RSTAMP(6);
     }
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+      if (chk[c]) CS[c] = apply_jump(jB, CS[c]);
     // ---- 3. exchange: block 0 aggregates and publishes one tagged word per tile
     // {rejection, b, tile prefix}; every other block polls only its own QPT words ----
     uint64_t* tw = p.fslot + (size_t)6 * G + (size_t)((step_base + (uint32_t)k) & 1u) * nt;
     uint32_t b, anyr, mypre = 0;  // lane q < QPT: global prefix of tile q
-    if (blockIdx.x == 0) {
+    if (blockIdx.x == 0 || p.xmode == 1) {
       uint64_t g[4];
       gather_blocks(p, slots, G, tag0, g);
+      if (lane == 0) RSTAMP(10);
       uint32_t rj = 0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) rj |= (uint32_t)(g[j] >> 48) & 1u;
@@ -1475,17 +1527,22 @@ __device__ __forceinline__ void fused_ctrl(const GridDev& p_in, FusedShared& sh,
         acc += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
       }
       b = acc;
+      if (p.xmode == 0) {
 #pragma unroll
-      for (int q = 0; q < QPT; ++q)
+        for (int q = 0; q < QPT; ++q)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int blk = lane * 4 + j, tau = q * G + blk;
-          if (blk < G && tau < nt)
-            __hip_atomic_store(&tw[tau], tword(tag0, anyr, b, pre[q][j]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+          for (int j = 0; j < 4; ++j) {
+            const int blk = lane * 4 + j, tau = q * G + blk;
+            if (blk < G && tau < nt)
+              __hip_atomic_store(&tw[tau], tword(tag0, anyr, b, pre[q][j]), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+          }
+      }
+      const int bl = (int)blockIdx.x >> 2, bj = (int)blockIdx.x & 3;
 #pragma unroll
       for (int q = 0; q < QPT; ++q) {
-        const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)pre[q][0], 0);
+        const uint32_t sel = bj == 0 ? pre[q][0] : bj == 1 ? pre[q][1] : bj == 2 ? pre[q][2] : pre[q][3];
+        const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)sel, bl);
         if (lane == q) mypre = v;
       }
     } else {
@@ -1511,12 +1568,14 @@ __device__ __forceinline__ void fused_ctrl(const GridDev& p_in, FusedShared& sh,
       b = (uint32_t)(w0 >> 24) & 0xFFFFFFu;
       anyr = (uint32_t)(w0 >> 48) & 1u;
     }
+    if (lane == 0) RSTAMP(8);
     const bool known = b == 0 || ncalls == 0 || (!anyr && ncalls == 1 && b <= (uint32_t)nt * RCOV);
     const bool drawn = known && ncalls == 1 && b > 0;
     if (lane < QPT) sh.tpre[lane] = mypre;
     wave_lds_sync();
     if (drawn) ctrl_draw_cells<QPT>(p, sh, tb, SB, st, 0u, nullptr, nullptr, -1);  // before B2
-    if (known) publish_next(tb.jt(), sh, SB, jB, ncalls ? b : 0u, st.h0, st.u0, lane == 0);
+    if (lane == 0) RSTAMP(9);
+    if (known) publish_next(tb, sh, SB, ncalls ? b : 0u, st.h0, st.u0, lane == 0);
     if (lane == 0) {
       sh.btot = b;
       sh.anyrej = anyr;
@@ -1526,7 +1585,8 @@ __device__ __forceinline__ void fused_ctrl(const GridDev& p_in, FusedShared& sh,
     }
     lds_barrier();  // B2
     // ---- 4. coverage exchanges / stream walks of the unusual cases ----
-    fused_resets<OK, QPT, true>(p, sh, tb, st, SB, jB, slots, tag0, nullptr, dummy_u, dummy_i, dummy_c, dummy_c);
+    fused_resets<OK, QPT, true>(p, sh, tb, st, SB, jB, slots, tag0, dummy_u, dummy_i, dummy_c, dummy_c, dummy_u,
+                                dummy_p);
     // ---- 5. advance ----
     {
       const PcgJump jt{sh.ju[0], sh.ju[1], sh.ju[2], sh.ju[3]};
@@ -1573,6 +1633,8 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
   lds_copy(dyn, p.lds.av, p.agent_valid);
   lds_copy(dyn, p.lds.doff, p.doff);
   lds_copy(dyn, p.lds.jt, p.jt);
+  lds_copy(dyn, p.lds.jt8, p.jt8);
+  if (tid < 4) sh.jB[tid] = (&p.fjB->a_hi)[tid];
   const LTabs tb{p_in, dyn};
   __syncthreads();
   float rsum = 0.f;
@@ -1754,7 +1816,7 @@ struct GridBackend : EnvBackend {
   std::vector<int32_t> cells;
   std::vector<uint16_t> goal_valid_h, agent_valid_h;
   DevBuf b_move, b_thr, b_gv, b_av, b_hbase, b_doff, b_hvec, b_t1, b_t2, b_coords, b_window, b_jt, b_lt4, b_lt2,
-      b_tja, b_tjw, b_ae, b_goal, b_ctl, b_tcount, b_tlist, b_rflag, b_mslot, b_ftj, b_flt4, b_fjB, b_fslot, b_dbg, b_self;
+      b_tja, b_tjw, b_ae, b_goal, b_ctl, b_tcount, b_tlist, b_rflag, b_mslot, b_ftj, b_flt4, b_fjB, b_fslot, b_dbg, b_self, b_jt8;
   int fused_G = 0, fused_qpt = 0;  // fused numpy rollout geometry (0 = not eligible)
   // replay pointers for the next step
   const uint64_t* rp_u = nullptr;
@@ -1812,7 +1874,7 @@ struct GridBackend : EnvBackend {
 #ifdef GP_STAMPS
   int debug_stamps(unsigned long long* out, int cap) override {
     GP_HIP_CHECK(hipDeviceSynchronize());
-    const int n = std::min(cap, 256 * 64 * 8);
+    const int n = std::min(cap, 256 * 64 * 16);
     GP_HIP_CHECK(hipMemcpy(out, d.dbg, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost));
     return n;
   }
@@ -1854,6 +1916,14 @@ int GridBackend::upload_rng() {
   GP_HIP_CHECK(hipMemcpy(d.ctl, &c, sizeof(c), hipMemcpyHostToDevice));
   std::vector<PcgJump> jt = build_jump_tables(rng.inc);
   GP_HIP_CHECK(hipMemcpy(b_jt.p, jt.data(), jt.size() * sizeof(PcgJump), hipMemcpyHostToDevice));
+  if (b_jt8.p) {
+    std::vector<PcgJump> j8(2 * 256);
+    for (int dgt = 0; dgt < 256; ++dgt) {
+      j8[dgt] = pcg_jump_params((u128)dgt, rng.inc);
+      j8[256 + dgt] = pcg_jump_params((u128)(256 * dgt), rng.inc);
+    }
+    GP_HIP_CHECK(hipMemcpy(b_jt8.p, j8.data(), j8.size() * sizeof(PcgJump), hipMemcpyHostToDevice));
+  }
   std::vector<PcgJump> l4(TPB), l2(TPB);
   for (int t = 0; t < TPB; ++t) {
     l4[t] = pcg_jump_params((u128)(4 * t), rng.inc);
@@ -2280,10 +2350,15 @@ int GridBackend::build(const gp_grid_config* cfg) {
     put(d.lds.av, agent_valid_h.size() * sizeof(uint16_t));
     put(d.lds.doff, doff.size() * sizeof(int32_t));
     put(d.lds.jt, sizeof(PcgJump) * JT_LEVELS * JT_RADIX);
+    put(d.lds.jt8, sizeof(PcgJump) * 2 * 256);
     d.lds.total = off <= LDS_TABLE_BUDGET ? off : 0;
   }
   // fused numpy rollout: one 512-thread block per CU, <= 4 tiles of 2048 envs per block
   d.fnt = (int)((B + FEPB - 1) / FEPB);
+  {
+    const char* xm = getenv("GP_XMODE");  // exchange variant (tuning knob)
+    d.xmode = xm ? atoi(xm) : 0;
+  }
   {
     hipDeviceProp_t prop;
     GP_HIP_CHECK(hipGetDeviceProperties(&prop, device));
@@ -2337,11 +2412,12 @@ int GridBackend::build(const gp_grid_config* cfg) {
   d.fjB = b_fjB.as<PcgJump>();
   d.fslot = b_fslot.as<uint64_t>();
 #ifdef GP_STAMPS
-  if ((e = b_dbg.alloc(sizeof(unsigned long long) * 256 * 64 * 8))) return e;
+  if ((e = b_dbg.alloc(sizeof(unsigned long long) * 256 * 64 * 16))) return e;
   d.dbg = b_dbg.as<unsigned long long>();
 #endif
-  if ((e = b_self.alloc(sizeof(GridDev)))) return e;
+  if ((e = b_self.alloc(sizeof(GridDev))) || (e = b_jt8.alloc(sizeof(PcgJump) * 2 * 256))) return e;
   d.self = b_self.as<GridDev>();
+  d.jt8 = b_jt8.as<PcgJump>();
   // default seed: numpy's SeedSequence(0) until the caller seeds
   rng = pcg64_from_seed({0u}, {});
   return upload_rng();

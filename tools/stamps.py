@@ -29,9 +29,9 @@ L = _lib.lib()
 fn = L.gp_debug_stamps
 fn.restype = ctypes.c_int
 fn.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
-buf = (ctypes.c_ulonglong * (256 * 64 * 8))()
-n = fn(env._handle, buf, 256 * 64 * 8)
-a = np.frombuffer(buf, dtype=np.uint64).reshape(256, 64, 8).astype(np.int64)
+buf = (ctypes.c_ulonglong * (256 * 64 * 16))()
+n = fn(env._handle, buf, 256 * 64 * 16)
+a = np.frombuffer(buf, dtype=np.uint64).reshape(256, 64, 16).astype(np.int64)
 G = min(256, (B + 2047) // 2048)
 a = a[:G, 2:K - 2] * 10  # ns
 def rep(name, d):
@@ -57,3 +57,8 @@ b0 = 0
 print("block 0 phases (ns) step 10:", np.diff(a[b0, 10, [0, 1, 2, 7, 4, 5]]).tolist())
 bs = int(slow[10])
 print(f"block {bs} phases (ns) step 10:", np.diff(a[bs, 10, [0, 1, 2, 7, 4, 5]]).tolist())
+pd, dd = a[:, :, 8], a[:, :, 9]
+print(f"poll done - last publish                 median {np.median(pd - pub.max(0)[None, :]):.0f} ns")
+print(f"block0 gather done - last publish        median {np.median(a[0, :, 10] - pub.max(0)):.0f} ns")
+print(f"draw cells (8->9)                        median {np.median(dd - pd):.0f} ns")
+print(f"publish_next etc (9->7)                  median {np.median(done - dd):.0f} ns")
