@@ -158,6 +158,48 @@ __device__ __forceinline__ void store4(T* __restrict__ p, int env0, int B, const
   }
 }
 
+// Fused-kernel variants: the host guarantees 16-B aligned base pointers (else the fused path is not
+// taken), so only the last, partial quad of a ragged batch takes the per-element path.
+template <class T>
+__device__ __forceinline__ void load4f(const T* __restrict__ p, int env0, int B, T (&v)[4]) {
+  if (env0 + 3 < B) {
+    if constexpr (sizeof(T) == 4) {
+      const uint4 q = *reinterpret_cast<const uint4*>(p + env0);
+      v[0] = __builtin_bit_cast(T, q.x); v[1] = __builtin_bit_cast(T, q.y);
+      v[2] = __builtin_bit_cast(T, q.z); v[3] = __builtin_bit_cast(T, q.w);
+    } else {
+      const uint2 q = *reinterpret_cast<const uint2*>(p + env0);
+      v[0] = (T)(q.x & 0xFFFF); v[1] = (T)(q.x >> 16); v[2] = (T)(q.y & 0xFFFF); v[3] = (T)(q.y >> 16);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = (env0 + i < B) ? p[env0 + i] : (T)0;
+  }
+}
+template <class T>
+__device__ __forceinline__ void store4f(T* __restrict__ p, int env0, int B, const T (&v)[4]) {
+  if (env0 + 3 < B) {
+    if constexpr (sizeof(T) == 4) {
+      uint4 q;
+      q.x = __builtin_bit_cast(uint32_t, v[0]); q.y = __builtin_bit_cast(uint32_t, v[1]);
+      q.z = __builtin_bit_cast(uint32_t, v[2]); q.w = __builtin_bit_cast(uint32_t, v[3]);
+      *reinterpret_cast<uint4*>(p + env0) = q;
+    } else if constexpr (sizeof(T) == 2) {
+      uint2 q;
+      q.x = (uint32_t)(uint16_t)v[0] | ((uint32_t)(uint16_t)v[1] << 16);
+      q.y = (uint32_t)(uint16_t)v[2] | ((uint32_t)(uint16_t)v[3] << 16);
+      *reinterpret_cast<uint2*>(p + env0) = q;
+    } else {
+      *reinterpret_cast<uint32_t*>(p + env0) = (uint32_t)(uint8_t)v[0] | ((uint32_t)(uint8_t)v[1] << 8) |
+                                               ((uint32_t)(uint8_t)v[2] << 16) | ((uint32_t)(uint8_t)v[3] << 24);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (env0 + i < B) p[env0 + i] = v[i];
+  }
+}
+
 // ------------------------------------------------------------------ lookup-table access ----
 // GTabs reads the tables from global memory (L1/L2 hot); LTabs from the fused kernel's LDS copy.
 struct GTabs {
@@ -256,7 +298,7 @@ __device__ __forceinline__ void write_obs(const GridDev& p, const TB& tb, int en
   }
 }
 
-template <int OK, class TB>
+template <int OK, class TB, bool ALIGNED = false>
 __device__ __forceinline__ void write_obs4(const GridDev& p, const TB& tb, int env0, const int (&agent)[4],
                                            const int (&goal)[4], void* __restrict__ obs) {
   if constexpr (OK == GP_OBS_HANSEN || OK == GP_OBS_TABLE) {
@@ -276,7 +318,10 @@ __device__ __forceinline__ void write_obs4(const GridDev& p, const TB& tb, int e
         v[i] = tb.t1(a) + (tb.has_t2() ? tb.t2(g) : 0);
       }
     }
-    store4<int32_t>((int32_t*)obs, env0, p.B, v);
+    if constexpr (ALIGNED)
+      store4f<int32_t>((int32_t*)obs, env0, p.B, v);
+    else
+      store4<int32_t>((int32_t*)obs, env0, p.B, v);
   } else {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -801,7 +846,6 @@ struct FusedShared {
   uint32_t btot, anyrej, known, flag, w1;
   uint64_t ju[4];                // this step's J_used (a_hi, a_lo, c_hi, c_lo)
   uint64_t jB[4];                // J_B: jump by num_envs
-  uint4 thr4[16];                // action-failure thresholds >> 21 (hi 32 bits), [a][j]
   uint64_t ns_hi, ns_lo;         // next step's s0
   uint32_t nh, nu;               // next step's has_uint32 / uinteger
   uint32_t drawn;                // the control wave drew this step's resetter cells before B2
@@ -1059,6 +1103,49 @@ __device__ __forceinline__ void lds_copy(char* dyn, const GridLdsTab& t, const T
 // Control wave: the cells (goal | agent << 16) of this block's resetters, rank r of tile q ->
 // sh.cell[q*FEPB + r]. Word positions: fast path P_q + r (goal call) and w1 + P_q + r (agent
 // call); slow path (only_q >= 0: one tile) from the stream walk's position lists pg / pa.
+// Control wave, common case (one reset call, no rejected word, b within the speculative window):
+// the next PCG64 state and the block's resetter cells in ONE straight-line block so that their
+// dependent jump chains overlap. tq / pre: lane q < QPT holds tile q's reset count / prefix.
+template <int QPT>
+__device__ __forceinline__ void ctrl_fast_finish(const GridDev& p, FusedShared& sh, const LTabs& tb, const u128 SB,
+                                                 const Stream& st, uint32_t b, uint32_t tq, uint32_t pre) {
+  const int lane = threadIdx.x & 63;
+  const bool rgoal = p.fixed_goal < 0;
+  const uint32_t mode = rgoal ? 1u : 2u;
+  const uint32_t ng = (uint32_t)p.n_goal_valid, na = (uint32_t)p.n_agent_valid;
+  uint32_t tc[QPT], P[QPT], cum[QPT + 1];
+  cum[0] = 0;
+#pragma unroll
+  for (int q = 0; q < QPT; ++q) {
+    tc[q] = (uint32_t)__builtin_amdgcn_readlane((int)tq, q);
+    P[q] = (uint32_t)__builtin_amdgcn_readlane((int)pre, q);
+    cum[q + 1] = cum[q] + tc[q];
+  }
+  // next state: s0' = jump(SB, used), J_used
+  uint32_t used, h;
+  words_to_draws(b, st.h0, used, h);
+  const PcgJump ju = jparams_small(tb.jt8(), tb.jt(), used);
+  const u128 s = jump_small(tb.jt8(), tb.jt(), SB, used);
+  for (uint32_t idx = lane; idx < max(cum[QPT], 1u); idx += 64) {
+    const uint32_t ii = min(idx, max(cum[QPT], 1u) - 1u);
+    int q = 0;
+#pragma unroll
+    for (int j = 1; j < QPT; ++j) q += ii >= cum[j] ? 1 : 0;
+    const uint32_t r = ii - cum[q];
+    const uint32_t w = P[q] + r;
+    const uint32_t v = draw_cells(tb.jt8(), tb.jt(), SB, st.h0, st.u0, w, w, mode, ng, na);
+    const uint32_t goal = rgoal ? (uint32_t)tb.gv((int)(v & 0xFFFFu)) : (uint32_t)p.fixed_goal;
+    const uint32_t agent = rgoal ? (uint32_t)p.fixed_agent : (uint32_t)tb.av((int)(v >> 16));
+    if (idx < cum[QPT]) sh.cell[q * FEPB + r] = goal | (agent << 16);
+  }
+  if (lane == 0) {
+    sh.ju[0] = ju.a_hi; sh.ju[1] = ju.a_lo; sh.ju[2] = ju.c_hi; sh.ju[3] = ju.c_lo;
+    sh.ns_hi = hi64(s); sh.ns_lo = lo64(s);
+    sh.nh = h;
+    sh.nu = used ? (uint32_t)(pcg_output(s) >> 32) : st.u0;
+  }
+}
+
 template <int QPT>
 __device__ __forceinline__ void ctrl_draw_cells(const GridDev& p, FusedShared& sh, const LTabs& tb, const u128 SB,
                                                 const Stream& st, uint32_t w1, const uint32_t* pg, const uint32_t* pa,
@@ -1204,21 +1291,13 @@ __device__ __forceinline__ void fused_resets(const GridDev& p, FusedShared& sh, 
 // Effective action of env with action a and 53-bit uniform k: #{j : k > thr[a][j]} (integer form
 // of action_utils.py:84-90), on the high 32 bits with an exact 64-bit fallback on a tie.
 template <int NA>
-__device__ __forceinline__ uint32_t fused_effective_action(const FusedShared& sh, const uint64_t* s_thr, int a,
-                                                           uint64_t k) {
-  const uint32_t khi = (uint32_t)(k >> 21);
+__device__ __forceinline__ uint32_t fused_effective_action(const uint64_t* s_thr, int a, uint64_t k) {
+  const ulonglong2* t = reinterpret_cast<const ulonglong2*>(s_thr + a * NA);
   uint32_t e = 0;
-  bool tie = false;
 #pragma unroll
-  for (int h = 0; h < NA / 4; ++h) {
-    const uint4 t = sh.thr4[a * (NA / 4) + h];
-    e += (khi > t.x) + (khi > t.y) + (khi > t.z) + (khi > t.w);
-    tie |= (khi == t.x) | (khi == t.y) | (khi == t.z) | (khi == t.w);
-  }
-  if (tie) {
-    e = 0;
-#pragma unroll
-    for (int j = 0; j < NA; ++j) e += (k > s_thr[a * NA + j]) ? 1u : 0u;
+  for (int h = 0; h < NA / 2; ++h) {
+    const ulonglong2 v = t[h];
+    e += (k > v.x ? 1u : 0u) + (k > v.y ? 1u : 0u);
   }
   return min(e, (uint32_t)NA - 1);
 }
@@ -1275,17 +1354,17 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
     const int tau = q * G + (int)blockIdx.x;
     const int env0 = tau * FEPB + tid * EPT;
     pfm[q] = 0;
-    load4<uint32_t>(p.ae, env0, B, ae[q]);
+    load4f<uint32_t>(p.ae, env0, B, ae[q]);
     if (rgoal) {
       uint16_t gg[4];
-      load4<uint16_t>(p.goal, env0, B, gg);
+      load4f<uint16_t>(p.goal, env0, B, gg);
 #pragma unroll
       for (int i = 0; i < 4; ++i) gl[q][i] = gg[i];
     } else {
 #pragma unroll
       for (int i = 0; i < 4; ++i) gl[q][i] = fixed_goal;
     }
-    load4<int32_t>(act, env0, B, a_cur[q]);
+    load4f<int32_t>(act, env0, B, a_cur[q]);
     S[q] = apply_jump(compose_jump(p.flt4[tid], p.ftj[min(tau, nt - 1)]), st.s0);
   }
   for (int k = 0; k < K; ++k) {
@@ -1296,7 +1375,7 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
     if (k + 1 < K) {
 #pragma unroll
       for (int q = 0; q < QPT; ++q)
-        load4<int32_t>(act + (size_t)(k + 1) * B, (q * G + (int)blockIdx.x) * FEPB + tid * EPT, B, a_nxt[q]);
+        load4f<int32_t>(act + (size_t)(k + 1) * B, (q * G + (int)blockIdx.x) * FEPB + tid * EPT, B, a_nxt[q]);
     }
     // ---- 1. draws + transitions (the critical path) ----
     float r[QPT][4];
@@ -1313,7 +1392,7 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
         int a = a_cur[q][i];
         if (a < 0) a += NA;                 // numpy negative indexing of action_matrix[action]
         a = min(max(a, 0), NA - 1);         // (out-of-range actions raise in the reference; clamped here)
-        const uint32_t eff = fused_effective_action<NA>(sh, s_thr, a, k53);
+        const uint32_t eff = fused_effective_action<NA>(s_thr, a, k53);
         const uint32_t s_ae = ae[q][i];
         const int agent = (int)(s_ae & 0xFFFFu);
         const uint32_t m = tb.move(agent * NA + (int)eff);
@@ -1368,12 +1447,12 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
         tr[i] = (uint8_t)((trm[q] >> i) & 1u);
         ag[i] = (int)(ae[q][i] & 0xFFFFu);
       }
-      store4<float>(rew + off, env0, B, r[q]);
-      store4<uint8_t>(term + off, env0, B, tm);
-      store4<uint8_t>(trunc + off, env0, B, tr);
+      store4f<float>(rew + off, env0, B, r[q]);
+      store4f<uint8_t>(term + off, env0, B, tm);
+      store4f<uint8_t>(trunc + off, env0, B, tr);
       // one vector store for all 4 envs (uniform store count per step: no vmcnt(0) at merges);
       // a resetter's obs is provisional here and rewritten in phase 4
-      write_obs4<OK>(p, tb, env0, ag, gl[q], ob);
+      write_obs4<OK, LTabs, true>(p, tb, env0, ag, gl[q], ob);
     }
     if (k > 0) flush_reset_obs<OK, QPT>(p, tb, (uint8_t*)obs + (off - B) * ow, tid, pc, pfm);
     {
@@ -1407,12 +1486,12 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
 #pragma unroll
   for (int q = 0; q < QPT; ++q) {
     const int env0 = (q * G + (int)blockIdx.x) * FEPB + tid * EPT;
-    store4<uint32_t>(p.ae, env0, B, ae[q]);
+    store4f<uint32_t>(p.ae, env0, B, ae[q]);
     if (rgoal) {
       uint16_t gg[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) gg[i] = (uint16_t)gl[q][i];
-      store4<uint16_t>(p.goal, env0, B, gg);
+      store4f<uint16_t>(p.goal, env0, B, gg);
     }
   }
 }
@@ -1573,9 +1652,12 @@ __device__ __forceinline__ void fused_ctrl(const GridDev& p_in, FusedShared& sh,
     const bool drawn = known && ncalls == 1 && b > 0;
     if (lane < QPT) sh.tpre[lane] = mypre;
     wave_lds_sync();
-    if (drawn) ctrl_draw_cells<QPT>(p, sh, tb, SB, st, 0u, nullptr, nullptr, -1);  // before B2
+    if (drawn) {
+      ctrl_fast_finish<QPT>(p, sh, tb, SB, st, b, tq, mypre);  // cells + next state, before B2
+    } else if (known) {
+      publish_next(tb, sh, SB, ncalls ? b : 0u, st.h0, st.u0, lane == 0);
+    }
     if (lane == 0) RSTAMP(9);
-    if (known) publish_next(tb, sh, SB, ncalls ? b : 0u, st.h0, st.u0, lane == 0);
     if (lane == 0) {
       sh.btot = b;
       sh.anyrej = anyr;
@@ -1612,15 +1694,11 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
                                                            void* __restrict__ obs, float* __restrict__ rew,
                                                            uint8_t* __restrict__ term, uint8_t* __restrict__ trunc) {
   __shared__ FusedShared sh;
-  __shared__ uint64_t s_thr[64];
+  __shared__ __attribute__((aligned(16))) uint64_t s_thr[64];
   extern __shared__ __attribute__((aligned(16))) char dyn[];
   const GridDev& p = p_in;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  if (tid < NA * NA) {
-    const uint64_t t = p.thr[tid];
-    s_thr[tid] = t;
-    reinterpret_cast<uint32_t*>(sh.thr4)[tid] = (t >> 21) > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)(t >> 21);
-  }
+  if (tid < NA * NA) s_thr[tid] = p.thr[tid];
   // stage the lookup tables in LDS (the fused path is only taken when they fit)
   lds_copy(dyn, p.lds.move, p.move);
   lds_copy(dyn, p.lds.hbase, p.hbase);
@@ -1888,6 +1966,12 @@ struct GridBackend : EnvBackend {
       hipLaunchKernelGGL((grid_rollout_numpy<OK, QPT, 8>), dim3(fused_G), dim3(FTPB), d.lds.total, s, d, K,
                          (const int32_t*)act, obs, rew, term, trunc);
   }
+  // the fused kernel's vector I/O assumes 16-B aligned bases (torch allocations are); K-step launches
+  // also need B % 4 == 0 so that every step's slice stays aligned
+  bool fused_ok(const void* act, const void* obs, const void* rew, const void* term, const void* trunc) const {
+    auto al = [](const void* x, uintptr_t m) { return ((uintptr_t)x & (m - 1)) == 0; };
+    return fused_G && al(act, 16) && al(obs, 16) && al(rew, 16) && al(term, 4) && al(trunc, 4);
+  }
   template <int OK>
   int launch_fused(int K, const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc, hipStream_t s) {
     timer.begin(s);
@@ -2043,7 +2127,7 @@ int GridBackend::step(const void* act, void* obs, float* rew, uint8_t* term, uin
   int e = dispatch_obs(d.obs_kind, [&](auto okc) -> int {
     constexpr int OK = decltype(okc)::value;
     if (rng_mode == GP_RNG_NUMPY) {
-      if (fused_G) return launch_fused<OK>(1, act, obs, rew, term, trunc, s);
+      if (fused_ok(act, obs, rew, term, trunc)) return launch_fused<OK>(1, act, obs, rew, term, trunc, s);
       timer.begin(s);
       hipLaunchKernelGGL(grid_step_numpy<OK>, dim3(d.nblk), dim3(TPB), 0, s, d, (const int32_t*)act, obs, rew, term,
                          trunc);
@@ -2077,7 +2161,7 @@ int GridBackend::step(const void* act, void* obs, float* rew, uint8_t* term, uin
 
 int GridBackend::rollout(int K, const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc,
                          hipStream_t s) {
-  if (rng_mode == GP_RNG_NUMPY && fused_G) {
+  if (rng_mode == GP_RNG_NUMPY && fused_ok(act, obs, rew, term, trunc) && B % 4 == 0) {
     if (!has_reset) {
       gp_set_error("rollout() before reset()");
       return GP_E_STATE;
