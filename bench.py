@@ -41,6 +41,22 @@ def lib_hash():
         return hashlib.sha1(f.read()).hexdigest()[:12]
 
 
+# sources that determine each measured kernel's code (PMC traffic is reused only for the same sources)
+KERNEL_SOURCES = {"fourrooms": ("grid.hip", "gp_common.h"), "taxi": ("taxi.hip", "gp_common.h", "gp_device.h"),
+                  "crooms": ("crooms.hip", "gp_common.h", "gp_device.h"),
+                  "anttag": ("anttag.hip", "gp_common.h", "gp_device.h")}
+
+
+def src_hash(workload):
+    h = hashlib.sha1()
+    for name in KERNEL_SOURCES[workload]:
+        p = os.path.join(ROOT, "gym-po-taxi_amd", "csrc", name)
+        if os.path.exists(p):
+            with open(p, "rb") as f:
+                h.update(f.read())
+    return h.hexdigest()[:12]
+
+
 def cpu_baseline(target_s=12.0):
     """The numpy oracle (the reference's algorithm restated, fixture-pinned) on one host core."""
     import numpy as np
@@ -63,16 +79,17 @@ def cpu_baseline(target_s=12.0):
                       f"1 process ({dt:.1f} s)"}
 
 
-def load_pmc(cfg_key):
-    """HBM traffic per launch from profiles/pmc_*.json, only if collected for this exact build."""
+def load_pmc(cfg_key, workload):
+    """HBM traffic per launch from profiles/*pmc_*.json (rocprofv3 FETCH_SIZE/WRITE_SIZE passes,
+    tools/pmc_to_json.py), only if collected for the same kernel sources."""
     import glob
     best = None
-    for fn in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json"))):
+    for fn in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_*.json"))):
         try:
             d = json.load(open(fn))
         except Exception:  # noqa: BLE001
             continue
-        if d.get("lib_hash") == lib_hash() and d.get("config") == cfg_key:
+        if d.get("src_hash") == src_hash(workload) and d.get("config") == cfg_key:
             best = d
     return best
 
@@ -168,7 +185,7 @@ def main():
 
     total_steps = B * args.steps * world
     cfg_key = f"fourrooms_hansen4_B{B}_{args.mode}"
-    pmc = load_pmc(cfg_key)
+    pmc = load_pmc(cfg_key, "fourrooms")
     traffic = pmc["hbm_bytes_per_launch"] if pmc else None
     line = {
         "metric": "env steps/sec (whole node), FourRooms 11x11 Hansen-4 at 1M envs, 1/2/4/8 GPUs",
