@@ -33,6 +33,33 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec); 6.29 TB/s measur
 BYTES_PER_ENV_STEP = 22
 # Philox fused rollout: per env-step action 4 + obs 4 + reward 4 + term 1 + trunc 1; state once per launch
 ROLLOUT_BYTES_PER_ENV_STEP = 14
+HEADLINE_METRIC = "env steps/sec (whole node), FourRooms 11x11 Hansen-4 at 1M envs, 1/2/4/8 GPUs"
+
+
+def _fourrooms(B, dev, mode):
+    from gym_po_amd import MultistoryFourRoomsEnv
+    return MultistoryFourRoomsEnv(B, grid_z=1, obs_type="hansen", device=dev, rng_mode=mode)
+
+
+def _taxi_onehot(B, dev, mode):
+    from gym_po_amd import HansenTaxiVecEnv
+    return HansenTaxiVecEnv(B, device=dev, rng_mode=mode, one_hot=True)
+
+
+# The headline (BASELINE.json configs[1]) and the other single-GPU configs, measured the same way.
+# bytes: algorithmic bytes per env-step of a fused rollout launch; state: bytes per env
+# read + written once per launch.
+WORKLOADS = {
+    "fourrooms": dict(make=_fourrooms, envs=1 << 20, n_actions=4, mode="numpy", bytes=14, state=8,
+                      metric=HEADLINE_METRIC, dtype="int32",
+                      desc="configs[1]: FourRooms 11x11 (FR_MAP) Hansen-4 obs, {B} envs per GPU, "
+                           "MultistoryFourRoomsEnv(grid_z=1, obs_type='hansen')"),
+    "taxi": dict(make=_taxi_onehot, envs=1 << 22, n_actions=5, mode="philox", bytes=4 + 320 + 4 + 1 + 1, state=8,
+                 metric="env steps/sec, PO-Taxi 5x5 Hansen one-hot obs (uint8[320]) at 4M envs per GPU",
+                 dtype="uint8", kernel="taxi_rollout<16,false>", chunk=16,
+                 desc="configs[2]: PO-Taxi 5x5 (TAXI_MAP) Hansen obs one-hot uint8[B,320], {B} envs per GPU, "
+                      "HansenTaxiVecEnv(one_hot=True)"),
+}
 
 
 def lib_hash():
@@ -57,14 +84,23 @@ def src_hash(workload):
     return h.hexdigest()[:12]
 
 
-def cpu_baseline(target_s=12.0):
+def cpu_baseline(workload="fourrooms", target_s=12.0):
     """The numpy oracle (the reference's algorithm restated, fixture-pinned) on one host core."""
     import numpy as np
-    from oracle.gridworld import FourRoomsOracle
     B = 1 << 18
-    ora = FourRoomsOracle(B, 1, obs_type="hansen")
+    if workload == "taxi":
+        from oracle.taxi import TaxiOracle
+        ora = TaxiOracle(B, hansen_obs=True)
+        name, na = "oracle.taxi.TaxiOracle(hansen_obs=True) + one-hot np.eye gather", 5
+        eye = np.eye(ora.no, dtype=np.uint8)
+        step = ora.step_seeded
+        ora.step_seeded = lambda a: (lambda r: (eye[r[0]],) + tuple(r[1:]))(step(a))
+    else:
+        from oracle.gridworld import FourRoomsOracle
+        ora = FourRoomsOracle(B, 1, obs_type="hansen")
+        name, na = "oracle.gridworld.FourRoomsOracle", 4
     ora.reset_seed(0)
-    acts = np.random.default_rng(1).integers(0, 4, (8, B))
+    acts = np.random.default_rng(1).integers(0, na, (8, B))
     ora.step_seeded(acts[0])  # warm
     t0 = time.perf_counter()
     n = 0
@@ -75,7 +111,7 @@ def cpu_baseline(target_s=12.0):
         if dt >= target_s or n >= 400:
             break
     return {"value": B * n / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"oracle.gridworld.FourRoomsOracle (numpy, reference-pinned), 2^18 envs x {n} steps, "
+            "sample": f"{name} (numpy, reference-pinned), 2^18 envs x {n} steps, "
                       f"1 process ({dt:.1f} s)"}
 
 
@@ -99,10 +135,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=200)
-    ap.add_argument("--envs", type=int, default=1 << 20, help="envs per GPU (weak scaling)")
+    ap.add_argument("--workload", default="fourrooms", choices=sorted(WORKLOADS),
+                    help="fourrooms = the BASELINE headline (default); others = the other single-GPU configs")
+    ap.add_argument("--envs", type=int, default=None, help="envs per GPU (weak scaling)")
     ap.add_argument("--strong", action="store_true", help="split --envs across GPUs instead")
-    ap.add_argument("--mode", default="numpy", choices=["numpy", "philox"])
-    ap.add_argument("--chunk", type=int, default=64, help="steps per gp_rollout call")
+    ap.add_argument("--mode", default=None, choices=["numpy", "philox"])
+    ap.add_argument("--chunk", type=int, default=None, help="steps per gp_rollout call")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -118,9 +156,12 @@ def main():
     dev = torch.device("cuda", local if world > 1 else 0)
     torch.cuda.set_device(dev)
 
-    from gym_po_amd import MultistoryFourRoomsEnv
+    W = WORKLOADS[args.workload]
+    args.envs = args.envs or W["envs"]
+    args.mode = args.mode or W["mode"]
+    args.chunk = args.chunk or W.get("chunk", 64)
     B = args.envs // world if args.strong else args.envs
-    env = MultistoryFourRoomsEnv(B, grid_z=1, obs_type="hansen", device=dev, rng_mode=args.mode)
+    env = W["make"](B, dev, args.mode)
     if world == 1:
         env.reset(seed=0)
     else:  # shard g: SeedSequence(0, spawn_key=(g,))
@@ -129,7 +170,7 @@ def main():
     C = max(1, min(args.chunk, args.steps))
     g = torch.Generator(device=dev)
     g.manual_seed(1 + rank)
-    acts = torch.randint(0, 4, (C, B), device=dev, dtype=torch.int32, generator=g)
+    acts = torch.randint(0, W["n_actions"], (C, B), device=dev, dtype=torch.int32, generator=g)
     out = env._alloc_outputs(C)
 
     def run(n):
@@ -171,8 +212,9 @@ def main():
     kavg_ms = kms / max(nk, 1)
     ravg_ms = rms / max(nr, 1)
     steps_per_launch = prof_steps / max(nk, 1)
-    if steps_per_launch > 1.5:  # fused launch of several steps; state read+written once per launch
-        bytes_per_launch = B * (ROLLOUT_BYTES_PER_ENV_STEP * steps_per_launch + 8)
+    if args.workload != "fourrooms" or steps_per_launch > 1.5:
+        # fused launch of several steps; state read+written once per launch
+        bytes_per_launch = B * (W["bytes"] * steps_per_launch + W["state"])
     else:
         bytes_per_launch = B * BYTES_PER_ENV_STEP
     achieved = bytes_per_launch / (kavg_ms * 1e-3) / 1e9
@@ -184,11 +226,12 @@ def main():
         dist.all_reduce(mt)  # RCCL: the only collective (episode statistics)
 
     total_steps = B * args.steps * world
-    cfg_key = f"fourrooms_hansen4_B{B}_{args.mode}"
-    pmc = load_pmc(cfg_key, "fourrooms")
+    cfg_key = (f"fourrooms_hansen4_B{B}_{args.mode}" if args.workload == "fourrooms" else
+               f"{args.workload}_B{B}_{args.mode}")
+    pmc = load_pmc(cfg_key, args.workload)
     traffic = pmc["hbm_bytes_per_launch"] if pmc else None
     line = {
-        "metric": "env steps/sec (whole node), FourRooms 11x11 Hansen-4 at 1M envs, 1/2/4/8 GPUs",
+        "metric": W["metric"],
         "value": total_steps / tmax,
         "unit": "env-steps/s",
         "n_gpus": world,
@@ -198,29 +241,31 @@ def main():
         "higher_is_better": True,
         "scaling": "strong" if args.strong else "weak",
         "vs_baseline": None,
-        "dtype": "int32",
-        "data": "synthetic (uniform random actions, seeded); reference RNG stream reproduced bit-exactly",
-        "config": {"workload": "configs[1]: FourRooms 11x11 (FR_MAP) Hansen-4 obs, "
-                               f"{B} envs per GPU, MultistoryFourRoomsEnv(grid_z=1, obs_type='hansen')",
+        "dtype": W["dtype"],
+        "data": "synthetic (uniform random actions, seeded); " + (
+            "reference RNG stream reproduced bit-exactly" if args.mode == "numpy" else
+            "counter-based Philox draws from the reference's exact laws"),
+        "config": {"workload": W["desc"].format(B=B),
                    "envs_per_gpu": B, "global_envs": B * world, "rng_mode": args.mode,
                    "parallelism": f"independent env shards x{world}", "steps_per_launch_call": C},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": ("grid_rollout_numpy<GP_OBS_HANSEN,1>" if steps_per_launch > 1.5 else
-                                "grid_step_numpy<GP_OBS_HANSEN>") if args.mode == "numpy" else
-                               "grid_rollout_counter<GP_OBS_HANSEN,false>",
+                     "kernel": W.get("kernel") or (("grid_rollout_numpy<GP_OBS_HANSEN,1>" if steps_per_launch > 1.5
+                                                   else "grid_step_numpy<GP_OBS_HANSEN>") if args.mode == "numpy"
+                                                  else "grid_rollout_counter<GP_OBS_HANSEN,false>"),
                      "steps_per_launch": steps_per_launch,
                      "kernel_avg_us": kavg_ms * 1e3,
                      "bytes_per_launch": bytes_per_launch,
                      "kernel_launches_timed": nk,
-                     "resolver_kernel": "grid_resolve_numpy<GP_OBS_HANSEN>" if args.mode == "numpy" else None,
+                     "resolver_kernel": ("grid_resolve_numpy<GP_OBS_HANSEN>"
+                                         if args.mode == "numpy" and args.workload == "fourrooms" else None),
                      "resolver_avg_us": ravg_ms * 1e3 if nr else None},
         "episodes": {"count": mt[0].item(), "mean_return": mt[1].item() / max(mt[0].item(), 1),
                      "mean_length": mt[2].item() / max(mt[0].item(), 1)},
         "lib_hash": lib_hash(),
     }
     if rank == 0:
-        line["cpu_baseline"] = None if args.no_cpu_baseline else cpu_baseline()
+        line["cpu_baseline"] = None if args.no_cpu_baseline else cpu_baseline(args.workload)
         print(json.dumps(line), flush=True)
     env.close()
     if world > 1:

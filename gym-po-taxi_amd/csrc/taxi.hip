@@ -1,0 +1,694 @@
+// taxi.hip — the (PO-)Taxi backend (GP_KIND_TAXI): TaxiVecEnv.step / _reset_mask /
+// _reset_passenger_and_destination / _obs (gym_po/envs/extended_taxi.py:244-372) for B envs.
+//
+// The whole Taxi transition is a function of (state, action): no draw is made on a step unless the
+// env completes a task or resets. So the host lowers the map once into
+//   trans[s*5 + a] = s' | goal << 12 | bad << 13    (move, wall/pseudo-wall check, pickup/dropoff)
+//   obs_of[s]      = s  or  (hansen[r,c]*(L+1) + p)*L + d
+//   cdf[k]         = the exact start-state law of  multinomial(ns, uniform over valid).argmax()
+//                    (dist.hip) as 64-bit thresholds over the valid states, ascending
+// and the device step is: one LDS lookup, a compare or two, the stores. State per env is ONE packed
+// uint32 (s | n_dropoffs << 12 | elapsed << 16) kept in registers across the K steps of a rollout.
+//
+// RNG: the reference's resets draw multinomial(500, p, b) = ~300 sequential binomial inversions per
+// resetting env from ONE numpy stream, with a data-dependent word count, so a parallel exact stream
+// is out of reach. Two modes:
+//   GP_RNG_PHILOX  Philox4x32-10 (env, step): reset state = CDF search of one 64-bit uniform (the
+//                  exact law, not an approximation of it); passenger/destination = Lemire draws with
+//                  the reference's "resample d while d == p" law (p uniform, d uniform over the rest).
+//   GP_RNG_REPLAY  caller-supplied per-env reset states and p*L+d pairs: bit-exact replay of the
+//                  reference stream, which is how parity with the reference is checked.
+//
+// Kernels: one persistent, grid-stride rollout kernel (tables staged in LDS once per block, 1024-env
+// tiles, K steps per tile with the state in registers) for both scalar and one-hot observations; the
+// one-hot rows (uint8 [B, n_obs], 320 B/env for Hansen) are written as a wave-contiguous stream of
+// 16-B chunks so every store instruction covers 1 KB of consecutive bytes.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "gp_internal.h"
+
+namespace {
+
+constexpr int TPB = 256;
+constexpr int EPT = 4;
+constexpr int EPB = TPB * EPT;  // envs per tile
+constexpr int WAVES = TPB / 64;
+constexpr int NACT = 5;         // N, S, W, E, Pickup/Dropoff (extended_taxi.py:154)
+constexpr int MAX_NS = 4096;    // s fits 12 bits of the packed state
+constexpr uint32_t PHILOX_TAG = 0x74617869u;  // 'taxi'
+
+struct alignas(32) TaxiSlot {
+  double return_sum;
+  unsigned long long episodes, length_sum, env_steps;
+};
+
+struct TaxiDev {
+  int32_t B, ntiles;
+  int32_t ns, nlocs, lpl;          // lpl = L*(L+1): states per taxi cell
+  int32_t n_valid, num_passengers, time_limit;
+  int32_t n_obs;                   // observation space size (one-hot width)
+  float r_goal, r_bad, r_any;
+  uint32_t key0, key1;
+  const uint8_t* tabs;             // packed tables (global), staged into LDS
+  int32_t off_trans, off_obs, off_cdf, off_valid, tab_bytes;
+  uint32_t* st;                    // [B] s | nd << 12 | elapsed << 16
+  TaxiSlot* mslot;                 // [grid]
+  const int32_t* rp_state;         // replay: reset state per env (GP_RNG_REPLAY)
+  const int32_t* rp_pd;            // replay: p*L + d per env
+};
+
+__device__ __forceinline__ const uint16_t* l_trans(const uint8_t* l, const TaxiDev& p) {
+  return (const uint16_t*)(l + p.off_trans);
+}
+__device__ __forceinline__ const uint16_t* l_obs(const uint8_t* l, const TaxiDev& p) {
+  return (const uint16_t*)(l + p.off_obs);
+}
+__device__ __forceinline__ const uint64_t* l_cdf(const uint8_t* l, const TaxiDev& p) {
+  return (const uint64_t*)(l + p.off_cdf);
+}
+__device__ __forceinline__ const uint16_t* l_valid(const uint8_t* l, const TaxiDev& p) {
+  return (const uint16_t*)(l + p.off_valid);
+}
+
+// Cooperative copy of the packed tables into LDS (16-B granules; tab_bytes is a multiple of 16).
+__device__ __forceinline__ void stage_tables(const TaxiDev& p, uint8_t* lds) {
+  const uint4* src = (const uint4*)p.tabs;
+  uint4* dst = (uint4*)lds;
+  for (int i = threadIdx.x; i < p.tab_bytes / 16; i += TPB) dst[i] = src[i];
+}
+
+// ---- the start-state law: smallest k with w < cdf[k] (cdf[n_valid-1] = 2^64-1, saturating) ----
+__device__ __forceinline__ uint32_t sample_reset_state(const TaxiDev& p, const uint8_t* lds, uint64_t w) {
+  const uint64_t* cdf = l_cdf(lds, p);
+  int lo = 0, hi = p.n_valid - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (w < cdf[mid]) hi = mid; else lo = mid + 1;
+  }
+  return l_valid(lds, p)[lo];
+}
+
+template <bool REPLAY>
+__device__ __forceinline__ uint32_t draw_reset(const TaxiDev& p, const uint8_t* lds, int env, uint64_t step) {
+  if constexpr (REPLAY) {
+    return (uint32_t)min(max(p.rp_state[env], 0), p.ns - 1);
+  } else {
+    const Philox4 r = philox4x32_10((uint32_t)env, (uint32_t)step, (uint32_t)(step >> 32), PHILOX_TAG, p.key0, p.key1);
+    return sample_reset_state(p, lds, ((uint64_t)r.x[0] << 32) | r.x[1]);
+  }
+}
+
+// extended_taxi.py:354-364: p = integers(L); d = integers(L), resampled while d == p. Its law is
+// p uniform and d uniform over the other L-1 locations.
+template <bool REPLAY>
+__device__ __forceinline__ uint32_t draw_pd(const TaxiDev& p, int env, uint64_t step) {
+  if constexpr (REPLAY) {
+    const uint32_t pd = (uint32_t)min(max(p.rp_pd[env], 0), p.nlocs * p.nlocs - 1);
+    return pd;
+  } else {
+    const Philox4 r = philox4x32_10((uint32_t)env, (uint32_t)step, (uint32_t)(step >> 32), PHILOX_TAG, p.key0, p.key1);
+    const uint32_t pp = lemire_value(r.x[2], (uint32_t)p.nlocs);
+    uint32_t dd = lemire_value(r.x[3], (uint32_t)(p.nlocs - 1));
+    dd += dd >= pp ? 1u : 0u;
+    return pp * (uint32_t)p.nlocs + dd;
+  }
+}
+
+struct StepOut {
+  float rew;
+  uint8_t term, trunc;
+};
+
+// One env-step of TaxiVecEnv.step (extended_taxi.py:244-287) on the packed state `u`.
+template <bool REPLAY>
+__device__ __forceinline__ StepOut taxi_env_step(const TaxiDev& p, const uint8_t* lds, uint32_t& u, int a, int env,
+                                                 bool live, uint64_t step, float& rsum, uint32_t& eps,
+                                                 uint32_t& lens) {
+  uint32_t s = u & 0xFFFu, nd = (u >> 12) & 0xFu, el = (u >> 16) + 1u;  // elapsed += 1 (:245)
+  if (a < 0) a += NACT;                       // numpy negative indexing of ACTIONS_YX[actions]
+  a = min(max(a, 0), NACT - 1);               // (out-of-range actions raise in the reference; clamped)
+  const uint32_t t = l_trans(lds, p)[s * NACT + (uint32_t)a];
+  s = t & 0xFFFu;
+  const uint32_t goal = (t >> 12) & 1u, bad = (t >> 13) & 1u;
+  nd += goal;                                 // n_dropoffs_completed[goal_move] += 1 (:266)
+  StepOut o;
+  o.rew = goal ? p.r_goal : (bad ? p.r_bad : p.r_any);
+  o.term = (nd == (uint32_t)p.num_passengers) ? 1 : 0;
+  o.trunc = (el > (uint32_t)p.time_limit) ? 1 : 0;
+  if (!live) return o;                        // padding lane of a ragged batch: no draws, no metrics
+  rsum += o.rew;
+  if (goal && !(o.term | o.trunc)) {          // task completed, episode continues (:281-284)
+    const uint32_t pd = draw_pd<REPLAY>(p, env, step);
+    s = (s / (uint32_t)p.lpl) * (uint32_t)p.lpl + pd;  // encode(r, c, p, d): taxi cell kept
+  }
+  if (o.term | o.trunc) {                     // _reset_mask(done | truncated) (:285, :344-352)
+    eps += 1u;
+    lens += el;
+    s = draw_reset<REPLAY>(p, lds, env, step);
+    el = 0u;
+    nd = 0u;
+  }
+  u = s | (nd << 12) | (min(el, 0xFFFFu) << 16);
+  return o;
+}
+
+// ---- vector I/O (4 consecutive envs per thread) ----
+__device__ __forceinline__ bool quad_ok(const void* base, int env0, int B, int esz) {
+  return env0 + 3 < B && ((((uintptr_t)base) + (size_t)env0 * esz) & (size_t)(4 * esz - 1)) == 0;
+}
+__device__ __forceinline__ void ld4_u32(const uint32_t* __restrict__ p, int env0, int B, uint32_t (&v)[4]) {
+  if (quad_ok(p, env0, B, 4)) {
+    const uint4 q = *reinterpret_cast<const uint4*>(p + env0);
+    v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = env0 + i < B ? p[env0 + i] : 0u;
+  }
+}
+__device__ __forceinline__ void st4_u32(uint32_t* __restrict__ p, int env0, int B, const uint32_t (&v)[4]) {
+  if (quad_ok(p, env0, B, 4)) {
+    *reinterpret_cast<uint4*>(p + env0) = make_uint4(v[0], v[1], v[2], v[3]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (env0 + i < B) p[env0 + i] = v[i];
+  }
+}
+__device__ __forceinline__ void st4_u8(uint8_t* __restrict__ p, int env0, int B, const uint8_t (&v)[4]) {
+  if (quad_ok(p, env0, B, 1)) {
+    *reinterpret_cast<uint32_t*>(p + env0) =
+        (uint32_t)v[0] | ((uint32_t)v[1] << 8) | ((uint32_t)v[2] << 16) | ((uint32_t)v[3] << 24);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (env0 + i < B) p[env0 + i] = v[i];
+  }
+}
+
+// ---- one-hot rows as a wave-contiguous chunk stream ----
+// The wave owns envs [e0, e0 + n) (lane l holds envs 4l..4l+3), i.e. the byte range
+// [e0*W, (e0+n)*W) of the output. Lane l writes chunks q = l, l+64, ... of CS bytes each; the
+// host guarantees W % CS == 0 and a CS-aligned range, so a chunk never straddles two rows. The
+// hot indices of the wave's envs are exchanged through a per-wave LDS array.
+template <int CS>
+__device__ __forceinline__ void write_onehot_wave(uint8_t* __restrict__ out, int n, int W, uint16_t* hs,
+                                                  const uint32_t (&h)[4], int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) hs[lane * 4 + i] = (uint16_t)h[i];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int cpe = W / CS;                 // chunks per env row
+  const int nchunks = n * cpe;
+  // lane's first chunk q = lane: env = lane / cpe, chunk-in-row c = lane % cpe; then += 64 chunks
+  int e = lane / cpe, c = lane - e * cpe;
+  const int de = 64 / cpe, dc = 64 - de * cpe;
+  for (int q = lane; q < nchunks; q += 64) {
+    const uint32_t hot = hs[e];
+    const int hc = (int)(hot / CS), hb = (int)(hot - (uint32_t)hc * CS);
+    uint8_t* dst = out + (size_t)q * CS;
+    if constexpr (CS == 16) {
+      const uint32_t m = (c == hc) ? (1u << ((hb & 3) * 8)) : 0u;
+      const int w = hb >> 2;
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      u32x4 v;
+      v.x = w == 0 ? m : 0u; v.y = w == 1 ? m : 0u; v.z = w == 2 ? m : 0u; v.w = w == 3 ? m : 0u;
+      __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst));
+    } else if constexpr (CS == 4) {
+      const uint32_t m = (c == hc) ? (1u << (hb * 8)) : 0u;
+      __builtin_nontemporal_store(m, reinterpret_cast<uint32_t*>(dst));
+    } else {
+      *dst = (c == hc) ? 1 : 0;
+    }
+    e += de;
+    c += dc;
+    if (c >= cpe) { c -= cpe; e += 1; }
+  }
+  __builtin_amdgcn_wave_barrier();  // hs is rewritten by the next step
+}
+
+// Per-block metrics into the block's own slot (the grid is persistent: block b owns slot b).
+__device__ void taxi_metrics(const TaxiDev& p, float rsum, uint32_t eps, uint32_t lens, uint32_t nst) {
+  __shared__ float s_r[WAVES];
+  __shared__ uint32_t s_e[WAVES], s_l[WAVES], s_n[WAVES];
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    rsum += __shfl_xor(rsum, d, 64);
+    eps += __shfl_xor(eps, d, 64);
+    lens += __shfl_xor(lens, d, 64);
+    nst += __shfl_xor(nst, d, 64);
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) { s_r[wid] = rsum; s_e[wid] = eps; s_l[wid] = lens; s_n[wid] = nst; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float r = 0.f;
+    unsigned long long e = 0, l = 0, n = 0;
+    for (int w = 0; w < WAVES; ++w) { r += s_r[w]; e += s_e[w]; l += s_l[w]; n += s_n[w]; }
+    TaxiSlot& m = p.mslot[blockIdx.x];
+    m.return_sum += (double)r;
+    m.episodes += e;
+    m.length_sum += l;
+    m.env_steps += n;
+  }
+}
+
+// ---- the rollout kernel: K steps for every env, persistent over 1024-env tiles ----
+// OH = 0: scalar int32 obs [K,B]; OH = CS in {16, 4, 1}: one-hot uint8 [K,B,n_obs] in CS-byte chunks.
+template <int OH, bool REPLAY>
+__global__ __launch_bounds__(TPB) void taxi_rollout(TaxiDev p, int K, uint64_t step0, const int32_t* __restrict__ act,
+                                                    void* __restrict__ obs, float* __restrict__ rew,
+                                                    uint8_t* __restrict__ term, uint8_t* __restrict__ trunc) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  __shared__ uint16_t s_hot[WAVES][256];
+  stage_tables(p, lds);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float rsum = 0.f;
+  uint32_t eps = 0, lens = 0, nst = 0;
+  const uint16_t* obs_of = l_obs(lds, p);
+  for (int tile = blockIdx.x; tile < p.ntiles; tile += gridDim.x) {
+    const int env0 = tile * EPB + threadIdx.x * EPT;
+    uint32_t u[4];
+    ld4_u32(p.st, env0, p.B, u);
+    for (int k = 0; k < K; ++k) {
+      const size_t off = (size_t)k * p.B;
+      uint32_t a4[4];
+      ld4_u32(reinterpret_cast<const uint32_t*>(act + off), env0, p.B, a4);
+      float r[4];
+      uint8_t tm[4], tr[4];
+      uint32_t h[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bool live = env0 + i < p.B;
+        StepOut o = taxi_env_step<REPLAY>(p, lds, u[i], (int)a4[i], env0 + i, live, step0 + (uint64_t)k, rsum, eps,
+                                          lens);
+        r[i] = o.rew;
+        tm[i] = o.term;
+        tr[i] = o.trunc;
+        h[i] = obs_of[u[i] & 0xFFFu];
+        nst += live ? 1u : 0u;
+      }
+      st4_u32(reinterpret_cast<uint32_t*>(rew + off), env0, p.B,
+              {__float_as_uint(r[0]), __float_as_uint(r[1]), __float_as_uint(r[2]), __float_as_uint(r[3])});
+      st4_u8(term + off, env0, p.B, tm);
+      st4_u8(trunc + off, env0, p.B, tr);
+      if constexpr (OH == 0) {
+        st4_u32(reinterpret_cast<uint32_t*>(obs) + off, env0, p.B, h);
+      } else {
+        const int we0 = tile * EPB + wid * 256;  // first env of this wave
+        const int n = min(256, p.B - we0);
+        if (n > 0)
+          write_onehot_wave<OH>((uint8_t*)obs + (off + (size_t)we0) * (size_t)p.n_obs, n, p.n_obs, s_hot[wid], h,
+                                lane);
+      }
+    }
+    st4_u32(p.st, env0, p.B, u);
+  }
+  taxi_metrics(p, rsum, eps, lens, nst);
+}
+
+// reset(): every env draws a start state (extended_taxi.py:232-242); one step index of the stream.
+template <int OH, bool REPLAY>
+__global__ __launch_bounds__(TPB) void taxi_reset(TaxiDev p, uint64_t step, void* __restrict__ obs) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  __shared__ uint16_t s_hot[WAVES][256];
+  stage_tables(p, lds);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int tile = blockIdx.x; tile < p.ntiles; tile += gridDim.x) {
+    const int env0 = tile * EPB + threadIdx.x * EPT;
+    uint32_t u[4], h[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int env = env0 + i;
+      u[i] = env < p.B ? draw_reset<REPLAY>(p, lds, env, step) : 0u;
+      h[i] = l_obs(lds, p)[u[i]];
+    }
+    st4_u32(p.st, env0, p.B, u);
+    if constexpr (OH == 0) {
+      st4_u32(reinterpret_cast<uint32_t*>(obs), env0, p.B, h);
+    } else {
+      const int we0 = tile * EPB + wid * 256;
+      const int n = min(256, p.B - we0);
+      if (n > 0) write_onehot_wave<OH>((uint8_t*)obs + (size_t)we0 * p.n_obs, n, p.n_obs, s_hot[wid], h, lane);
+    }
+  }
+}
+
+__global__ void taxi_get_state(TaxiDev p, int32_t* s, int32_t* elapsed, int32_t* nd) {
+  const int env = blockIdx.x * TPB + threadIdx.x;
+  if (env >= p.B) return;
+  const uint32_t u = p.st[env];
+  if (s) s[env] = (int32_t)(u & 0xFFFu);
+  if (nd) nd[env] = (int32_t)((u >> 12) & 0xFu);
+  if (elapsed) elapsed[env] = (int32_t)(u >> 16);
+}
+__global__ void taxi_set_state(TaxiDev p, const int32_t* s, const int32_t* elapsed, const int32_t* nd) {
+  const int env = blockIdx.x * TPB + threadIdx.x;
+  if (env >= p.B) return;
+  uint32_t u = p.st[env];
+  if (s) u = (u & ~0xFFFu) | (uint32_t)min(max(s[env], 0), p.ns - 1);
+  if (nd) u = (u & ~0xF000u) | ((uint32_t)min(max(nd[env], 0), 15) << 12);
+  if (elapsed) u = (u & 0xFFFFu) | ((uint32_t)min(max(elapsed[env], 0), 65535) << 16);
+  p.st[env] = u;
+}
+
+// ------------------------------------------------------------------ host backend ----
+struct TaxiBackend : EnvBackend {
+  TaxiDev d{};
+  int grid = 1;                 // persistent grid size (= metric slots)
+  int one_hot = 0;
+  uint64_t philox_step = 0;
+  std::vector<double> law;      // P(start state = valid[k])
+  DevBuf b_tabs, b_st, b_slot;
+  const int32_t* rp_state = nullptr;
+  const int32_t* rp_pd = nullptr;
+
+  int build(const gp_taxi_config* cfg);
+  int seed(const RngHost& r, const uint32_t key[2]) override {
+    rng = r;
+    philox_key[0] = key[0];
+    philox_key[1] = key[1];
+    d.key0 = key[0];
+    d.key1 = key[1];
+    philox_step = 0;
+    return GP_OK;
+  }
+  int set_rng_state(const RngHost& r) override {
+    gp_set_error("taxi: the PCG64 stream is not used on the device (philox / replay modes)");
+    return GP_E_UNSUPPORTED;
+  }
+  int get_rng_state(RngHost* r) override {
+    gp_set_error("taxi: the PCG64 stream is not used on the device (philox / replay modes)");
+    return GP_E_UNSUPPORTED;
+  }
+  // Largest chunk size the one-hot stream may use for these buffers.
+  int chunk_size(const void* obs, int K) const {
+    for (int cs : {16, 4}) {
+      if (d.n_obs % cs) continue;
+      if (((uintptr_t)obs) % cs) continue;
+      if (K > 1 && ((size_t)B * d.n_obs) % cs) continue;
+      return cs;
+    }
+    return 1;
+  }
+  TaxiDev dev_for_launch() const {
+    TaxiDev dd = d;
+    dd.rp_state = rp_state;
+    dd.rp_pd = rp_pd;
+    return dd;
+  }
+  template <bool REPLAY>
+  void launch_rollout(int cs, int K, uint64_t step0, const void* act, void* obs, float* rew, uint8_t* term,
+                      uint8_t* trunc, hipStream_t s) {
+    const TaxiDev dd = dev_for_launch();
+    const dim3 g((unsigned)grid), b(TPB);
+    const size_t lds = (size_t)d.tab_bytes;
+    const int32_t* a = (const int32_t*)act;
+    if (!one_hot)
+      hipLaunchKernelGGL((taxi_rollout<0, REPLAY>), g, b, lds, s, dd, K, step0, a, obs, rew, term, trunc);
+    else if (cs == 16)
+      hipLaunchKernelGGL((taxi_rollout<16, REPLAY>), g, b, lds, s, dd, K, step0, a, obs, rew, term, trunc);
+    else if (cs == 4)
+      hipLaunchKernelGGL((taxi_rollout<4, REPLAY>), g, b, lds, s, dd, K, step0, a, obs, rew, term, trunc);
+    else
+      hipLaunchKernelGGL((taxi_rollout<1, REPLAY>), g, b, lds, s, dd, K, step0, a, obs, rew, term, trunc);
+  }
+  template <bool REPLAY>
+  void launch_reset(int cs, uint64_t step, void* obs, hipStream_t s) {
+    const TaxiDev dd = dev_for_launch();
+    const dim3 g((unsigned)grid), b(TPB);
+    const size_t lds = (size_t)d.tab_bytes;
+    if (!one_hot) hipLaunchKernelGGL((taxi_reset<0, REPLAY>), g, b, lds, s, dd, step, obs);
+    else if (cs == 16) hipLaunchKernelGGL((taxi_reset<16, REPLAY>), g, b, lds, s, dd, step, obs);
+    else if (cs == 4) hipLaunchKernelGGL((taxi_reset<4, REPLAY>), g, b, lds, s, dd, step, obs);
+    else hipLaunchKernelGGL((taxi_reset<1, REPLAY>), g, b, lds, s, dd, step, obs);
+  }
+  int reset(void* obs, hipStream_t s) override {
+    GP_HIP_CHECK(hipMemsetAsync(d.mslot, 0, sizeof(TaxiSlot) * grid, s));
+    const int cs = chunk_size(obs, 1);
+    if (rng_mode == GP_RNG_REPLAY) {
+      if (!rp_state) {
+        gp_set_error("taxi replay reset needs reset states (gp_set_replay i0)");
+        return GP_E_STATE;
+      }
+      launch_reset<true>(cs, 0, obs, s);
+    } else {
+      launch_reset<false>(cs, philox_step, obs, s);
+      ++philox_step;
+    }
+    GP_HIP_CHECK(hipGetLastError());
+    has_reset = true;
+    return GP_OK;
+  }
+  int rollout(int K, const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc, hipStream_t s) override {
+    if (!has_reset) {
+      gp_set_error("step() before reset()");
+      return GP_E_STATE;
+    }
+    if (rng_mode == GP_RNG_REPLAY) {
+      if (!rp_state || (d.num_passengers > 1 && !rp_pd)) {
+        gp_set_error("taxi replay step needs reset states (i0) and, with num_passengers > 1, p/d pairs (i1)");
+        return GP_E_STATE;
+      }
+      if (K > 1) return EnvBackend::rollout(K, act, obs, rew, term, trunc, s);  // one draw set per step
+    }
+    const int cs = chunk_size(obs, K);
+    timer.begin(s);
+    if (rng_mode == GP_RNG_REPLAY) launch_rollout<true>(cs, K, 0, act, obs, rew, term, trunc, s);
+    else launch_rollout<false>(cs, K, philox_step, act, obs, rew, term, trunc, s);
+    timer.end(s);
+    GP_HIP_CHECK(hipGetLastError());
+    if (rng_mode != GP_RNG_REPLAY) philox_step += (uint64_t)K;
+    return GP_OK;
+  }
+  int step(const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc, hipStream_t s) override {
+    return rollout(1, act, obs, rew, term, trunc, s);
+  }
+  int get_state(void* a, void* b, void* c, void* dd, hipStream_t s) override {
+    hipLaunchKernelGGL(taxi_get_state, dim3((unsigned)((B + TPB - 1) / TPB)), dim3(TPB), 0, s, d, (int32_t*)a,
+                       (int32_t*)b, (int32_t*)c);
+    GP_HIP_CHECK(hipGetLastError());
+    return GP_OK;
+  }
+  int set_state(const void* a, const void* b, const void* c, const void* dd, hipStream_t s) override {
+    hipLaunchKernelGGL(taxi_set_state, dim3((unsigned)((B + TPB - 1) / TPB)), dim3(TPB), 0, s, d,
+                       (const int32_t*)a, (const int32_t*)b, (const int32_t*)c);
+    GP_HIP_CHECK(hipGetLastError());
+    has_reset = true;
+    return GP_OK;
+  }
+  int set_replay(const void* u, const void* i0, const void* i1, const void* f0, const void* f1) override {
+    if (rng_mode != GP_RNG_REPLAY) {
+      gp_set_error("gp_set_replay requires GP_RNG_REPLAY");
+      return GP_E_STATE;
+    }
+    rp_state = (const int32_t*)i0;
+    rp_pd = (const int32_t*)i1;
+    return GP_OK;
+  }
+  int metrics(double out[4]) override {
+    GP_HIP_CHECK(hipDeviceSynchronize());
+    std::vector<TaxiSlot> m(grid);
+    GP_HIP_CHECK(hipMemcpy(m.data(), d.mslot, sizeof(TaxiSlot) * grid, hipMemcpyDeviceToHost));
+    out[0] = out[1] = out[2] = out[3] = 0;
+    for (const TaxiSlot& x : m) {
+      out[0] += (double)x.episodes;
+      out[1] += x.return_sum;
+      out[2] += (double)x.length_sum;
+      out[3] += (double)x.env_steps;
+    }
+    return GP_OK;
+  }
+  int reset_distribution(double* out, int cap) const override {
+    for (int k = 0; k < (int)law.size() && k < cap; ++k) out[k] = law[k];
+    return (int)law.size();
+  }
+};
+
+int TaxiBackend::build(const gp_taxi_config* cfg) {
+  const int R = cfg->rows, C = cfg->cols, L = cfg->n_locs;
+  const int DR = cfg->desc_rows, DC = cfg->desc_cols;
+  if (R < 1 || C < 1 || L < 1 || !cfg->desc || !cfg->locs) {
+    gp_set_error("taxi: bad map (rows=%d cols=%d n_locs=%d)", R, C, L);
+    return GP_E_INVALID;
+  }
+  const bool pseudo = cfg->pseudo_walls != 0;
+  if (DR != R + 2 || DC != (pseudo ? 2 * C + 1 : C + 2)) {
+    gp_set_error("taxi: desc %dx%d does not border a %dx%d grid", DR, DC, R, C);
+    return GP_E_INVALID;
+  }
+  const int ns = R * C * L * (L + 1);
+  if (ns > MAX_NS) {
+    gp_set_error("taxi: %d states exceed the packed-state limit %d", ns, MAX_NS);
+    return GP_E_INVALID;
+  }
+  if (cfg->num_passengers < 0 || cfg->num_passengers > 15) {
+    gp_set_error("taxi: num_passengers %d outside [0, 15]", cfg->num_passengers);
+    return GP_E_INVALID;
+  }
+  if (cfg->num_passengers > 1 && L < 2) {
+    gp_set_error("taxi: num_passengers > 1 needs >= 2 locations (the reference's d != p loop never ends)");
+    return GP_E_INVALID;
+  }
+  if (cfg->time_limit < 0 || cfg->time_limit > 65534) {
+    gp_set_error("taxi: time_limit %d outside [0, 65534]", cfg->time_limit);
+    return GP_E_INVALID;
+  }
+  if (cfg->obs_kind != GP_OBS_TABLE && cfg->obs_kind != GP_OBS_HANSEN) {
+    gp_set_error("taxi: obs_kind must be GP_OBS_TABLE (state) or GP_OBS_HANSEN");
+    return GP_E_INVALID;
+  }
+  auto desc = [&](int r, int c) { return cfg->desc[(size_t)r * DC + c]; };
+  auto cc_r = [&](int r) { return r + 1; };
+  auto cc_c = [&](int c) { return pseudo ? 2 * c + 1 : c + 1; };
+  std::vector<int> loc_r(L + 1), loc_c(L + 1);
+  for (int i = 0; i < L; ++i) {
+    loc_r[i] = cfg->locs[2 * i];
+    loc_c[i] = cfg->locs[2 * i + 1];
+  }
+  loc_r[L] = loc_c[L] = -1;  // extraneous "in taxi" location (extended_taxi.py:185)
+  auto encode = [&](int r, int c, int p, int dd) { return ((r * C + c) * (L + 1) + p) * L + dd; };
+  // generate_hansen_map (extended_taxi.py:102-114): N=1, S=2, W=4, E=8
+  std::vector<int> hansen((size_t)R * C);
+  for (int r = 0; r < R; ++r)
+    for (int c = 0; c < C; ++c) {
+      const int br = cc_r(r), bc = cc_c(c);
+      hansen[(size_t)r * C + c] = (desc(br - 1, bc) == '|') + 2 * (desc(br + 1, bc) == '|') +
+                                  4 * (desc(br, bc - 1) == '|') + 8 * (desc(br, bc + 1) == '|');
+    }
+  static const int AY[NACT] = {-1, 1, 0, 0, 0}, AX[NACT] = {0, 0, -1, 1, 0};
+  std::vector<uint16_t> trans((size_t)ns * NACT), obs_of(ns);
+  for (int s = 0; s < ns; ++s) {
+    const int dd = s % L, t1 = s / L, p = t1 % (L + 1), t2 = t1 / (L + 1), c = t2 % C, r = t2 / C;
+    obs_of[s] = (uint16_t)(cfg->obs_kind == GP_OBS_HANSEN ? (hansen[(size_t)r * C + c] * (L + 1) + p) * L + dd : s);
+    for (int a = 0; a < NACT; ++a) {
+      // extended_taxi.py:248-260
+      const int rn = std::min(std::max(r + AY[a], 0), R - 1), cn = std::min(std::max(c + AX[a], 0), C - 1);
+      const int br = cc_r(rn), bc = cc_c(cn);
+      bool ok = desc(br, bc) != '|';
+      if (AX[a] != 0 && desc(br, bc - AX[a]) == '|') ok = false;
+      const int r2 = ok ? rn : r, c2 = ok ? cn : c;
+      // extended_taxi.py:262-275 (goal evaluated on the pre-update p; a dropoff keeps p)
+      int p2 = p, goal = 0, bad = 0;
+      if (a == 4) {
+        goal = (p == L) && loc_r[dd] == r2 && loc_c[dd] == c2;
+        const int pick = (p < L) && loc_r[p] == r2 && loc_c[p] == c2;
+        if (pick) p2 = L;
+        bad = !goal && !pick;
+      }
+      trans[(size_t)s * NACT + a] = (uint16_t)(encode(r2, c2, p2, dd) | (goal << 12) | (bad << 13));
+    }
+  }
+  // valid start states (extended_taxi.py:208-218), ascending, and the argmax-multinomial law
+  std::vector<uint16_t> valid;
+  for (int r = 0; r < R; ++r)
+    for (int c = 0; c < C; ++c) {
+      const char g = desc(cc_r(r), cc_c(c));
+      if (g == '|') continue;
+      for (int p = 0; p < L; ++p)
+        for (int dd = 0; dd < L; ++dd)
+          if (dd != p) valid.push_back((uint16_t)encode(r, c, p, dd));
+    }
+  if (valid.empty()) {
+    gp_set_error("taxi: no valid start state");
+    return GP_E_INVALID;
+  }
+  const int V = (int)valid.size();
+  law = argmax_multinomial_distribution(V, ns);
+  long double tot = 0.0L;
+  for (double v : law) tot += v;
+  std::vector<uint64_t> cdf(V);
+  long double acc = 0.0L;
+  const long double two64 = 18446744073709551616.0L;
+  for (int k = 0; k < V; ++k) {
+    acc += law[k];
+    const long double x = acc / tot * two64;
+    cdf[k] = (k == V - 1 || x >= two64) ? ~0ull : (uint64_t)x;
+  }
+  // pack: trans | obs_of | cdf | valid, each 16-B aligned
+  auto al16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+  const size_t o_trans = 0, o_obs = al16(o_trans + trans.size() * 2), o_cdf = al16(o_obs + obs_of.size() * 2),
+               o_valid = al16(o_cdf + cdf.size() * 8), total = al16(o_valid + valid.size() * 2);
+  std::vector<uint8_t> blob(total, 0);
+  memcpy(blob.data() + o_trans, trans.data(), trans.size() * 2);
+  memcpy(blob.data() + o_obs, obs_of.data(), obs_of.size() * 2);
+  memcpy(blob.data() + o_cdf, cdf.data(), cdf.size() * 8);
+  memcpy(blob.data() + o_valid, valid.data(), valid.size() * 2);
+  if (int e = b_tabs.upload(blob)) return e;
+  d.tabs = b_tabs.as<uint8_t>();
+  d.off_trans = (int)o_trans;
+  d.off_obs = (int)o_obs;
+  d.off_cdf = (int)o_cdf;
+  d.off_valid = (int)o_valid;
+  d.tab_bytes = (int)total;
+
+  d.B = (int32_t)B;
+  d.ntiles = (int32_t)((B + EPB - 1) / EPB);
+  d.ns = ns;
+  d.nlocs = L;
+  d.lpl = L * (L + 1);
+  d.n_valid = V;
+  d.num_passengers = cfg->num_passengers;
+  d.time_limit = cfg->time_limit;
+  d.n_obs = cfg->obs_kind == GP_OBS_HANSEN ? 16 * L * (L + 1) : ns;  // compute_obs_space (:72-81)
+  d.r_goal = cfg->reward_goal;
+  d.r_bad = cfg->reward_bad;
+  d.r_any = cfg->reward_any;
+  one_hot = cfg->one_hot != 0;
+  obs_dtype = one_hot ? GP_DTYPE_U8 : GP_DTYPE_I32;
+  obs_width = one_hot ? d.n_obs : 1;
+
+  if (int e = b_st.alloc((size_t)B * 4 + 16)) return e;
+  d.st = b_st.as<uint32_t>();
+  // persistent grid: as many blocks as are co-resident, capped by the number of tiles
+  hipDeviceProp_t prop;
+  GP_HIP_CHECK(hipGetDeviceProperties(&prop, device));
+  int occ = 0;
+  GP_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, taxi_rollout<16, false>, TPB, d.tab_bytes));
+  occ = std::max(1, std::min(occ, 8));
+  grid = std::max(1, std::min(d.ntiles, prop.multiProcessorCount * occ));
+  if (int e = b_slot.alloc(sizeof(TaxiSlot) * grid)) return e;
+  d.mslot = b_slot.as<TaxiSlot>();
+  if (d.tab_bytes > 64 * 1024) {
+    gp_set_error("taxi: tables (%d B) exceed the LDS budget", d.tab_bytes);
+    return GP_E_INVALID;
+  }
+  return GP_OK;
+}
+
+}  // namespace
+
+std::unique_ptr<EnvBackend> make_taxi_backend(const gp_taxi_config* cfg, int64_t B, int device, int rng_mode,
+                                              int* err) {
+  if (rng_mode == GP_RNG_NUMPY) {
+    gp_set_error("taxi: rng_mode numpy is not available on the device (the reference's multinomial reset draws "
+                 "~300 data-dependent binomials per env from one stream); use philox (same law) or replay");
+    *err = GP_E_UNSUPPORTED;
+    return nullptr;
+  }
+  if (B < 1 || B > (int64_t)1 << 30) {
+    gp_set_error("taxi: num_envs %lld out of range", (long long)B);
+    *err = GP_E_INVALID;
+    return nullptr;
+  }
+  auto be = std::make_unique<TaxiBackend>();
+  be->B = B;
+  be->device = device;
+  be->rng_mode = rng_mode;
+  if (hipSetDevice(device) != hipSuccess) {
+    gp_set_error("taxi: hipSetDevice(%d) failed", device);
+    *err = GP_E_HIP;
+    return nullptr;
+  }
+  int e = be->build(cfg);
+  if (e) {
+    *err = e;
+    return nullptr;
+  }
+  return be;
+}

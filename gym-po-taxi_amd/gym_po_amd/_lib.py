@@ -36,7 +36,8 @@ class TaxiConfig(ctypes.Structure):
     _fields_ = [("rows", ctypes.c_int32), ("cols", ctypes.c_int32), ("desc_rows", ctypes.c_int32),
                 ("desc_cols", ctypes.c_int32), ("desc", ctypes.c_char_p), ("pseudo_walls", ctypes.c_int32),
                 ("n_locs", ctypes.c_int32), ("locs", _i32p), ("num_passengers", ctypes.c_int32),
-                ("time_limit", ctypes.c_int32), ("obs_kind", ctypes.c_int32), ("reward_goal", ctypes.c_float),
+                ("time_limit", ctypes.c_int32), ("obs_kind", ctypes.c_int32), ("one_hot", ctypes.c_int32),
+                ("reward_goal", ctypes.c_float),
                 ("reward_bad", ctypes.c_float), ("reward_any", ctypes.c_float)]
 
 

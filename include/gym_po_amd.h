@@ -101,8 +101,10 @@ typedef struct gp_taxi_config {
   const int32_t* locs;     /* [n_locs*2] (row, col) of R,G,Y,B in row-major order               */
   int32_t num_passengers;
   int32_t time_limit;
-  int32_t obs_kind;        /* GP_OBS_TABLE (raw state), GP_OBS_HANSEN (hansen index) or
-                              GP_OBS_ONEHOT (one-hot of the hansen index, uint8 [B,320])         */
+  int32_t obs_kind;        /* GP_OBS_TABLE (raw state s, extended_taxi.py:368) or GP_OBS_HANSEN
+                              ((hansen[r,c]*(L+1)+p)*L+d, extended_taxi.py:370-372)              */
+  int32_t one_hot;         /* 1: emit that index one-hot, uint8 [B, n_obs] (GP_OBS_ONEHOT layout;
+                              a build-side encoding, the reference has none)                     */
   float reward_goal, reward_bad, reward_any;
 } gp_taxi_config;
 
