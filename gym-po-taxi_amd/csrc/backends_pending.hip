@@ -1,3 +1,2 @@
 #include "gp_internal.h"
-std::unique_ptr<EnvBackend> make_crooms_backend(const gp_crooms_config*, int64_t, int, int, int* err) { gp_set_error("crooms: not built"); *err = GP_E_UNSUPPORTED; return nullptr; }
 std::unique_ptr<EnvBackend> make_anttag_backend(const gp_anttag_config*, int64_t, int, int, int* err) { gp_set_error("anttag: not built"); *err = GP_E_UNSUPPORTED; return nullptr; }

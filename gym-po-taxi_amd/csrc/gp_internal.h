@@ -67,7 +67,7 @@ struct EnvBackend {
     gp_set_error("no reset distribution for this env kind");
     return GP_E_UNSUPPORTED;
   }
-  size_t obs_elem_size() const { return obs_dtype == GP_DTYPE_U8 ? 1 : 4; }
+  size_t obs_elem_size() const { return obs_dtype == GP_DTYPE_U8 ? 1 : (obs_dtype == GP_DTYPE_F64 ? 8 : 4); }
   virtual size_t rollout_action_bytes_per_env() const { return 4; }
 };
 

@@ -3,7 +3,8 @@
 //
 // The whole Taxi transition is a function of (state, action): no draw is made on a step unless the
 // env completes a task or resets. So the host lowers the map once into
-//   trans[s*5 + a] = s' | goal << 12 | bad << 13    (move, wall/pseudo-wall check, pickup/dropoff)
+//   trans[s*6 + a] = s' | goal << 12 | bad << 13    (move, wall/pseudo-wall check, pickup/dropoff;
+//                                                    column 5 = action -1, a no-op)
 //   obs_of[s]      = s  or  (hansen[r,c]*(L+1) + p)*L + d
 //   cdf[k]         = the exact start-state law of  multinomial(ns, uniform over valid).argmax()
 //                    (dist.hip) as 64-bit thresholds over the valid states, ascending
@@ -37,6 +38,7 @@ constexpr int EPT = 4;
 constexpr int EPB = TPB * EPT;  // envs per tile
 constexpr int WAVES = TPB / 64;
 constexpr int NACT = 5;         // N, S, W, E, Pickup/Dropoff (extended_taxi.py:154)
+constexpr int TCOL = NACT + 1;  // transition-table columns: the 5 actions + the action -1 no-op
 constexpr int MAX_NS = 4096;    // s fits 12 bits of the packed state
 constexpr uint32_t PHILOX_TAG = 0x74617869u;  // 'taxi'
 
@@ -128,9 +130,11 @@ __device__ __forceinline__ StepOut taxi_env_step(const TaxiDev& p, const uint8_t
                                                  bool live, uint64_t step, float& rsum, uint32_t& eps,
                                                  uint32_t& lens) {
   uint32_t s = u & 0xFFFu, nd = (u >> 12) & 0xFu, el = (u >> 16) + 1u;  // elapsed += 1 (:245)
-  if (a < 0) a += NACT;                       // numpy negative indexing of ACTIONS_YX[actions]
-  a = min(max(a, 0), NACT - 1);               // (out-of-range actions raise in the reference; clamped)
-  const uint32_t t = l_trans(lds, p)[s * NACT + (uint32_t)a];
+  // numpy negative indexing of ACTIONS_YX[actions]: -5..-2 are the moves, -1 moves (0,0) but is not
+  // a pickup/dropoff (p_or_d = actions == 4, extended_taxi.py:264) -> table column 5 (a no-op).
+  // Out-of-range actions raise in the reference; they are clamped here.
+  a = a < 0 ? (a == -1 ? NACT : max(a + NACT, 0)) : min(a, NACT - 1);
+  const uint32_t t = l_trans(lds, p)[s * TCOL + (uint32_t)a];
   s = t & 0xFFFu;
   const uint32_t goal = (t >> 12) & 1u, bad = (t >> 13) & 1u;
   nd += goal;                                 // n_dropoffs_completed[goal_move] += 1 (:266)
@@ -562,7 +566,7 @@ int TaxiBackend::build(const gp_taxi_config* cfg) {
                                   4 * (desc(br, bc - 1) == '|') + 8 * (desc(br, bc + 1) == '|');
     }
   static const int AY[NACT] = {-1, 1, 0, 0, 0}, AX[NACT] = {0, 0, -1, 1, 0};
-  std::vector<uint16_t> trans((size_t)ns * NACT), obs_of(ns);
+  std::vector<uint16_t> trans((size_t)ns * TCOL), obs_of(ns);
   for (int s = 0; s < ns; ++s) {
     const int dd = s % L, t1 = s / L, p = t1 % (L + 1), t2 = t1 / (L + 1), c = t2 % C, r = t2 / C;
     obs_of[s] = (uint16_t)(cfg->obs_kind == GP_OBS_HANSEN ? (hansen[(size_t)r * C + c] * (L + 1) + p) * L + dd : s);
@@ -581,8 +585,9 @@ int TaxiBackend::build(const gp_taxi_config* cfg) {
         if (pick) p2 = L;
         bad = !goal && !pick;
       }
-      trans[(size_t)s * NACT + a] = (uint16_t)(encode(r2, c2, p2, dd) | (goal << 12) | (bad << 13));
+      trans[(size_t)s * TCOL + a] = (uint16_t)(encode(r2, c2, p2, dd) | (goal << 12) | (bad << 13));
     }
+    trans[(size_t)s * TCOL + NACT] = (uint16_t)s;  // action -1: ACTIONS_YX[-1] = (0,0), not a pickup/dropoff
   }
   // valid start states (extended_taxi.py:208-218), ascending, and the argmax-multinomial law
   std::vector<uint16_t> valid;

@@ -13,7 +13,7 @@ GP_OK = 0
 GP_KIND_GRID, GP_KIND_TAXI, GP_KIND_CROOMS, GP_KIND_ANTTAG = 1, 2, 3, 4
 GP_RNG_NUMPY, GP_RNG_PHILOX, GP_RNG_REPLAY = 0, 1, 2
 RNG_MODES = {"numpy": GP_RNG_NUMPY, "philox": GP_RNG_PHILOX, "replay": GP_RNG_REPLAY}
-GP_DTYPE_I32, GP_DTYPE_U8, GP_DTYPE_F32 = 0, 1, 2
+GP_DTYPE_I32, GP_DTYPE_U8, GP_DTYPE_F32, GP_DTYPE_F64 = 0, 1, 2, 3
 GP_FLAVOR_ROOMS, GP_FLAVOR_MULTISTORY = 0, 1
 (GP_OBS_HANSEN, GP_OBS_HANSEN_VEC, GP_OBS_TABLE, GP_OBS_COORDS, GP_OBS_WINDOW, GP_OBS_ONEHOT,
  GP_OBS_F32) = range(7)
@@ -43,13 +43,15 @@ class TaxiConfig(ctypes.Structure):
 
 class CRoomsConfig(ctypes.Structure):
     _fields_ = [("height", ctypes.c_int32), ("width", ctypes.c_int32), ("cells", _i32p),
-                ("use_velocity", ctypes.c_int32), ("cell_size", ctypes.c_float), ("action_kind", ctypes.c_int32),
-                ("action_failure_probability", ctypes.c_double), ("action_std", ctypes.c_float),
-                ("action_power", ctypes.c_float), ("obs_kind", ctypes.c_int32), ("obs_dirs", ctypes.c_int32),
-                ("obs_goal", ctypes.c_int32), ("obs_n", ctypes.c_int32), ("obs_table", _i32p),
-                ("obs_table2", _i32p), ("fixed_goal", ctypes.c_int32), ("fixed_agent", ctypes.c_int32),
+                ("use_velocity", ctypes.c_int32), ("cell_size", ctypes.c_double), ("action_kind", ctypes.c_int32),
+                ("action_f64", ctypes.c_int32), ("action_failure_probability", ctypes.c_double),
+                ("action_std", ctypes.c_double), ("action_power", ctypes.c_double), ("obs_kind", ctypes.c_int32),
+                ("obs_f64", ctypes.c_int32), ("obs_dirs", ctypes.c_int32), ("obs_goal", ctypes.c_int32),
+                ("obs_n", ctypes.c_int32), ("obs_table", _i32p), ("obs_table2", _i32p),
+                ("goal_fixed", ctypes.c_int32), ("goal_y", ctypes.c_int32), ("goal_x", ctypes.c_int32),
+                ("agent_fixed", ctypes.c_int32), ("agent_y", ctypes.c_int32), ("agent_x", ctypes.c_int32),
                 ("time_limit", ctypes.c_int32), ("step_reward", ctypes.c_float), ("wall_reward", ctypes.c_float),
-                ("goal_reward", ctypes.c_float), ("goal_threshold", ctypes.c_float)]
+                ("goal_reward", ctypes.c_float), ("goal_threshold", ctypes.c_double)]
 
 
 class AntTagConfig(ctypes.Structure):

@@ -49,7 +49,7 @@ class NativeVecEnv:
         self._handle = h
         dt, w = ctypes.c_int(), ctypes.c_int()
         check(lib().gp_obs_info(h, ctypes.byref(dt), ctypes.byref(w)), "gp_obs_info")
-        self._obs_dtype = {0: torch.int32, 1: torch.uint8, 2: torch.float32}[dt.value]
+        self._obs_dtype = {0: torch.int32, 1: torch.uint8, 2: torch.float32, 3: torch.float64}[dt.value]
         self._obs_width = w.value
         self._seeded = False
         self._replay_keep = None
@@ -85,7 +85,7 @@ class NativeVecEnv:
 
     def _as_actions(self, actions, K=None):
         torch = _torch()
-        dt = torch.int32 if self._action_dtype == "int32" else torch.float32
+        dt = {"int32": torch.int32, "float32": torch.float32, "float64": torch.float64}[self._action_dtype]
         shape = ((self.num_envs,) if K is None else (K, self.num_envs)) + self._action_tail
         if isinstance(actions, torch.Tensor):
             a = actions.to(device=self.device, dtype=dt)

@@ -60,6 +60,7 @@ extern "C" {
 #define GP_DTYPE_I32 0
 #define GP_DTYPE_U8 1
 #define GP_DTYPE_F32 2
+#define GP_DTYPE_F64 3
 
 /* ---- GRID config (FourRooms / ROOMS) ---- */
 #define GP_FLAVOR_ROOMS 0      /* rooms.py: wall == -1, binary Hansen (observations.py:44-71)       */
@@ -110,20 +111,26 @@ typedef struct gp_taxi_config {
 
 typedef struct gp_crooms_config {
   int32_t height, width;
-  const int32_t* cells;    /* room-id grid, wall == -1                                          */
-  int32_t use_velocity;
-  float cell_size;
-  int32_t action_kind;     /* 0 = continuous (y,x); 4 / 8 = discrete cardinal / ordinal        */
+  const int32_t* cells;    /* room-id grid, wall == -1 (layouts.py np_to_grid)                    */
+  int32_t use_velocity;    /* crooms.py:304-310: v = clip(v + a, +-5), proposed = agent + v        */
+  double cell_size;        /* >= 1 (smaller cells index past the grid: the reference raises)       */
+  int32_t action_kind;     /* 0 = continuous (y,x) [B,2]; 4 / 8 = discrete cardinal / ordinal [B]  */
+  int32_t action_f64;      /* continuous actions are float64 [B,2] (1) or float32 [B,2] (0)        */
   double action_failure_probability;
-  float action_std, action_power;
-  int32_t obs_kind;        /* GP_OBS_F32 (vector mdp) or the discrete kinds on the cell        */
+  double action_std, action_power;
+  int32_t obs_kind;        /* GP_OBS_F32 (vector mdp: agent [+ goal] y,x) or GP_OBS_HANSEN /
+                              _HANSEN_VEC / _TABLE / _WINDOW evaluated on floor(coord / cell_size)  */
+  int32_t obs_f64;         /* GP_OBS_F32 emitted as float64 (GP_DTYPE_F64) instead of float32       */
   int32_t obs_dirs, obs_goal, obs_n;
-  const int32_t* obs_table;
-  const int32_t* obs_table2;
-  int32_t fixed_goal;      /* flat cell or -1                                                   */
-  int32_t fixed_agent;     /* flat cell or -1                                                   */
+  const int32_t* obs_table;  /* GP_OBS_TABLE: per-cell value for the agent [height*width]         */
+  const int32_t* obs_table2; /* GP_OBS_TABLE: per-cell value for the goal (may be NULL)           */
+  int32_t goal_fixed;      /* 1: goal cell (goal_y, goal_x) every reset (may lie off the grid)    */
+  int32_t goal_y, goal_x;
+  int32_t agent_fixed;     /* 1: agent cell (agent_y, agent_x) every reset                         */
+  int32_t agent_y, agent_x;
   int32_t time_limit;
-  float step_reward, wall_reward, goal_reward, goal_threshold;
+  float step_reward, wall_reward, goal_reward;
+  double goal_threshold;   /* terminated = ||agent - goal||_2 <= goal_threshold (float64)         */
 } gp_crooms_config;
 
 typedef struct gp_anttag_config {
@@ -171,16 +178,17 @@ int gp_rollout(gp_env* env, int K, const void* actions, void* obs, float* rew, u
                void* stream);
 
 /* Canonical state (device pointers, int32 unless noted). GRID: agent cell, goal cell, elapsed
- * [B] each. TAXI: s, elapsed, n_dropoffs. CROOMS: agent yx f32[B,2], goal yx f32[B,2],
- * velocity f32[B,2], elapsed i32[B]. ANTTAG: agent cell, target cell, elapsed. */
+ * [B] each. TAXI: s, elapsed, n_dropoffs. CROOMS: agent yx f64[B,2], goal cell yx i32[B,2],
+ * velocity f64[B,2], elapsed i32[B]. ANTTAG: agent cell, target cell, elapsed. */
 int gp_get_state(gp_env* env, void* a, void* b, void* c, void* d, void* stream);
 int gp_set_state(gp_env* env, const void* a, const void* b, const void* c, const void* d, void* stream);
 
 /* Replay mode: device pointers holding this step's pre-decided per-env draws (read by the next
  * gp_step). GRID: uniform k53 uint64 [B] (u = k*2^-53), goal index int32 [B], agent index
  * int32 [B] (indices into the valid-cell lists). TAXI: reset state int32 [B], passenger/dest
- * pair int32 [B] (p*n_locs+d). CROOMS: action noise f32 [B,2], wall noise f32 [B,2],
- * goal/agent index int32 [B] each (+ uniform k53 for discrete actions in `u`). */
+ * pair int32 [B] (p*n_locs+d). CROOMS: action noise f64 [B,2] (the value numpy's
+ * normal(scale=action_std) returned), wall noise f64 [B,2] (normal(scale=0.5)), goal/agent index
+ * int32 [B] each, uniform k53 uint64 [B] for discrete action failures. */
 int gp_set_replay(gp_env* env, const void* u, const void* i0, const void* i1, const void* f0, const void* f1);
 
 /* Valid-cell lists (host copies) used by the index draws: which = 0 goal, 1 agent. */

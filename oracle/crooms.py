@@ -133,7 +133,11 @@ class CRoomsOracle:
 
     def _normal(self, draws, scale, mask, site):
         if isinstance(draws, NumpyDraws):
-            return draws.normal(scale, int(mask.sum()), site).astype(self.f)
+            v = draws.normal(scale, int(mask.sum()), site)
+            hook = getattr(draws, "record_normal", None)  # tests: capture the stream's values per env
+            if hook is not None:
+                hook(site, mask, v)
+            return v.astype(self.f)
         return draws.normal_masked(mask, site).astype(self.f)
 
     def _sample_action(self, a, draws):

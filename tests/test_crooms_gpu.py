@@ -1,0 +1,204 @@
+"""GPU parity of the C-ROOMS backend (csrc/crooms.hip) against the reference fixtures and the oracle.
+
+The device computes in float64 exactly as the reference. Replay mode is fed the values the
+reference's own numpy stream produced (captured from the fixture-pinned oracle run on the same seed):
+with float64 I/O every output must equal the reference bit-for-bit; with float32 I/O (BASELINE
+configs[4]) the observation must be the float64 reference observation rounded once to float32, i.e.
+|obs - ref| <= 2^-24 |ref| (<= 1e-6 for the coordinates of every layout) — tolerance written below.
+Philox mode is checked in law (Box-Muller normals) and for rollout/step consistency.
+"""
+import numpy as np
+import pytest
+
+from fixtures import digest, load_case, load_index, step_actions
+from oracle.crooms import CRoomsOracle
+from oracle.draws import NumpyDraws
+
+pytestmark = pytest.mark.gpu
+
+CASES = {k: v for k, v in load_index()["cases"].items() if v["kind"] == "crooms"}
+F32_REL_TOL = 2.0 ** -24  # one float32 rounding of the float64 observation
+
+
+class RecordingDraws(NumpyDraws):
+    """The reference's numpy calls (NumpyDraws) + per-env capture of every value for GPU replay."""
+
+    def __init__(self, gen, B, valid):
+        super().__init__(gen)
+        self.B, self.valid, self.rec = B, valid, {}
+
+    def uniform(self, n):
+        u = super().uniform(n)
+        self.rec["u"] = np.round(u * 2.0 ** 53).astype(np.uint64)  # random() = k * 2^-53 exactly
+        return u
+
+    def choice(self, values, mask, site):
+        v = super().choice(values, mask, site)
+        idx = np.zeros(self.B, np.int32)
+        idx[mask] = np.searchsorted(self.valid, v)
+        self.rec[site] = idx
+        return v
+
+    def record_normal(self, site, mask, v):
+        arr = np.zeros((self.B, 2), np.float64)
+        arr[mask] = v
+        self.rec[site] = arr
+
+
+def make_env(kw, B, **extra):
+    from gym_po_amd import CRoomsEnv
+    kw = dict(kw)
+    if "goal_xy" in kw and kw["goal_xy"] is not None:
+        kw["goal_xy"] = tuple(kw["goal_xy"])
+    return CRoomsEnv(B, **kw, **extra)
+
+
+def make_oracle(kw, B):
+    kw = dict(kw)
+    if "goal_xy" in kw and kw["goal_xy"] is not None:
+        kw["goal_xy"] = tuple(kw["goal_xy"])
+    return CRoomsOracle(B, **kw)
+
+
+def _replay_args(rec, B):
+    z2 = np.zeros((B, 2))
+    return dict(u=rec.get("u", np.zeros(B, np.uint64)), goal_idx=rec.get("goal", np.zeros(B, np.int32)),
+                agent_idx=rec.get("agent", np.zeros(B, np.int32)), noise=rec.get("noise", z2),
+                wall_noise=rec.get("wall_noise", z2))
+
+
+def run_replay(kw, B, seed, acts, dtype):
+    """Oracle on the reference stream and GPU on its replayed values, step by step."""
+    import torch
+    ora = make_oracle(kw, B)
+    env = make_env(kw, B, rng_mode="replay", dtype=dtype)
+    ora.gen = np.random.Generator(np.random.PCG64(np.random.SeedSequence(seed)))
+    rd = RecordingDraws(ora.gen, B, ora.valid)
+    o_ref = ora.reset(rd)
+    env.set_replay(**_replay_args(rd.rec, B))
+    o = env.reset()
+    yield -1, np.asarray(o_ref), (o.cpu().numpy(),), ora, env
+    for t in range(acts.shape[0]):
+        rd = RecordingDraws(ora.gen, B, ora.valid)
+        ro, rr, rdn, rt = ora.step(acts[t], rd)
+        env.set_replay(**_replay_args(rd.rec, B))
+        a = torch.as_tensor(acts[t]).to(dtype) if acts.dtype.kind == "f" else acts[t]
+        o, r, d, tr, _ = env.step(a)
+        yield t, (np.asarray(ro), rr, rdn, rt), (o.cpu().numpy(), r.cpu().numpy(), d.cpu().numpy(),
+                                                 tr.cpu().numpy()), ora, env
+
+
+def _acts(meta):
+    a = step_actions(meta)
+    return a
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_replay_f64_bit_exact_vs_reference_fixture(name, gpu_device):
+    import torch
+    meta, data = load_case(name)
+    acts = _acts(meta)
+    for t, ref, got, ora, env in run_replay(meta["kwargs"], meta["num_envs"], meta["seed"], acts, torch.float64):
+        if t < 0:
+            np.testing.assert_array_equal(got[0].astype(np.float64), data["obs0"].astype(np.float64))
+            continue
+        o, r, d, tr = got
+        np.testing.assert_array_equal(o.astype(np.float64), data["obs"][t].astype(np.float64), err_msg=f"t={t}")
+        np.testing.assert_array_equal(r, data["rew"][t], err_msg=f"t={t}")
+        np.testing.assert_array_equal(d.astype(bool), data["term"][t], err_msg=f"t={t}")
+        np.testing.assert_array_equal(tr.astype(bool), data["trunc"][t], err_msg=f"t={t}")
+        od = o.astype(np.float64) if o.dtype.kind == "f" else o.astype(np.int64)
+        assert digest(od) == data["digests"][t][0], f"obs digest t={t}"
+    a, g, v, e = (x.cpu().numpy() for x in env.get_state())
+    np.testing.assert_array_equal(a, data["final_agent"])
+    np.testing.assert_array_equal(g + 0.5, data["final_goal"])
+    np.testing.assert_array_equal(v, data["final_velocity"])
+    np.testing.assert_array_equal(e, data["final_elapsed"])
+
+
+@pytest.mark.parametrize("kw,B", [({"obs_type": "vector_mdp"}, 100003),
+                                  ({"obs_type": "vector_goal_mdp", "use_velocity": True, "goal_xy": None,
+                                    "time_limit": 60}, 30001),
+                                  ({"obs_type": "hansen8", "action_type": "ordinal", "layout": "16"}, 9999),
+                                  ({"obs_type": "mdp", "action_type": "cardinal", "action_std": 0.0,
+                                    "action_power": 2.0, "time_limit": 40}, 4097),
+                                  ({"obs_type": "goal_room", "layout": "8b", "goal_xy": None}, 2049)])
+def test_replay_f32_io_vs_oracle_ragged(kw, B, gpu_device):
+    """float32 actions in, float32 obs out: state math is float64, obs = f32(reference obs)."""
+    import torch
+    rng = np.random.default_rng(5)
+    yx = kw.get("action_type", "yx") == "yx"
+    if yx:
+        acts = rng.uniform(-1, 1, (120, B, 2)).astype(np.float32).astype(np.float64)
+    else:
+        acts = rng.integers(0, 8 if kw.get("action_type") == "ordinal" else 4, (120, B))
+    eps = 0
+    for t, ref, got, ora, env in run_replay(kw, B, 17, acts, torch.float32):
+        if t < 0:
+            continue
+        o = got[0]
+        if o.dtype.kind == "f":
+            assert o.dtype == np.float32
+            r64 = ref[0].astype(np.float64)
+            np.testing.assert_array_equal(o, ref[0].astype(np.float32), err_msg=f"t={t}")
+            assert np.all(np.abs(o.astype(np.float64) - r64) <= F32_REL_TOL * np.abs(r64))
+        else:
+            np.testing.assert_array_equal(o.astype(np.int64), ref[0].astype(np.int64), err_msg=f"t={t}")
+        for name, a, b in zip(("rew", "term", "trunc"), ref[1:], got[1:]):
+            np.testing.assert_array_equal(np.asarray(a).astype(np.float64), b.astype(np.float64),
+                                          err_msg=f"{name} t={t}")
+        eps += int((ref[2] | ref[3]).sum())
+    m = env.metrics()
+    assert m["episodes"] == eps and m["env_steps"] == 120 * B
+
+
+def test_philox_rollout_equals_single_steps(gpu_device):
+    import torch
+    B, K = 7001, 33
+    kw = {"obs_type": "vector_goal_mdp", "use_velocity": True, "goal_xy": None, "time_limit": 20}
+    a, b = make_env(kw, B), make_env(kw, B)
+    a.reset(seed=3)
+    b.reset(seed=3)
+    acts = torch.rand((K, B, 2), device=gpu_device) * 2 - 1
+    ro, rr, rd, rt = a.rollout(acts)
+    for t in range(K):
+        o, r, d, tr, _ = b.step(acts[t])
+        assert torch.equal(o, ro[t]) and torch.equal(r, rr[t]) and torch.equal(d, rd[t]) and torch.equal(tr, rt[t])
+    for x, y in zip(a.get_state(), b.get_state()):
+        assert torch.equal(x, y)
+
+
+def test_philox_action_noise_law(gpu_device):
+    """Zero actions from cell centres far from walls: the displacement is the action noise N(0, 0.2)."""
+    import torch
+    from scipy.stats import kstest
+    B = 1 << 20
+    env = make_env({"obs_type": "vector_mdp", "layout": "1", "time_limit": 10}, B, dtype=torch.float64)
+    env.reset(seed=8)
+    H, W = env.grid.shape
+    cy, cx = H // 2 + 0.5, W // 2 + 0.5
+    start = np.tile([cy, cx], (B, 1))
+    env.set_state(agent_yx=start, elapsed=np.zeros(B, np.int32))
+    o, r, d, tr, _ = env.step(torch.zeros((B, 2), dtype=torch.float64, device=gpu_device))
+    disp = (env.agent_yx.cpu().numpy() - start).ravel()
+    assert abs(disp.mean()) < 3e-3 and abs(disp.std() - 0.2) < 2e-3
+    assert kstest(disp / 0.2, "norm").pvalue > 1e-4
+
+
+def test_philox_reset_cells_uniform(gpu_device):
+    import torch
+    from scipy.stats import chisquare
+    B = 1 << 20
+    env = make_env({"obs_type": "vector_goal_mdp", "goal_xy": None}, B, dtype=torch.float64)
+    env.reset(seed=1)
+    a, g, _, _ = env.get_state()
+    H, W = env.grid.shape
+    ac = np.floor(a.cpu().numpy()).astype(int)
+    cells = ac[:, 0] * W + ac[:, 1]
+    idx = np.searchsorted(env.valid_states, cells)
+    assert np.array_equal(env.valid_states[idx], cells)
+    counts = np.bincount(idx, minlength=len(env.valid_states))
+    assert chisquare(counts).pvalue > 1e-4
+    gc = g.cpu().numpy()
+    gidx = np.searchsorted(env.valid_states, gc[:, 0] * W + gc[:, 1])
+    assert chisquare(np.bincount(gidx, minlength=len(env.valid_states))).pvalue > 1e-4

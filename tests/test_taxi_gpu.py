@@ -92,15 +92,15 @@ def test_replay_bit_exact_vs_oracle_ragged(kw, B, gpu_device):
     assert m["episodes"] == eps and m["env_steps"] == 250 * B
 
 
-def test_negative_actions_wrap_like_numpy(gpu_device):
+def test_negative_actions_index_like_numpy(gpu_device):
+    """ACTIONS_YX[a] wraps a in -5..-1; -1 moves (0,0) but is not a pickup/dropoff (a == 4 test)."""
     B = 512
     rng = np.random.default_rng(3)
-    acts = rng.integers(0, 5, (40, B))
-    outs = [[], []]
-    for i, a in enumerate((acts, acts - 5)):
-        for t, ref, got, ora, env in run_replay({"hansen_obs": True}, B, 5, a):
-            outs[i].append(got[0])
-    np.testing.assert_array_equal(np.stack(outs[0]), np.stack(outs[1]))
+    acts = rng.integers(-5, 5, (60, B))
+    for t, ref, got, ora, env in run_replay({"hansen_obs": True, "num_passengers": 2}, B, 5, acts):
+        for name, a, b in zip(("obs", "rew", "term", "trunc"), ref, got):
+            np.testing.assert_array_equal(np.asarray(a).astype(np.float64), b.astype(np.float64),
+                                          err_msg=f"{name} t={t}")
 
 
 @pytest.mark.parametrize("kw", [{"hansen_obs": True}, {}, {"map": "EXTENDED", "hansen_obs": True}])
