@@ -46,6 +46,16 @@ def _taxi_onehot(B, dev, mode):
     return HansenTaxiVecEnv(B, device=dev, rng_mode=mode, one_hot=True)
 
 
+def _crooms(B, dev, mode):
+    from gym_po_amd import CRoomsEnv
+    return CRoomsEnv(B, obs_type="vector_mdp", device=dev, rng_mode=mode)
+
+
+def _anttag(B, dev, mode):
+    from gym_po_amd import AntTagGridEnv
+    return AntTagGridEnv(B, device=dev, rng_mode=mode)
+
+
 # The headline (BASELINE.json configs[1]) and the other single-GPU configs, measured the same way.
 # bytes: algorithmic bytes per env-step of a fused rollout launch; state: bytes per env
 # read + written once per launch.
@@ -59,6 +69,15 @@ WORKLOADS = {
                  dtype="uint8", kernel="taxi_rollout<16,false>", chunk=16,
                  desc="configs[2]: PO-Taxi 5x5 (TAXI_MAP) Hansen obs one-hot uint8[B,320], {B} envs per GPU, "
                       "HansenTaxiVecEnv(one_hot=True)"),
+    "crooms": dict(make=_crooms, envs=1 << 21, n_actions=None, mode="philox", bytes=8 + 8 + 4 + 1 + 1, state=40,
+                   metric="env steps/sec, C-ROOMS layout 4 continuous (y,x) + N(0,0.2) action noise, 2M envs per GPU",
+                   dtype="f64 state / f32 I/O", kernel="crooms_rollout<GP_OBS_F32,false>",
+                   desc="configs[4]: C-ROOMS layout 4, yx actions f32 U[-1,1]^2, vector_mdp obs f32[B,2], {B} envs per "
+                        "GPU, CRoomsEnv(obs_type='vector_mdp')"),
+    "anttag": dict(make=_anttag, envs=1 << 21, n_actions=5, mode="philox", bytes=4 + 16 + 4 + 1 + 1, state=8,
+                   metric="env steps/sec, grid Ant-Tag 10x10 (build-defined), 2M envs per GPU (16M on 8 GPUs)",
+                   dtype="int32", kernel="anttag_rollout<false>",
+                   desc="configs[3]: grid Ant-Tag 10x10, {B} envs per GPU (2M x 8 GPUs = 16M), AntTagGridEnv()"),
 }
 
 
@@ -88,6 +107,28 @@ def cpu_baseline(workload="fourrooms", target_s=12.0):
     """The numpy oracle (the reference's algorithm restated, fixture-pinned) on one host core."""
     import numpy as np
     B = 1 << 18
+    if workload == "crooms":
+        from oracle.crooms import CRoomsOracle
+        ora = CRoomsOracle(B, obs_type="vector_mdp")
+        name = "oracle.crooms.CRoomsOracle(vector_mdp, float64)"
+        acts = np.random.default_rng(1).uniform(-1, 1, (8, B, 2))
+        return _time_oracle(ora, acts, name, B, target_s)
+    if workload == "anttag":
+        from oracle.anttag import AntTagOracle
+        from oracle.philox import philox_key
+        ora = AntTagOracle(B)
+        key = philox_key(0)
+        ora.reset(ora.philox_draws(0, key))
+        ctr = [0]
+
+        def step(a):
+            ctr[0] += 1
+            return ora.step(a, ora.philox_draws(ctr[0], key))
+        ora.step_seeded = step
+        ora.reset_seed = lambda seed: None
+        acts = np.random.default_rng(1).integers(0, 5, (8, B))
+        return _time_oracle(ora, acts, "oracle.anttag.AntTagOracle (numpy, philox draws; build-defined spec, "
+                                       "no reference to pin)", B, target_s)
     if workload == "taxi":
         from oracle.taxi import TaxiOracle
         ora = TaxiOracle(B, hansen_obs=True)
@@ -99,8 +140,12 @@ def cpu_baseline(workload="fourrooms", target_s=12.0):
         from oracle.gridworld import FourRoomsOracle
         ora = FourRoomsOracle(B, 1, obs_type="hansen")
         name, na = "oracle.gridworld.FourRoomsOracle", 4
-    ora.reset_seed(0)
     acts = np.random.default_rng(1).integers(0, na, (8, B))
+    return _time_oracle(ora, acts, name, B, target_s)
+
+
+def _time_oracle(ora, acts, name, B, target_s):
+    ora.reset_seed(0)
     ora.step_seeded(acts[0])  # warm
     t0 = time.perf_counter()
     n = 0
@@ -111,7 +156,7 @@ def cpu_baseline(workload="fourrooms", target_s=12.0):
         if dt >= target_s or n >= 400:
             break
     return {"value": B * n / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"{name} (numpy, reference-pinned), 2^18 envs x {n} steps, "
+            "sample": f"{name} (numpy{'' if 'build-defined' in name else ', reference-pinned'}), 2^18 envs x {n} steps, "
                       f"1 process ({dt:.1f} s)"}
 
 
@@ -170,7 +215,10 @@ def main():
     C = max(1, min(args.chunk, args.steps))
     g = torch.Generator(device=dev)
     g.manual_seed(1 + rank)
-    acts = torch.randint(0, W["n_actions"], (C, B), device=dev, dtype=torch.int32, generator=g)
+    if W["n_actions"] is None:  # continuous (y, x) actions, float32 U[-1, 1]^2
+        acts = torch.rand((C, B, 2), device=dev, dtype=torch.float32, generator=g) * 2 - 1
+    else:
+        acts = torch.randint(0, W["n_actions"], (C, B), device=dev, dtype=torch.int32, generator=g)
     out = env._alloc_outputs(C)
 
     def run(n):

@@ -107,7 +107,7 @@ def test_replay_f64_bit_exact_vs_reference_fixture(name, gpu_device):
         np.testing.assert_array_equal(r, data["rew"][t], err_msg=f"t={t}")
         np.testing.assert_array_equal(d.astype(bool), data["term"][t], err_msg=f"t={t}")
         np.testing.assert_array_equal(tr.astype(bool), data["trunc"][t], err_msg=f"t={t}")
-        od = o.astype(np.float64) if o.dtype.kind == "f" else o.astype(np.int64)
+        od = o.astype(np.float64) if data["obs0"].dtype.kind == "f" else o.astype(np.int64)
         assert digest(od) == data["digests"][t][0], f"obs digest t={t}"
     a, g, v, e = (x.cpu().numpy() for x in env.get_state())
     np.testing.assert_array_equal(a, data["final_agent"])
