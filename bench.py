@@ -205,13 +205,11 @@ def main():
     args.envs = args.envs or W["envs"]
     args.mode = args.mode or W["mode"]
     args.chunk = args.chunk or W.get("chunk", 64)
-    B = args.envs // world if args.strong else args.envs
+    from gym_po_amd import shard
+    B = shard.shard_size(args.envs, world, rank, args.strong)
     env = W["make"](B, dev, args.mode)
-    if world == 1:
-        env.reset(seed=0)
-    else:  # shard g: SeedSequence(0, spawn_key=(g,))
-        env.seed(0, spawn_key=(rank,))
-        env.reset()
+    shard.seed_shard(env, 0, rank, world)  # shard g: SeedSequence(0, spawn_key=(g,))
+    env.reset()
     C = max(1, min(args.chunk, args.steps))
     g = torch.Generator(device=dev)
     g.manual_seed(1 + rank)
@@ -245,10 +243,7 @@ def main():
     barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    tmax = float(t.item())
+    tmax = shard.max_over_ranks(elapsed, dev)
 
     # live roofline: HIP events bracketing every step-kernel launch on its stream
     env.set_profiling(True)
@@ -267,13 +262,9 @@ def main():
         bytes_per_launch = B * BYTES_PER_ENV_STEP
     achieved = bytes_per_launch / (kavg_ms * 1e-3) / 1e9
 
-    m = env.metrics()
-    mt = torch.tensor([m["episodes"], m["return_sum"], m["length_sum"], m["env_steps"]], dtype=torch.float64,
-                      device=dev)
-    if world > 1:
-        dist.all_reduce(mt)  # RCCL: the only collective (episode statistics)
+    m = shard.allreduce_metrics(env.metrics(), dev)  # RCCL: the only collective (episode statistics)
 
-    total_steps = B * args.steps * world
+    total_steps = (args.envs if args.strong else B * world) * args.steps
     cfg_key = (f"fourrooms_hansen4_B{B}_{args.mode}" if args.workload == "fourrooms" else
                f"{args.workload}_B{B}_{args.mode}")
     pmc = load_pmc(cfg_key, args.workload)
@@ -294,7 +285,7 @@ def main():
             "reference RNG stream reproduced bit-exactly" if args.mode == "numpy" else
             "counter-based Philox draws from the reference's exact laws"),
         "config": {"workload": W["desc"].format(B=B),
-                   "envs_per_gpu": B, "global_envs": B * world, "rng_mode": args.mode,
+                   "envs_per_gpu": B, "global_envs": args.envs if args.strong else B * world, "rng_mode": args.mode,
                    "parallelism": f"independent env shards x{world}", "steps_per_launch_call": C},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -308,8 +299,8 @@ def main():
                      "resolver_kernel": ("grid_resolve_numpy<GP_OBS_HANSEN>"
                                          if args.mode == "numpy" and args.workload == "fourrooms" else None),
                      "resolver_avg_us": ravg_ms * 1e3 if nr else None},
-        "episodes": {"count": mt[0].item(), "mean_return": mt[1].item() / max(mt[0].item(), 1),
-                     "mean_length": mt[2].item() / max(mt[0].item(), 1)},
+        "episodes": {"count": m["episodes"], "mean_return": m["return_sum"] / max(m["episodes"], 1),
+                     "mean_length": m["length_sum"] / max(m["episodes"], 1)},
         "lib_hash": lib_hash(),
     }
     if rank == 0:
