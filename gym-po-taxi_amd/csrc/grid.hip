@@ -298,6 +298,22 @@ __device__ __forceinline__ void write_obs(const GridDev& p, const TB& tb, int en
   }
 }
 
+// Scalar obs of one env (GP_OBS_HANSEN / GP_OBS_TABLE), as write_obs4 computes it.
+template <int OK, class TB>
+__device__ __forceinline__ int32_t obs_value(const GridDev& p, const TB& tb, int a, int g) {
+  if constexpr (OK == GP_OBS_HANSEN) {
+    int mult = 1;
+    if ((unsigned)g < (unsigned)p.ncells) {
+      int diff = g - a;
+      for (int d = p.obs_dirs - 1; d >= 0; --d)
+        if (diff == tb.doff(d)) mult = d + 1;
+    }
+    return (int32_t)tb.hbase(a) * mult;
+  } else {
+    return tb.t1(a) + (tb.has_t2() ? tb.t2(g) : 0);
+  }
+}
+
 template <int OK, class TB, bool ALIGNED = false>
 __device__ __forceinline__ void write_obs4(const GridDev& p, const TB& tb, int env0, const int (&agent)[4],
                                            const int (&goal)[4], void* __restrict__ obs) {
@@ -829,14 +845,21 @@ __global__ __launch_bounds__(TPB) void grid_reset_init(GridDev p) {
 // block publishes step t+2 only after every block has published step t+1, i.e. finished
 // reading step t's slots), so a stale granule never carries the expected tag.
 constexpr int FENVW = 8;                 // env waves per block (2 per SIMD)
-constexpr int FTPB = (FENVW + 1) * 64;   // + one control wave
-constexpr int FWAVES = FENVW + 1;
+constexpr int FSTW = 2;                  // store waves (LDS-staged outputs -> HBM)
+constexpr int FWAVES = FENVW + 1 + FSTW; // + one control wave + the store waves
+constexpr int FTPB = FWAVES * 64;
 constexpr int FEPB = FENVW * 64 * EPT;   // 2048 envs per fused tile
 constexpr int RCOV = 62;                 // speculative rejection-check words per tile per step (32 u64 lanes)
 constexpr int FMAXG = 256;        // blocks: wave 0 gathers 4 granules per lane
 constexpr int FMAXQ = 4;          // tiles per block (12-bit counts: 4 per granule)
 constexpr int FMAXT = FMAXG * FMAXQ;
 constexpr int LDS_TABLE_BUDGET = 96 * 1024;
+// Output staging (scalar obs kinds, <= 2 tiles per block): per tile obs int32[FEPB], reward f32[FEPB],
+// terminated u8[FEPB], truncated u8[FEPB], in dynamic LDS after the tables.
+constexpr int STG_TILE_BYTES = FEPB * 10;
+constexpr int R_ENV = 0, R_CTRL = 1, R_PASS = 2;  // fused_resets roles: env wave, control wave, store wave
+template <int OK, int QPT>
+constexpr bool fused_staged() { return QPT <= 2 && (OK == GP_OBS_HANSEN || OK == GP_OBS_TABLE); }
 constexpr uint32_t TAG_MASK = 0x7FFFu;
 
 struct FusedShared {
@@ -849,6 +872,8 @@ struct FusedShared {
   uint64_t ns_hi, ns_lo;         // next step's s0
   uint32_t nh, nu;               // next step's has_uint32 / uinteger
   uint32_t drawn;                // the control wave drew this step's resetter cells before B2
+  uint32_t rdone;                // env waves done listing their resetters in renv (monotone)
+  uint16_t renv[2][FEPB];        // STG: env (in tile) of resetter rank r of tile q
   uint32_t pos[FEPB];            // slow path: accepted-word positions of one tile's resetters
   uint32_t pos2[FEPB];
   uint32_t cell[FMAXQ * FEPB];   // resetter cells (goal | agent << 16) by tile and rank
@@ -1098,21 +1123,29 @@ __device__ __forceinline__ void lds_copy(char* dyn, const GridLdsTab& t, const T
 }
 
 // Phase 4 of a fused step (both roles; every barrier here is block-uniform): the resetters'
-// choice() draws. CTRL = the control wave (coverage exchanges, stream walks, J_used of the
-// unusual cases); otherwise an env wave with its env state.
+// choice() draws. ROLE: R_CTRL = the control wave (coverage exchanges, stream walks, J_used of the
+// unusual cases); R_ENV = an env wave with its env state; R_PASS = a store wave (barriers only).
 // Control wave: the cells (goal | agent << 16) of this block's resetters, rank r of tile q ->
 // sh.cell[q*FEPB + r]. Word positions: fast path P_q + r (goal call) and w1 + P_q + r (agent
 // call); slow path (only_q >= 0: one tile) from the stream walk's position lists pg / pa.
 // Control wave, common case (one reset call, no rejected word, b within the speculative window):
 // the next PCG64 state and the block's resetter cells in ONE straight-line block so that their
 // dependent jump chains overlap. tq / pre: lane q < QPT holds tile q's reset count / prefix.
-template <int QPT>
+// STG: the final obs of resetter rank r of tile q (new cells goal | agent << 16) into the staging area.
+template <int OK, bool STG>
+__device__ __forceinline__ void stage_reset_obs(const GridDev& p, const FusedShared& sh, const LTabs& tb, char* stg,
+                                                int q, uint32_t r, uint32_t cell) {
+  if constexpr (STG)
+    reinterpret_cast<int32_t*>(stg + q * STG_TILE_BYTES)[sh.renv[q][r]] =
+        obs_value<OK>(p, tb, (int)(cell >> 16), (int)(cell & 0xFFFFu));
+}
+
+template <int OK, int QPT, bool STG>
 __device__ __forceinline__ void ctrl_fast_finish(const GridDev& p, FusedShared& sh, const LTabs& tb, const u128 SB,
-                                                 const Stream& st, uint32_t b, uint32_t tq, uint32_t pre) {
+                                                 const Stream& st, uint32_t b, uint32_t tq, uint32_t pre, char* stg) {
   const int lane = threadIdx.x & 63;
   const bool rgoal = p.fixed_goal < 0;
-  const uint32_t mode = rgoal ? 1u : 2u;
-  const uint32_t ng = (uint32_t)p.n_goal_valid, na = (uint32_t)p.n_agent_valid;
+  const uint32_t nsel = rgoal ? (uint32_t)p.n_goal_valid : (uint32_t)p.n_agent_valid;
   uint32_t tc[QPT], P[QPT], cum[QPT + 1];
   cum[0] = 0;
 #pragma unroll
@@ -1121,35 +1154,65 @@ __device__ __forceinline__ void ctrl_fast_finish(const GridDev& p, FusedShared& 
     P[q] = (uint32_t)__builtin_amdgcn_readlane((int)pre, q);
     cum[q + 1] = cum[q] + tc[q];
   }
-  // next state: s0' = jump(SB, used), J_used
   uint32_t used, h;
   words_to_draws(b, st.h0, used, h);
-  const PcgJump ju = jparams_small(tb.jt8(), tb.jt(), used);
-  const u128 s = jump_small(tb.jt8(), tb.jt(), SB, used);
-  for (uint32_t idx = lane; idx < max(cum[QPT], 1u); idx += 64) {
-    const uint32_t ii = min(idx, max(cum[QPT], 1u) - 1u);
+  // Every lane evaluates ONE two-level jump X = J2(J1(X0)) from the radix-256 tables (all jumps here
+  // are < 2^16: b <= nt * RCOV). Cell lanes: SB jumped to their choice() word. In the first pass
+  // lanes 61..63 produce the next step's state instead: J_used = J_hi o J_lo as its multiplier
+  // a_hi * a_lo (lane 61) and increment a_hi * c_lo + c_hi (lane 62), and s0' = J_used(SB) (lane 63),
+  // so that the whole wave pays for one jump chain instead of four.
+  constexpr uint32_t XL = 61;
+  const uint32_t ncell = cum[QPT];
+  const uint32_t npass = ncell <= XL ? 1u : 1u + (ncell - XL + 63u) / 64u;
+  const PcgJump* t8 = tb.jt8();
+  for (uint32_t it = 0; it < npass; ++it) {  // wave-uniform
+    const uint32_t idx = it == 0 ? (uint32_t)lane : XL + (it - 1u) * 64u + (uint32_t)lane;
+    const bool extra = it == 0 && (uint32_t)lane >= XL;
+    const bool cellj = !extra && idx < ncell;
     int q = 0;
 #pragma unroll
-    for (int j = 1; j < QPT; ++j) q += ii >= cum[j] ? 1 : 0;
-    const uint32_t r = ii - cum[q];
+    for (int j = 1; j < QPT; ++j) q += idx >= cum[j] ? 1 : 0;
+    const uint32_t r = idx - cum[q];
     const uint32_t w = P[q] + r;
-    const uint32_t v = draw_cells(tb.jt8(), tb.jt(), SB, st.h0, st.u0, w, w, mode, ng, na);
-    const uint32_t goal = rgoal ? (uint32_t)tb.gv((int)(v & 0xFFFFu)) : (uint32_t)p.fixed_goal;
-    const uint32_t agent = rgoal ? (uint32_t)p.fixed_agent : (uint32_t)tb.av((int)(v >> 16));
-    if (idx < cum[QPT]) sh.cell[q * FEPB + r] = goal | (agent << 16);
-  }
-  if (lane == 0) {
-    sh.ju[0] = ju.a_hi; sh.ju[1] = ju.a_lo; sh.ju[2] = ju.c_hi; sh.ju[3] = ju.c_lo;
-    sh.ns_hi = hi64(s); sh.ns_lo = lo64(s);
-    sh.nh = h;
-    sh.nu = used ? (uint32_t)(pcg_output(s) >> 32) : st.u0;
+    const bool buffered = st.h0 && w == 0;  // numpy's buffered half-word
+    const uint32_t ww = w - st.h0;
+    const uint32_t n = extra ? used : (cellj && !buffered ? (ww >> 1) + 1u : 0u);
+    const PcgJump jlo = t8[n & 255u], jhi = t8[256u + ((n >> 8) & 255u)];
+    PcgJump J1 = jlo, J2 = jhi;
+    u128 X0 = SB;
+    if (extra && lane == 61) {
+      J1 = PcgJump{0, 1, 0, 0};
+      J2.c_hi = 0; J2.c_lo = 0;
+      X0 = mk128(jlo.a_hi, jlo.a_lo);
+    } else if (extra && lane == 62) {
+      J1 = PcgJump{0, 1, 0, 0};
+      X0 = mk128(jlo.c_hi, jlo.c_lo);
+    }
+    const u128 X = apply_jump(J2, apply_jump(J1, X0));
+    const uint64_t x = pcg_output(X);
+    if (cellj) {
+      const uint32_t word = buffered ? st.u0 : ((ww & 1u) ? (uint32_t)(x >> 32) : (uint32_t)x);
+      const uint32_t v = lemire_value(word, nsel);
+      const uint32_t goal = rgoal ? (uint32_t)tb.gv((int)v) : (uint32_t)p.fixed_goal;
+      const uint32_t agent = rgoal ? (uint32_t)p.fixed_agent : (uint32_t)tb.av((int)v);
+      sh.cell[q * FEPB + r] = goal | (agent << 16);
+      stage_reset_obs<OK, STG>(p, sh, tb, stg, q, r, goal | (agent << 16));
+    } else if (extra) {
+      if (lane == 61) { sh.ju[0] = hi64(X); sh.ju[1] = lo64(X); }
+      if (lane == 62) { sh.ju[2] = hi64(X); sh.ju[3] = lo64(X); }
+      if (lane == 63) {
+        sh.ns_hi = hi64(X); sh.ns_lo = lo64(X);
+        sh.nh = h;
+        sh.nu = used ? (uint32_t)(x >> 32) : st.u0;
+      }
+    }
   }
 }
 
-template <int QPT>
+template <int OK, int QPT, bool STG>
 __device__ __forceinline__ void ctrl_draw_cells(const GridDev& p, FusedShared& sh, const LTabs& tb, const u128 SB,
                                                 const Stream& st, uint32_t w1, const uint32_t* pg, const uint32_t* pa,
-                                                int only_q) {
+                                                int only_q, char* stg) {
   const int lane = threadIdx.x & 63;
   const bool rgoal = p.fixed_goal < 0, ragent = p.fixed_agent < 0;
   const uint32_t mode = (rgoal ? 1u : 0u) | (ragent ? 2u : 0u);
@@ -1182,16 +1245,17 @@ __device__ __forceinline__ void ctrl_draw_cells(const GridDev& p, FusedShared& s
     const uint32_t goal = rgoal ? (uint32_t)tb.gv((int)(v & 0xFFFFu)) : (uint32_t)p.fixed_goal;
     const uint32_t agent = ragent ? (uint32_t)tb.av((int)(v >> 16)) : (uint32_t)p.fixed_agent;
     sh.cell[q * FEPB + r] = goal | (agent << 16);
+    stage_reset_obs<OK, STG>(p, sh, tb, stg, q, r, goal | (agent << 16));
   }
 }
 
 
-template <int OK, int QPT, bool CTRL>
+template <int OK, int QPT, int ROLE, bool STG = false>
 __device__ __forceinline__ void fused_resets(const GridDev& p, FusedShared& sh, const LTabs& tb, const Stream& st,
                                              const u128 SB, const PcgJump& jB, uint64_t* slots, uint32_t tag0,
                                              uint32_t (&ae)[QPT][4], int (&gl)[QPT][4], const uint32_t (&fm)[QPT],
                                              const uint32_t (&excl)[QPT], uint32_t (&pc)[QPT][4],
-                                             uint32_t (&pfm)[QPT]) {
+                                             uint32_t (&pfm)[QPT], char* stg = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int G = (int)gridDim.x, nt = p.fnt;
   const bool rgoal = p.fixed_goal < 0, ragent = p.fixed_agent < 0;
@@ -1202,24 +1266,30 @@ __device__ __forceinline__ void fused_resets(const GridDev& p, FusedShared& sh, 
   if (!(ncalls && b)) return;
   // env waves: take the resetters' cells the control wave drew for tile q
   auto consume = [&](int q) {
-    if constexpr (!CTRL) {
+    if constexpr (ROLE == R_ENV) {
       // the resetters' new cells (independent LDS loads); their obs are written in the next step's
       // output phase, off the critical path (pc / pfm)
+      // (STG: the control wave wrote their final obs into the LDS staging area when it drew them)
       uint32_t r = excl[q];
+      uint32_t c[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const uint32_t bit = (fm[q] >> i) & 1u;
-        pc[q][i] = sh.cell[q * FEPB + min(r, (uint32_t)FEPB - 1u)];
+        c[i] = sh.cell[q * FEPB + min(r, (uint32_t)FEPB - 1u)];
         r += bit;
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         if ((fm[q] >> i) & 1u) {
-          gl[q][i] = (int)(pc[q][i] & 0xFFFFu);
-          ae[q][i] = pc[q][i] >> 16;
+          gl[q][i] = (int)(c[i] & 0xFFFFu);
+          ae[q][i] = c[i] >> 16;
         }
       }
-      pfm[q] = fm[q];
+      if constexpr (!STG) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pc[q][i] = c[i];
+        pfm[q] = fm[q];
+      }
     }
   };
   if (sh.drawn) {  // common case: drawn before B2
@@ -1236,7 +1306,7 @@ __device__ __forceinline__ void fused_resets(const GridDev& p, FusedShared& sh, 
                           p.thr_agent, sh);
   uint32_t w1 = b;
   if (slow && ncalls == 2) {
-    if constexpr (CTRL) {
+    if constexpr (ROLE == R_CTRL) {
       const uint32_t a = scan_accepted(p.self, st, 0, n1, thr1, b - 1, b, nullptr);
       if (lane == 0) sh.w1 = a;
     }
@@ -1244,7 +1314,7 @@ __device__ __forceinline__ void fused_resets(const GridDev& p, FusedShared& sh, 
     w1 = sh.w1;
   }
   if (!slow) {
-    if constexpr (CTRL) ctrl_draw_cells<QPT>(p, sh, tb, SB, st, w1, nullptr, nullptr, -1);
+    if constexpr (ROLE == R_CTRL) ctrl_draw_cells<OK, QPT, STG>(p, sh, tb, SB, st, w1, nullptr, nullptr, -1, stg);
     lds_barrier();
 #pragma unroll
     for (int q = 0; q < QPT; ++q) consume(q);
@@ -1254,7 +1324,7 @@ __device__ __forceinline__ void fused_resets(const GridDev& p, FusedShared& sh, 
     for (int q = 0; q < QPT; ++q) {
       const int tau = q * G + (int)blockIdx.x;
       if (tau >= nt) continue;  // block-uniform
-      if constexpr (CTRL) {
+      if constexpr (ROLE == R_CTRL) {
         const uint32_t P = sh.tpre[q];
         uint32_t tc = 0;
 #pragma unroll
@@ -1265,14 +1335,14 @@ __device__ __forceinline__ void fused_resets(const GridDev& p, FusedShared& sh, 
             scan_accepted(p.self, st, rgoal ? w1 : 0, (uint32_t)p.n_agent_valid, p.thr_agent, P, P + tc,
                           rgoal ? sh.pos2 : sh.pos);
         }
-        ctrl_draw_cells<QPT>(p, sh, tb, SB, st, w1, sh.pos, rgoal ? sh.pos2 : sh.pos, q);
+        ctrl_draw_cells<OK, QPT, STG>(p, sh, tb, SB, st, w1, sh.pos, rgoal ? sh.pos2 : sh.pos, q, stg);
       }
       lds_barrier();
       consume(q);
     }
   }
   if (!sh.known) {  // block-uniform: the slow / multi-call / extended cases
-    if constexpr (CTRL) {
+    if constexpr (ROLE == R_CTRL) {
       uint32_t wtot;
       if (!slow) {
         wtot = (uint32_t)ncalls * b;
@@ -1319,9 +1389,9 @@ __device__ __forceinline__ void flush_reset_obs(const GridDev& p, const LTabs& t
 }
 
 // The env waves of the fused kernel.
-template <int OK, int QPT, int NA>
+template <int OK, int QPT, int NA, bool STG>
 __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, const uint64_t* s_thr,
-                                          const LTabs& tb, int K, const int32_t* __restrict__ act,
+                                          const LTabs& tb, char* stg, int K, const int32_t* __restrict__ act,
                                           void* __restrict__ obs, float* __restrict__ rew,
                                           uint8_t* __restrict__ term, uint8_t* __restrict__ trunc, float& rsum,
                                           uint32_t& eps, uint32_t& lens, uint32_t& nst) {
@@ -1378,12 +1448,11 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
         load4f<int32_t>(act + (size_t)(k + 1) * B, (q * G + (int)blockIdx.x) * FEPB + tid * EPT, B, a_nxt[q]);
     }
     // ---- 1. draws + transitions (the critical path) ----
-    float r[QPT][4];
-    uint32_t fm[QPT], tmm[QPT], trm[QPT], excl[QPT], wex[QPT], wt[QPT];
+    uint32_t fm[QPT], tmm[QPT], trm[QPT], bkm[QPT], excl[QPT], wex[QPT], wt[QPT];
 #pragma unroll
     for (int q = 0; q < QPT; ++q) {
       const int env0 = (q * G + (int)blockIdx.x) * FEPB + tid * EPT;
-      fm[q] = tmm[q] = trm[q] = 0;
+      fm[q] = tmm[q] = trm[q] = bkm[q] = 0;
       u128 s = S[q];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -1404,8 +1473,8 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
         const bool valid = env0 + i < B;
         const bool f = valid && (tm_ || tr_);
         const float rw = tm_ ? r_goal : (blocked ? r_wall : r_step);
-        r[q][i] = rw;
         tmm[q] |= (uint32_t)tm_ << i;
+        bkm[q] |= (uint32_t)blocked << i;
         trm[q] |= (uint32_t)tr_ << i;
         fm[q] |= (uint32_t)f << i;
         const int ag = f && fixed_agent >= 0 ? fixed_agent : na_;
@@ -1433,28 +1502,89 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
       for (int w = 0; w < FENVW; ++w) woff += w < wid ? sh.wcnt[q][w] : 0u;
       excl[q] = wex[q] + woff;
     }
-    // ---- 3. this step's outputs (overlap the exchange) ----
-    const size_t off = (size_t)k * B;
-    void* ob = (uint8_t*)obs + off * ow;
+    if constexpr (STG) {
+      // list this wave's resetters (rank -> env in tile) for the control wave, which writes their
+      // final obs into the staging area once it has drawn their cells
 #pragma unroll
-    for (int q = 0; q < QPT; ++q) {
-      const int env0 = (q * G + (int)blockIdx.x) * FEPB + tid * EPT;
-      uint8_t tm[4], tr[4];
-      int ag[4];
+      for (int q = 0; q < QPT; ++q) {
+        uint32_t r = excl[q];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        tm[i] = (uint8_t)((tmm[q] >> i) & 1u);
-        tr[i] = (uint8_t)((trm[q] >> i) & 1u);
-        ag[i] = (int)(ae[q][i] & 0xFFFFu);
+        for (int i = 0; i < 4; ++i)
+          if ((fm[q] >> i) & 1u) {
+            sh.renv[q][min(r, (uint32_t)FEPB - 1u)] = (uint16_t)(tid * EPT + i);
+            ++r;
+          }
       }
-      store4f<float>(rew + off, env0, B, r[q]);
-      store4f<uint8_t>(term + off, env0, B, tm);
-      store4f<uint8_t>(trunc + off, env0, B, tr);
-      // one vector store for all 4 envs (uniform store count per step: no vmcnt(0) at merges);
-      // a resetter's obs is provisional here and rewritten in phase 4
-      write_obs4<OK, LTabs, true>(p, tb, env0, ag, gl[q], ob);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+      if (lane == 0) __hip_atomic_fetch_add(&sh.rdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    if (k > 0) flush_reset_obs<OK, QPT>(p, tb, (uint8_t*)obs + (off - B) * ow, tid, pc, pfm);
+    // ---- 3. this step's outputs (overlap the exchange) ----
+    size_t off = (size_t)k * B;
+#ifdef GP_STAMPS
+    if (p.xmode & 8) off = 0;  // diagnostic: every step writes the first step's slice
+#endif
+    void* ob = (uint8_t*)obs + off * ow;
+    if constexpr (STG) {
+      // into the LDS staging area; the store waves move it to HBM during the next VALU phases, so
+      // no global store competes with the exchange (resetters' obs: written by the control wave)
+#pragma unroll
+      for (int q = 0; q < QPT; ++q) {
+        char* t = stg + q * STG_TILE_BYTES;
+        int4 ov;
+        ov.x = obs_value<OK>(p, tb, (int)(ae[q][0] & 0xFFFFu), gl[q][0]);
+        ov.y = obs_value<OK>(p, tb, (int)(ae[q][1] & 0xFFFFu), gl[q][1]);
+        ov.z = obs_value<OK>(p, tb, (int)(ae[q][2] & 0xFFFFu), gl[q][2]);
+        ov.w = obs_value<OK>(p, tb, (int)(ae[q][3] & 0xFFFFu), gl[q][3]);
+        const uint32_t drawm = ncalls ? fm[q] : 0u;  // resetters whose cells the control wave draws
+        if (!drawm) {
+          reinterpret_cast<int4*>(t)[tid] = ov;
+        } else {
+          int32_t* o = reinterpret_cast<int32_t*>(t) + tid * EPT;
+          if (!(drawm & 1u)) o[0] = ov.x;
+          if (!(drawm & 2u)) o[1] = ov.y;
+          if (!(drawm & 4u)) o[2] = ov.z;
+          if (!(drawm & 8u)) o[3] = ov.w;
+        }
+        float rw[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          rw[i] = ((tmm[q] >> i) & 1u) ? r_goal : (((bkm[q] >> i) & 1u) ? r_wall : r_step);
+        reinterpret_cast<float4*>(t + FEPB * 4)[tid] = make_float4(rw[0], rw[1], rw[2], rw[3]);
+        uint32_t tmw = 0, trw = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          tmw |= ((tmm[q] >> i) & 1u) << (8 * i);
+          trw |= ((trm[q] >> i) & 1u) << (8 * i);
+        }
+        reinterpret_cast<uint32_t*>(t + FEPB * 8)[tid] = tmw;
+        reinterpret_cast<uint32_t*>(t + FEPB * 9)[tid] = trw;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < QPT; ++q) {
+#ifdef GP_STAMPS
+        if (p.xmode & 4) break;  // diagnostic: no output stores
+#endif
+        const int env0 = (q * G + (int)blockIdx.x) * FEPB + tid * EPT;
+        uint8_t tm[4], tr[4];
+        int ag[4];
+        float rw[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          tm[i] = (uint8_t)((tmm[q] >> i) & 1u);
+          tr[i] = (uint8_t)((trm[q] >> i) & 1u);
+          ag[i] = (int)(ae[q][i] & 0xFFFFu);
+          rw[i] = tm[i] ? r_goal : (((bkm[q] >> i) & 1u) ? r_wall : r_step);
+        }
+        store4f<float>(rew + off, env0, B, rw);
+        store4f<uint8_t>(term + off, env0, B, tm);
+        store4f<uint8_t>(trunc + off, env0, B, tr);
+        // one vector store for all 4 envs (uniform store count per step: no vmcnt(0) at merges);
+        // a resetter's obs is provisional here and rewritten in phase 4
+        write_obs4<OK, LTabs, true>(p, tb, env0, ag, gl[q], ob);
+      }
+    }
+    if (!STG && k > 0) flush_reset_obs<OK, QPT>(p, tb, (uint8_t*)obs + (off ? off - B : 0) * ow, tid, pc, pfm);
     {
       const PcgJump jB{sh.jB[0], sh.jB[1], sh.jB[2], sh.jB[3]};
 #pragma unroll
@@ -1463,7 +1593,7 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
     lds_barrier();  // B2: the exchange result is in LDS
     STAMP(4);
     // ---- 4. the resetters' draws ----
-    fused_resets<OK, QPT, false>(p, sh, tb, st, st.s0, jB_unused, slots, tag0, ae, gl, fm, excl, pc, pfm);
+    fused_resets<OK, QPT, R_ENV, STG>(p, sh, tb, st, st.s0, jB_unused, slots, tag0, ae, gl, fm, excl, pc, pfm, stg);
     STAMP(3);
     // ---- 5. advance: lane states jump by J_used (J_B was applied while waiting for the exchange) ----
     {
@@ -1482,7 +1612,7 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
     }
     STAMP(5);
   }
-  if (K > 0) flush_reset_obs<OK, QPT>(p, tb, (uint8_t*)obs + (size_t)(K - 1) * B * ow, tid, pc, pfm);
+  if (!STG && K > 0) flush_reset_obs<OK, QPT>(p, tb, (uint8_t*)obs + (size_t)(K - 1) * B * ow, tid, pc, pfm);
 #pragma unroll
   for (int q = 0; q < QPT; ++q) {
     const int env0 = (q * G + (int)blockIdx.x) * FEPB + tid * EPT;
@@ -1498,8 +1628,8 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
 
 // The control wave of the fused kernel: speculative rejection checks, the granule exchange, the
 // next PCG64 state; publishes the RNG state at the end (block 0).
-template <int OK, int QPT>
-__device__ __forceinline__ void fused_ctrl(const GridDev& p_in, FusedShared& sh, const LTabs& tb, int K) {
+template <int OK, int QPT, bool STG>
+__device__ __forceinline__ void fused_ctrl(const GridDev& p_in, FusedShared& sh, const LTabs& tb, char* stg, int K) {
   constexpr int NC = (QPT + 1) / 2;  // checker states per lane (32 lanes per tile)
   const GridDev& p = p_in;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1581,7 +1711,7 @@ __device__ __forceinline__ void fused_ctrl(const GridDev& p_in, FusedShared& sh,
     // {rejection, b, tile prefix}; every other block polls only its own QPT words ----
     uint64_t* tw = p.fslot + (size_t)6 * G + (size_t)((step_base + (uint32_t)k) & 1u) * nt;
     uint32_t b, anyr, mypre = 0;  // lane q < QPT: global prefix of tile q
-    if (blockIdx.x == 0 || p.xmode == 1) {
+    if (blockIdx.x == 0 || (p.xmode & 3) == 1) {
       uint64_t g[4];
       gather_blocks(p, slots, G, tag0, g);
       if (lane == 0) RSTAMP(10);
@@ -1606,7 +1736,7 @@ __device__ __forceinline__ void fused_ctrl(const GridDev& p_in, FusedShared& sh,
         acc += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
       }
       b = acc;
-      if (p.xmode == 0) {
+      if ((p.xmode & 3) == 0) {
 #pragma unroll
         for (int q = 0; q < QPT; ++q)
 #pragma unroll
@@ -1652,8 +1782,14 @@ __device__ __forceinline__ void fused_ctrl(const GridDev& p_in, FusedShared& sh,
     const bool drawn = known && ncalls == 1 && b > 0;
     if (lane < QPT) sh.tpre[lane] = mypre;
     wave_lds_sync();
+    if (STG && ncalls) {  // the env waves' resetter lists (written right after B1: normally long done)
+      const uint32_t want = (uint32_t)FENVW * (uint32_t)(k + 1);
+      while (__hip_atomic_load(&sh.rdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want)
+        __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    }
     if (drawn) {
-      ctrl_fast_finish<QPT>(p, sh, tb, SB, st, b, tq, mypre);  // cells + next state, before B2
+      ctrl_fast_finish<OK, QPT, STG>(p, sh, tb, SB, st, b, tq, mypre, stg);  // cells + next state, before B2
     } else if (known) {
       publish_next(tb, sh, SB, ncalls ? b : 0u, st.h0, st.u0, lane == 0);
     }
@@ -1667,8 +1803,8 @@ __device__ __forceinline__ void fused_ctrl(const GridDev& p_in, FusedShared& sh,
     }
     lds_barrier();  // B2
     // ---- 4. coverage exchanges / stream walks of the unusual cases ----
-    fused_resets<OK, QPT, true>(p, sh, tb, st, SB, jB, slots, tag0, dummy_u, dummy_i, dummy_c, dummy_c, dummy_u,
-                                dummy_p);
+    fused_resets<OK, QPT, R_CTRL, STG>(p, sh, tb, st, SB, jB, slots, tag0, dummy_u, dummy_i, dummy_c, dummy_c, dummy_u,
+                                dummy_p, stg);
     // ---- 5. advance ----
     {
       const PcgJump jt{sh.ju[0], sh.ju[1], sh.ju[2], sh.ju[3]};
@@ -1689,7 +1825,101 @@ __device__ __forceinline__ void fused_ctrl(const GridDev& p_in, FusedShared& sh,
   }
 }
 
-template <int OK, int QPT, int NA>
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// Copy one staged output plane of tile tau (n32 = 32-bit words per env) to HBM: 16-B chunks of
+// 4 (n32 = 1) or 16 (n32 = 0: byte planes) envs when the destination is 16-B aligned, else 4-B words.
+__device__ __forceinline__ void stage_plane(const char* src, char* dst, int env_base, int B, int esz, int sl,
+                                            bool nt) {
+  constexpr int NL = FSTW * 64;
+  if (env_base + FEPB <= B && (((uintptr_t)dst + (size_t)env_base * esz) & 15) == 0) {
+    // whole aligned tile (the common case): straight-line 16-B copies, immediate offsets
+    const u32x4* s4 = reinterpret_cast<const u32x4*>(src) + sl;
+    u32x4* d4 = reinterpret_cast<u32x4*>(dst + (size_t)env_base * esz) + sl;
+    if (esz == 4) {
+#pragma unroll
+      for (int j = 0; j < FEPB / 4 / NL; ++j) {
+        if (nt) __builtin_nontemporal_store(s4[j * NL], d4 + j * NL);
+        else d4[j * NL] = s4[j * NL];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < FEPB / 16 / NL; ++j) {
+        if (nt) __builtin_nontemporal_store(s4[j * NL], d4 + j * NL);
+        else d4[j * NL] = s4[j * NL];
+      }
+    }
+    return;
+  }
+  const bool a16 = (((uintptr_t)dst + (size_t)env_base * esz) & 15) == 0;  // wave-uniform
+  const int epc = a16 ? 16 / esz : 4 / esz;                                   // envs per chunk
+  for (int c = sl; c < FEPB / epc; c += NL) {
+    const int e = env_base + c * epc;
+    if (e + epc <= B) {
+      if (a16 && nt)
+        __builtin_nontemporal_store(reinterpret_cast<const u32x4*>(src)[c], reinterpret_cast<u32x4*>(dst + (size_t)e * esz));
+      else if (a16)
+        *reinterpret_cast<uint4*>(dst + (size_t)e * esz) = reinterpret_cast<const uint4*>(src)[c];
+      else
+        *reinterpret_cast<uint32_t*>(dst + (size_t)e * esz) = reinterpret_cast<const uint32_t*>(src)[c];
+    } else {
+      for (int i = 0; i < epc && e + i < B; ++i)
+        for (int j = 0; j < esz; ++j) dst[(size_t)(e + i) * esz + j] = src[(size_t)(c * epc + i) * esz + j];
+    }
+  }
+}
+
+// The store waves of the fused kernel. They take part in every block barrier (fused_resets role
+// R_PASS) and, with STG, move step k's staged outputs from LDS to HBM right after step k's resets,
+// i.e. while the env waves advance and run step k+1's VALU-bound transitions, so that the outputs'
+// HBM write burst does not overlap the next exchange (whose polling loads it would slow down).
+template <int OK, int QPT, bool STG>
+__device__ __forceinline__ void fused_store(const GridDev& p, FusedShared& sh, const LTabs& tb, const char* stg, int K,
+                                            void* __restrict__ obs, float* __restrict__ rew,
+                                            uint8_t* __restrict__ term, uint8_t* __restrict__ trunc) {
+  const int sl = (int)threadIdx.x - (FENVW + 1) * 64;
+  const int G = (int)gridDim.x, B = p.B;
+  const bool nt = (p.xmode & 16) == 0;  // non-temporal output stores (xmode bit 4 = tuning knob: plain)
+  const uint32_t step_base = p.ctl->step;
+  const Stream st{};
+  const PcgJump jB{0, 1, 0, 0};
+  uint32_t du[QPT][4], dp[QPT] = {};
+  int di[QPT][4];
+  int32_t dov[QPT][4];
+  const uint32_t dc[QPT] = {};
+  (void)dov;
+  for (int k = 0; k < K; ++k) {
+    const uint32_t tag0 = (step_base + (uint32_t)k + 1u) * 4u;
+    uint64_t* slots = p.fslot + (size_t)((step_base + (uint32_t)k) & 1u) * 3 * G;
+    lds_barrier();  // B1
+    lds_barrier();  // B2
+    fused_resets<OK, QPT, R_PASS>(p, sh, tb, st, (u128)0, jB, slots, tag0, du, di, dc, dc, du, dp);
+    if constexpr (STG) {
+      size_t off = (size_t)k * B;
+#ifdef GP_STAMPS
+      if (p.xmode & 8) off = 0;  // diagnostic: every step writes the first step's slice
+      if (p.xmode & 4) continue;  // diagnostic: no output stores
+#endif
+#pragma unroll
+      for (int q = 0; q < QPT; ++q) {
+        const int tau = q * G + (int)blockIdx.x;
+        if (tau >= p.fnt) continue;
+        const char* t = stg + q * STG_TILE_BYTES;
+        stage_plane(t + FEPB * 4, (char*)(rew + off), tau * FEPB, B, 4, sl, nt);
+        stage_plane(t + FEPB * 8, (char*)(term + off), tau * FEPB, B, 1, sl, nt);
+        stage_plane(t + FEPB * 9, (char*)(trunc + off), tau * FEPB, B, 1, sl, nt);
+      }
+      // the obs: the resetters' final obs were written by the control wave before the last barrier
+#pragma unroll
+      for (int q = 0; q < QPT; ++q) {
+        const int tau = q * G + (int)blockIdx.x;
+        if (tau >= p.fnt) continue;
+        stage_plane(stg + q * STG_TILE_BYTES, (char*)obs + off * 4, tau * FEPB, B, 4, sl, nt);
+      }
+    }
+  }
+}
+
+template <int OK, int QPT, int NA, bool STG>
 __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, const int32_t* __restrict__ act,
                                                            void* __restrict__ obs, float* __restrict__ rew,
                                                            uint8_t* __restrict__ term, uint8_t* __restrict__ trunc) {
@@ -1713,15 +1943,20 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
   lds_copy(dyn, p.lds.jt, p.jt);
   lds_copy(dyn, p.lds.jt8, p.jt8);
   if (tid < 4) sh.jB[tid] = (&p.fjB->a_hi)[tid];
+  if (tid == 0) sh.rdone = 0;
   const LTabs tb{p_in, dyn};
+  char* stg = dyn + p.lds.total;  // output staging (STG): after the tables, 16-B aligned
   __syncthreads();
   float rsum = 0.f;
   uint32_t eps = 0, lens = 0, nst = 0;
   if (wid == FENVW) {
     __builtin_amdgcn_s_setprio(3);  // the exchange is on every step's critical path
-    fused_ctrl<OK, QPT>(p, sh, tb, K);
+    fused_ctrl<OK, QPT, STG>(p, sh, tb, stg, K);
+  } else if (wid > FENVW) {
+    __builtin_amdgcn_s_setprio(0);
+    fused_store<OK, QPT, STG>(p, sh, tb, stg, K, obs, rew, term, trunc);
   } else {
-    fused_env<OK, QPT, NA>(p, sh, s_thr, tb, K, act, obs, rew, term, trunc, rsum, eps, lens, nst);
+    fused_env<OK, QPT, NA, STG>(p, sh, s_thr, tb, stg, K, act, obs, rew, term, trunc, rsum, eps, lens, nst);
   }
   // metrics (the control wave contributes zeros)
 #pragma unroll
@@ -1896,6 +2131,7 @@ struct GridBackend : EnvBackend {
   DevBuf b_move, b_thr, b_gv, b_av, b_hbase, b_doff, b_hvec, b_t1, b_t2, b_coords, b_window, b_jt, b_lt4, b_lt2,
       b_tja, b_tjw, b_ae, b_goal, b_ctl, b_tcount, b_tlist, b_rflag, b_mslot, b_ftj, b_flt4, b_fjB, b_fslot, b_dbg, b_self, b_jt8;
   int fused_G = 0, fused_qpt = 0;  // fused numpy rollout geometry (0 = not eligible)
+  bool fused_stg = false;          // outputs staged in LDS and written by the store waves
   // replay pointers for the next step
   const uint64_t* rp_u = nullptr;
   const int32_t* rp_goal = nullptr;
@@ -1957,14 +2193,22 @@ struct GridBackend : EnvBackend {
     return n;
   }
 #endif
-  template <int OK, int QPT>
-  void launch_fused_q(int K, const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc, hipStream_t s) {
+  template <int OK, int QPT, bool STG>
+  void launch_fused_qs(int K, const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc, hipStream_t s) {
+    const size_t lds = (size_t)d.lds.total + (STG ? (size_t)QPT * STG_TILE_BYTES : 0);
     if (d.nact == 4)
-      hipLaunchKernelGGL((grid_rollout_numpy<OK, QPT, 4>), dim3(fused_G), dim3(FTPB), d.lds.total, s, d, K,
+      hipLaunchKernelGGL((grid_rollout_numpy<OK, QPT, 4, STG>), dim3(fused_G), dim3(FTPB), lds, s, d, K,
                          (const int32_t*)act, obs, rew, term, trunc);
     else
-      hipLaunchKernelGGL((grid_rollout_numpy<OK, QPT, 8>), dim3(fused_G), dim3(FTPB), d.lds.total, s, d, K,
+      hipLaunchKernelGGL((grid_rollout_numpy<OK, QPT, 8, STG>), dim3(fused_G), dim3(FTPB), lds, s, d, K,
                          (const int32_t*)act, obs, rew, term, trunc);
+  }
+  template <int OK, int QPT>
+  void launch_fused_q(int K, const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc, hipStream_t s) {
+    if constexpr (fused_staged<OK, QPT>()) {
+      if (fused_stg) return launch_fused_qs<OK, QPT, true>(K, act, obs, rew, term, trunc, s);
+    }
+    launch_fused_qs<OK, QPT, false>(K, act, obs, rew, term, trunc, s);
   }
   // the fused kernel's vector I/O assumes 16-B aligned bases (torch allocations are); K-step launches
   // also need B % 4 == 0 so that every step's slice stays aligned
@@ -2441,20 +2685,30 @@ int GridBackend::build(const gp_grid_config* cfg) {
   d.fnt = (int)((B + FEPB - 1) / FEPB);
   {
     const char* xm = getenv("GP_XMODE");  // exchange variant (tuning knob)
-    d.xmode = xm ? atoi(xm) : 0;
+    // bits 0-1: 1 = every block all-gathers the granules (default), 0 = block-0 aggregator; bit 4: plain
+    // (not non-temporal) staged output stores; bits 2-3 (stamps builds only): output-store diagnostics
+    d.xmode = xm ? atoi(xm) : 1;
   }
   {
     hipDeviceProp_t prop;
     GP_HIP_CHECK(hipGetDeviceProperties(&prop, device));
     int occ = 0;
-    GP_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, grid_rollout_numpy<GP_OBS_WINDOW, 4, 8>, FTPB,
-                                                             d.lds.total));
+    GP_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, grid_rollout_numpy<GP_OBS_WINDOW, 4, 8, false>,
+                                                             FTPB, d.lds.total));
     const int G = std::min({prop.multiProcessorCount, FMAXG, d.fnt});
     const int qpt = (d.fnt + G - 1) / G;
     const char* off = getenv("GP_DISABLE_FUSED");  // testing knob: force the two-kernel numpy path
     if (occ >= 1 && d.fnt <= FMAXT && qpt <= 4 && d.lds.total > 0 && !(off && off[0] == '1')) {
       fused_G = G;
       fused_qpt = qpt <= 1 ? 1 : (qpt <= 2 ? 2 : 4);
+      const int k = cfg->obs_kind;
+      const char* ns = getenv("GP_NO_STAGING");  // tuning knob: direct output stores from the env waves
+      if (fused_qpt <= 2 && (k == GP_OBS_HANSEN || k == GP_OBS_TABLE) && !(ns && ns[0] == '1')) {
+        int occ2 = 0;
+        GP_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &occ2, grid_rollout_numpy<GP_OBS_HANSEN, 2, 8, true>, FTPB, d.lds.total + 2 * STG_TILE_BYTES));
+        fused_stg = occ2 >= 1;
+      }
     }
   }
   nslots = std::max({d.nblk, grid_persist, fused_G});

@@ -11,12 +11,12 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ok, qpt = (sys.argv[1] if len(sys.argv) > 1 else "0"), (sys.argv[2] if len(sys.argv) > 2 else "2")
 out = "/tmp/grid_stamps.s"
-subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-std=c++17", "-O3", "-DGP_STAMPS", "-I",
+if not os.environ.get("ISA_REUSE"): subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-std=c++17", "-O3", "-DGP_STAMPS", "-I",
                 os.path.join(ROOT, "include"), "--cuda-device-only", "-S",
                 os.path.join(ROOT, "gym-po-taxi_amd", "csrc", "grid.hip"), "-o", out], check=True,
                stderr=subprocess.DEVNULL)
 s = open(out).read()
-name = f"_ZN12_GLOBAL__N_118grid_rollout_numpyILi{ok}ELi{qpt}EEEvNS_7GridDevEiPKiPvPfPhS6_"
+name = f"_ZN12_GLOBAL__N_118grid_rollout_numpyILi{ok}ELi{qpt}ELi4EEEvNS_7GridDevEiPKiPvPfPhS6_"
 i = s.index(name + ":")
 j = s.index(".amdhsa_kernel " + name, i)
 lines = s[i:j].split("\n")
@@ -31,7 +31,7 @@ def dump(tag):
     print(f"[{tag}] VALU {v} SALU {sa} LDS {lds} GMEM {gm} | {top}")
 for ln in lines:
     t = ln.strip()
-    if t.startswith("s_memtime"):
+    if t.startswith(("s_memtime", "s_memrealtime")):
         dump(f"before stamp #{seg}")
         seg += 1
         c = collections.Counter()
