@@ -314,6 +314,22 @@ __device__ __forceinline__ int32_t obs_value(const GridDev& p, const TB& tb, int
   }
 }
 
+// The same with the goal-direction offsets held in registers (dof[d] = doff(d) for d < obs_dirs, else a
+// value no cell difference takes): no dependent LDS loads, just the hbase gather.
+template <int OK, class TB>
+__device__ __forceinline__ int32_t obs_value_r(const GridDev& p, const TB& tb, int a, int g, const int (&dof)[8]) {
+  if constexpr (OK == GP_OBS_HANSEN) {
+    int mult = 1;
+    const int diff = g - a;
+#pragma unroll
+    for (int d = 7; d >= 0; --d) mult = diff == dof[d] ? d + 1 : mult;
+    if ((unsigned)g >= (unsigned)p.ncells) mult = 1;
+    return (int32_t)tb.hbase(a) * mult;
+  } else {
+    return tb.t1(a) + (tb.has_t2() ? tb.t2(g) : 0);
+  }
+}
+
 template <int OK, class TB, bool ALIGNED = false>
 __device__ __forceinline__ void write_obs4(const GridDev& p, const TB& tb, int env0, const int (&agent)[4],
                                            const int (&goal)[4], void* __restrict__ obs) {
@@ -873,6 +889,7 @@ struct FusedShared {
   uint32_t nh, nu;               // next step's has_uint32 / uinteger
   uint32_t drawn;                // the control wave drew this step's resetter cells before B2
   uint32_t rdone;                // env waves done listing their resetters in renv (monotone)
+  int32_t dof[8];                // goal-direction cell offsets (Hansen goal multiplier)
   uint16_t renv[2][FEPB];        // STG: env (in tile) of resetter rank r of tile q
   uint32_t pos[FEPB];            // slow path: accepted-word positions of one tile's resetters
   uint32_t pos2[FEPB];
@@ -1135,9 +1152,13 @@ __device__ __forceinline__ void lds_copy(char* dyn, const GridLdsTab& t, const T
 template <int OK, bool STG>
 __device__ __forceinline__ void stage_reset_obs(const GridDev& p, const FusedShared& sh, const LTabs& tb, char* stg,
                                                 int q, uint32_t r, uint32_t cell) {
-  if constexpr (STG)
+  if constexpr (STG) {
+    int dof[8];
+#pragma unroll
+    for (int d = 0; d < 8; ++d) dof[d] = (OK == GP_OBS_HANSEN && d < p.obs_dirs) ? sh.dof[d] : 0x7FFFFFFF;
     reinterpret_cast<int32_t*>(stg + q * STG_TILE_BYTES)[sh.renv[q][r]] =
-        obs_value<OK>(p, tb, (int)(cell >> 16), (int)(cell & 0xFFFFu));
+        obs_value_r<OK>(p, tb, (int)(cell >> 16), (int)(cell & 0xFFFFu), dof);
+  }
 }
 
 template <int OK, int QPT, bool STG>
@@ -1419,6 +1440,10 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
   int32_t a_cur[QPT][4];
   u128 S[QPT];  // lane draw state: jump(s0, e0 + 1)
   uint32_t pc[QPT][4], pfm[QPT];  // previous step's resetters: new cells (goal | agent << 16), masks
+  int dof[8];                     // goal-direction offsets (wave-uniform) for the staged Hansen obs
+#pragma unroll
+  for (int d = 0; d < 8; ++d)
+    dof[d] = (OK == GP_OBS_HANSEN && d < p.obs_dirs) ? __builtin_amdgcn_readfirstlane(tb.doff(d)) : 0x7FFFFFFF;
 #pragma unroll
   for (int q = 0; q < QPT; ++q) {
     const int tau = q * G + (int)blockIdx.x;
@@ -1518,6 +1543,7 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
       if (lane == 0) __hip_atomic_fetch_add(&sh.rdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
+    STAMP(11);
     // ---- 3. this step's outputs (overlap the exchange) ----
     size_t off = (size_t)k * B;
 #ifdef GP_STAMPS
@@ -1531,10 +1557,10 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
       for (int q = 0; q < QPT; ++q) {
         char* t = stg + q * STG_TILE_BYTES;
         int4 ov;
-        ov.x = obs_value<OK>(p, tb, (int)(ae[q][0] & 0xFFFFu), gl[q][0]);
-        ov.y = obs_value<OK>(p, tb, (int)(ae[q][1] & 0xFFFFu), gl[q][1]);
-        ov.z = obs_value<OK>(p, tb, (int)(ae[q][2] & 0xFFFFu), gl[q][2]);
-        ov.w = obs_value<OK>(p, tb, (int)(ae[q][3] & 0xFFFFu), gl[q][3]);
+        ov.x = obs_value_r<OK>(p, tb, (int)(ae[q][0] & 0xFFFFu), gl[q][0], dof);
+        ov.y = obs_value_r<OK>(p, tb, (int)(ae[q][1] & 0xFFFFu), gl[q][1], dof);
+        ov.z = obs_value_r<OK>(p, tb, (int)(ae[q][2] & 0xFFFFu), gl[q][2], dof);
+        ov.w = obs_value_r<OK>(p, tb, (int)(ae[q][3] & 0xFFFFu), gl[q][3], dof);
         const uint32_t drawm = ncalls ? fm[q] : 0u;  // resetters whose cells the control wave draws
         if (!drawm) {
           reinterpret_cast<int4*>(t)[tid] = ov;
@@ -1584,12 +1610,14 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
         write_obs4<OK, LTabs, true>(p, tb, env0, ag, gl[q], ob);
       }
     }
+    STAMP(12);
     if (!STG && k > 0) flush_reset_obs<OK, QPT>(p, tb, (uint8_t*)obs + (off ? off - B : 0) * ow, tid, pc, pfm);
     {
       const PcgJump jB{sh.jB[0], sh.jB[1], sh.jB[2], sh.jB[3]};
 #pragma unroll
       for (int q = 0; q < QPT; ++q) S[q] = apply_jump(jB, S[q]);  // first half of the advance (J_B)
     }
+    STAMP(13);
     lds_barrier();  // B2: the exchange result is in LDS
     STAMP(4);
     // ---- 4. the resetters' draws ----
@@ -1944,6 +1972,7 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
   lds_copy(dyn, p.lds.jt8, p.jt8);
   if (tid < 4) sh.jB[tid] = (&p.fjB->a_hi)[tid];
   if (tid == 0) sh.rdone = 0;
+  if (tid < 8) sh.dof[tid] = (OK == GP_OBS_HANSEN && p.doff && tid < p.obs_dirs) ? p.doff[tid] : 0x7FFFFFFF;
   const LTabs tb{p_in, dyn};
   char* stg = dyn + p.lds.total;  // output staging (STG): after the tables, 16-B aligned
   __syncthreads();
