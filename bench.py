@@ -289,7 +289,7 @@ def main():
                    "parallelism": f"independent env shards x{world}", "steps_per_launch_call": C},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": W.get("kernel") or (("grid_rollout_numpy<GP_OBS_HANSEN,1>" if steps_per_launch > 1.5
+                     "kernel": W.get("kernel") or (("grid_rollout_numpy<GP_OBS_HANSEN,2,4,true>" if steps_per_launch > 1.5
                                                    else "grid_step_numpy<GP_OBS_HANSEN>") if args.mode == "numpy"
                                                   else "grid_rollout_counter<GP_OBS_HANSEN,false>"),
                      "steps_per_launch": steps_per_launch,
