@@ -40,6 +40,7 @@ struct alignas(32) AtSlot {
 
 struct AtDev {
   int32_t B, ntiles, N, ncells;
+  uint32_t divm;           // ceil(2^16 / N): cell / N == (cell * divm) >> 16 for cells < 256
   int32_t tag_r2, vis_r2, time_limit;
   float r_tag, r_step;
   uint32_t key0, key1;
@@ -59,15 +60,21 @@ __device__ __forceinline__ void stage_tables(const AtDev& p, uint8_t* lds) {
 }
 
 __device__ __forceinline__ int isgn(int v) { return (v > 0) - (v < 0); }
+// cell / N without an integer divide (exact for cells < 256, N <= 16)
+__device__ __forceinline__ int cdiv(const AtDev& p, int c) { return (int)(((uint32_t)c * p.divm) >> 16); }
 
+// The reset draws of env `env` at `step`: words 1, 2 of its Philox block (word 0 is the target-move
+// choice of the same step; `r` passes the block when the caller already has it).
 template <bool REPLAY>
-__device__ __forceinline__ uint32_t draw_reset(const AtDev& p, const uint8_t* lds, int env, uint64_t step) {
+__device__ __forceinline__ uint32_t draw_reset(const AtDev& p, const uint8_t* lds, int env, uint64_t step,
+                                               const Philox4* have = nullptr) {
   uint32_t ant, k;
   if constexpr (REPLAY) {
     ant = (uint32_t)min(max(p.rp_ant[env], 0), p.ncells - 1);
     k = (uint32_t)max(p.rp_tgt[env], 0);
   } else {
-    const Philox4 r = philox4x32_10((uint32_t)env, (uint32_t)step, (uint32_t)(step >> 32), TAG, p.key0, p.key1);
+    const Philox4 r = have ? *have
+                           : philox4x32_10((uint32_t)env, (uint32_t)step, (uint32_t)(step >> 32), TAG, p.key0, p.key1);
     ant = lemire_value(r.x[1], (uint32_t)p.ncells);
     k = lemire_value(r.x[2], (uint32_t)lds[p.off_cnt + ant]);
   }
@@ -87,7 +94,7 @@ __device__ __forceinline__ StepOut at_env_step(const AtDev& p, const uint8_t* ld
   const int N = p.N;
   int ant = (int)(u & 0xFFu), tgt = (int)((u >> 8) & 0xFFu);
   uint32_t el = (u >> 16) + 1u;
-  int ay = ant / N, ax = ant - ay * N, ty = tgt / N, tx = tgt - ty * N;
+  int ay = cdiv(p, ant), ax = ant - ay * N, ty = cdiv(p, tgt), tx = tgt - ty * N;
   // ant move
   if (a < 0) a += NACT;
   a = min(max(a, 0), NACT - 1);
@@ -96,11 +103,12 @@ __device__ __forceinline__ StepOut at_env_step(const AtDev& p, const uint8_t* ld
   if (ny >= 0 && ny < N && nx >= 0 && nx < N) { ay = ny; ax = nx; }
   // target move (choose uniform over 4)
   uint32_t choose = 3;
+  Philox4 r{};
   if (live) {
     if constexpr (REPLAY) {
       choose = (uint32_t)p.rp_choose[env] & 3u;
     } else {
-      const Philox4 r = philox4x32_10((uint32_t)env, (uint32_t)step, (uint32_t)(step >> 32), TAG, p.key0, p.key1);
+      r = philox4x32_10((uint32_t)env, (uint32_t)step, (uint32_t)(step >> 32), TAG, p.key0, p.key1);
       choose = r.x[0] >> 30;
     }
   }
@@ -124,14 +132,14 @@ __device__ __forceinline__ StepOut at_env_step(const AtDev& p, const uint8_t* ld
   if (o.term | o.trunc) {
     eps += 1u;
     lens += el;
-    u = draw_reset<REPLAY>(p, lds, env, step);
+    u = draw_reset<REPLAY>(p, lds, env, step, &r);
   }
   return o;
 }
 
 __device__ __forceinline__ int4 at_obs(const AtDev& p, uint32_t u) {
   const int N = p.N, ant = (int)(u & 0xFFu), tgt = (int)((u >> 8) & 0xFFu);
-  const int ay = ant / N, ax = ant - ay * N, ty = tgt / N, tx = tgt - ty * N;
+  const int ay = cdiv(p, ant), ax = ant - ay * N, ty = cdiv(p, tgt), tx = tgt - ty * N;
   const int dy = ay - ty, dx = ax - tx;
   const bool vis = dy * dy + dx * dx < p.vis_r2;
   return make_int4(ay, ax, vis ? ty : -1, vis ? tx : -1);
@@ -171,8 +179,11 @@ __global__ __launch_bounds__(TPB) void anttag_rollout(AtDev p, int K, uint64_t s
                                                       int4* __restrict__ obs, float* __restrict__ rew,
                                                       uint8_t* __restrict__ term, uint8_t* __restrict__ trunc) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  __shared__ int4 s_obs[TPB * EPT];  // per-wave obs transpose: lane-contiguous 16-B obs stores
   stage_tables(p, lds);
   __syncthreads();
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int4* wv = s_obs + wid * 64 * EPT;
   float rsum = 0.f;
   uint32_t eps = 0, lens = 0, nst = 0;
   for (int tile = blockIdx.x; tile < p.ntiles; tile += gridDim.x) {
@@ -186,9 +197,8 @@ __global__ __launch_bounds__(TPB) void anttag_rollout(AtDev p, int K, uint64_t s
 #pragma unroll
       for (int i = 0; i < EPT; ++i) u[i] = env0 + i < p.B ? p.st[env0 + i] : 0u;
     }
-    for (int k = 0; k < K; ++k) {
+    auto load_act = [&](int k, int (&a)[EPT]) {
       const size_t off = (size_t)k * p.B;
-      int a[EPT];
       if (quad_ok(act + off, env0, p.B, 4)) {
         const int4 q = *reinterpret_cast<const int4*>(act + off + env0);
         a[0] = q.x; a[1] = q.y; a[2] = q.z; a[3] = q.w;
@@ -196,6 +206,15 @@ __global__ __launch_bounds__(TPB) void anttag_rollout(AtDev p, int K, uint64_t s
 #pragma unroll
         for (int i = 0; i < EPT; ++i) a[i] = env0 + i < p.B ? act[off + env0 + i] : 0;
       }
+    };
+    int a_nxt[EPT];
+    if (K > 0) load_act(0, a_nxt);
+    for (int k = 0; k < K; ++k) {
+      const size_t off = (size_t)k * p.B;
+      int a[EPT];
+#pragma unroll
+      for (int i = 0; i < EPT; ++i) a[i] = a_nxt[i];
+      if (k + 1 < K) load_act(k + 1, a_nxt);  // one step ahead
       float r[EPT];
       uint8_t tm[EPT], tr[EPT];
 #pragma unroll
@@ -218,9 +237,18 @@ __global__ __launch_bounds__(TPB) void anttag_rollout(AtDev p, int K, uint64_t s
         for (int i = 0; i < EPT; ++i)
           if (env0 + i < p.B) { rew[off + env0 + i] = r[i]; term[off + env0 + i] = tm[i]; trunc[off + env0 + i] = tr[i]; }
       }
+      // obs: through LDS so that each store instruction writes 64 consecutive envs (1 KB)
 #pragma unroll
-      for (int i = 0; i < EPT; ++i)
-        if (env0 + i < p.B) obs[off + env0 + i] = at_obs(p, u[i]);
+      for (int i = 0; i < EPT; ++i) wv[lane * EPT + i] = at_obs(p, u[i]);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+      const int wenv0 = tile * EPB + wid * 64 * EPT;
+#pragma unroll
+      for (int j = 0; j < EPT; ++j) {
+        const int e = wenv0 + j * 64 + lane;
+        if (e < p.B) obs[off + e] = wv[j * 64 + lane];
+      }
     }
     if (sq) {
       *reinterpret_cast<uint4*>(p.st + env0) = make_uint4(u[0], u[1], u[2], u[3]);
@@ -429,6 +457,7 @@ int AntTagBackend::build(const gp_anttag_config* cfg) {
   d.B = (int32_t)B;
   d.ntiles = (int32_t)((B + EPB - 1) / EPB);
   d.N = N;
+  d.divm = (65536u + (uint32_t)N - 1u) / (uint32_t)N;
   d.ncells = nc;
   d.tag_r2 = cfg->tag_radius2;
   d.vis_r2 = cfg->visible_radius2;

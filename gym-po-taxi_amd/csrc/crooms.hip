@@ -50,6 +50,7 @@ struct CrDev {
   int32_t n_valid, time_limit;
   uint32_t key0, key1;
   double cell, half_cell, hi_y, hi_x, s_thr, action_std, action_power;
+  double inv_cell;       // 1 / cell when cell is a power of two (then y * inv_cell == y / cell exactly), else 0
   float r_step, r_wall, r_goal;
   const uint8_t* tabs;   // packed tables, staged into LDS
   int32_t off_wall, off_valid, off_thr, off_t1, off_t2, off_hbase, off_hvec, off_doff, off_window, tab_bytes;
@@ -100,14 +101,21 @@ struct Draws {
 // :194-195), pair 1 = wall noise N(0, 0.5) (:324). Replay: the values numpy returned.
 template <bool REPLAY>
 __device__ __forceinline__ void draw_normals(const CrDev& p, int env, uint64_t step, int pair, double scale,
-                                             double& y, double& x) {
+                                             double& y, double& x, Philox4* blk = nullptr, bool* have = nullptr) {
   if constexpr (REPLAY) {
     const double* src = pair == 0 ? p.rp_noise : p.rp_wall;
     const double2 v = *reinterpret_cast<const double2*>(src + 2 * (size_t)env);
     y = v.x;
     x = v.y;
   } else {
-    const Philox4 r = philox4x32_10((uint32_t)env, (uint32_t)step, (uint32_t)(step >> 32), TAG_NOISE, p.key0, p.key1);
+    // one Philox block per env-step serves both pairs (the caller keeps it in blk / have)
+    Philox4 r;
+    if (have && *have) {
+      r = *blk;
+    } else {
+      r = philox4x32_10((uint32_t)env, (uint32_t)step, (uint32_t)(step >> 32), TAG_NOISE, p.key0, p.key1);
+      if (have) { *blk = r; *have = true; }
+    }
     double z0, z1;
     box_muller(r.x[2 * pair], r.x[2 * pair + 1], z0, z1);
     y = scale * z0;
@@ -134,9 +142,14 @@ struct Cells {
   int ac, gc;      // flat cells of agent / goal (gc = -1 when the goal lies off the grid)
 };
 
+// coord / cell_size, exactly as numpy divides (a multiply when cell_size is a power of two)
+__device__ __forceinline__ double per_cell(const CrDev& p, double v) {
+  return p.inv_cell != 0.0 ? v * p.inv_cell : v / p.cell;
+}
+
 __device__ __forceinline__ int cell_of(const CrDev& p, double y, double x) {
   // coord_to_grid (utils.py:15-20): floor(coord / cell_size)
-  const int cy = (int)floor(y / p.cell), cx = (int)floor(x / p.cell);
+  const int cy = (int)floor(per_cell(p, y)), cx = (int)floor(per_cell(p, x));
   if (cy < 0 || cx < 0 || cy >= p.H || cx >= p.W) return -1;
   return cy * p.W + cx;
 }
@@ -239,9 +252,11 @@ __device__ __forceinline__ StepOut crooms_env_step(const CrDev& p, const uint8_t
   d.gi = d.ai = 0;
   // _sample_action (crooms.py:175-198) * action_power (:288)
   double my, mx;
+  Philox4 nblk;
+  bool nhave = false;
   if (p.action_kind == 0) {
     double ny = 0.0, nx = 0.0;
-    if (live) draw_normals<REPLAY>(p, env, step, 0, p.action_std, ny, nx);
+    if (live) draw_normals<REPLAY>(p, env, step, 0, p.action_std, ny, nx, &nblk, &nhave);
     my = a0 + ny;
     mx = a1 + nx;
   } else {
@@ -259,7 +274,7 @@ __device__ __forceinline__ StepOut crooms_env_step(const CrDev& p, const uint8_t
     mx = (double)DX[o8];
     if (p.action_std != 0.0) {
       double ny = 0.0, nx = 0.0;
-      if (live) draw_normals<REPLAY>(p, env, step, 0, p.action_std, ny, nx);
+      if (live) draw_normals<REPLAY>(p, env, step, 0, p.action_std, ny, nx, &nblk, &nhave);
       my = my + ny;
       mx = mx + nx;
     }
@@ -286,10 +301,10 @@ __device__ __forceinline__ StepOut crooms_env_step(const CrDev& p, const uint8_t
     ax = px;
   } else {
     // stay in the current square: c = grid_to_coord(coord_to_grid(agent)), agent = clip(c + n, c - cs/2, c + cs/2 - 1e-8)
-    const double cy = floor(ay / p.cell) * p.cell + p.half_cell;
-    const double cx = floor(ax / p.cell) * p.cell + p.half_cell;
+    const double cy = floor(per_cell(p, ay)) * p.cell + p.half_cell;
+    const double cx = floor(per_cell(p, ax)) * p.cell + p.half_cell;
     double wy = 0.0, wx = 0.0;
-    if (live) draw_normals<REPLAY>(p, env, step, 1, 0.5, wy, wx);
+    if (live) draw_normals<REPLAY>(p, env, step, 1, 0.5, wy, wx, &nblk, &nhave);
     ay = fmin(fmax(cy + wy, cy - p.half_cell), (cy + p.half_cell) - 1e-8);
     ax = fmin(fmax(cx + wx, cx - p.half_cell), (cx + p.half_cell) - 1e-8);
     vy = 0.0;
@@ -387,13 +402,18 @@ __global__ __launch_bounds__(TPB) void crooms_rollout(CrDev p, int K, uint64_t s
             }
         } else {
           const float* A = (const float*)act + 2 * (off + env0);
+          if (full) {  // both envs' (y, x) in one 16-B load
+            const float4 q = *reinterpret_cast<const float4*>(A);
+            a0[0] = q.x; a1[0] = q.y; a0[1] = q.z; a1[1] = q.w;
+          } else {
 #pragma unroll
-          for (int i = 0; i < EPT; ++i)
-            if (env0 + i < p.B) {
-              const float2 q = *reinterpret_cast<const float2*>(A + 2 * i);
-              a0[i] = q.x;
-              a1[i] = q.y;
-            }
+            for (int i = 0; i < EPT; ++i)
+              if (env0 + i < p.B) {
+                const float2 q = *reinterpret_cast<const float2*>(A + 2 * i);
+                a0[i] = q.x;
+                a1[i] = q.y;
+              }
+          }
         }
       } else {
         const int32_t* A = (const int32_t*)act + off + env0;
@@ -428,9 +448,15 @@ __global__ __launch_bounds__(TPB) void crooms_rollout(CrDev p, int K, uint64_t s
       }
       const size_t ob = (size_t)k * p.B * (size_t)p.obs_width * (OK == GP_OBS_F32 ? (p.obs_f64 ? 8 : 4)
                                                                    : (OK == GP_OBS_HANSEN || OK == GP_OBS_TABLE ? 4 : 1));
+      if (OK == GP_OBS_F32 && !p.obs_f64 && p.obs_width == 2 && full) {
+        // vector_mdp (configs[4]): both envs' float32 (y, x) in one 16-B store
+        *reinterpret_cast<float4*>((float*)((uint8_t*)obs + ob) + 2 * (size_t)env0) =
+            make_float4((float)ay[0], (float)ax[0], (float)ay[1], (float)ax[1]);
+      } else {
 #pragma unroll
-      for (int i = 0; i < EPT; ++i)
-        if (env0 + i < p.B) write_obs<OK>(p, lds, env0 + i, ay[i], ax[i], g[i], (uint8_t*)obs + ob);
+        for (int i = 0; i < EPT; ++i)
+          if (env0 + i < p.B) write_obs<OK>(p, lds, env0 + i, ay[i], ax[i], g[i], (uint8_t*)obs + ob);
+      }
     }
 #pragma unroll
     for (int i = 0; i < EPT; ++i) {
@@ -714,6 +740,11 @@ int CRoomsBackend::build(const gp_crooms_config* cfg) {
   d.nact = cfg->action_kind == 0 ? 0 : cfg->action_kind;
   d.cell = cfg->cell_size;
   d.half_cell = cfg->cell_size / 2;
+  {
+    int ex = 0;
+    const double m = std::frexp(cfg->cell_size, &ex);
+    d.inv_cell = (m == 0.5 && cfg->cell_size > 0) ? 1.0 / cfg->cell_size : 0.0;  // exact reciprocal of 2^k
+  }
   d.hi_y = (double)(H - 1) - 1e-6;  // gridshape - 1 - 1e-6 (crooms.py:311-313)
   d.hi_x = (double)(W - 1) - 1e-6;
   d.s_thr = sq_threshold(cfg->goal_threshold);
