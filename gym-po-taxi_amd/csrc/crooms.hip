@@ -83,13 +83,14 @@ __device__ __forceinline__ void stage_tables(const CrDev& p, uint8_t* lds) {
 
 // ---- draws ----
 // Box-Muller on two 32-bit words: z0 = r cos(2 pi u2), z1 = r sin(2 pi u2), r = sqrt(-2 ln u1), u1 in (0,1].
+// Hardware transcendentals (float32 accuracy, which is all the law needs): v_log_f32 = log2,
+// v_sin/cos_f32 take revolutions, i.e. sin(2 pi u2) directly.
 __device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, double& z0, double& z1) {
-  const float u1 = ((float)(a >> 8) + 1.0f) * 5.9604644775390625e-08f;  // (k+1) 2^-24
-  const float r = sqrtf(-2.0f * logf(u1));
-  float s, c;
-  sincospif((float)(b >> 8) * 1.1920928955078125e-07f, &s, &c);       // 2 u2 with u2 = k 2^-24
-  z0 = (double)(r * c);
-  z1 = (double)(r * s);
+  const float u1 = ((float)(a >> 8) + 1.0f) * 5.9604644775390625e-08f;  // (k+1) 2^-24, in (0, 1]
+  const float r = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));  // sqrt(-2 ln u1)
+  const float u2 = (float)(b >> 8) * 5.9604644775390625e-08f;           // k 2^-24, in [0, 1)
+  z0 = (double)(r * __builtin_amdgcn_cosf(u2));
+  z1 = (double)(r * __builtin_amdgcn_sinf(u2));
 }
 
 struct Draws {
