@@ -60,7 +60,7 @@ def _anttag(B, dev, mode):
 # bytes: algorithmic bytes per env-step of a fused rollout launch; state: bytes per env
 # read + written once per launch.
 WORKLOADS = {
-    "fourrooms": dict(make=_fourrooms, envs=1 << 20, n_actions=4, mode="numpy", bytes=14, state=8,
+    "fourrooms": dict(make=_fourrooms, envs=1 << 20, n_actions=4, mode="numpy", bytes=14, state=8, chunk=128,
                       metric=HEADLINE_METRIC, dtype="int32",
                       desc="configs[1]: FourRooms 11x11 (FR_MAP) Hansen-4 obs, {B} envs per GPU, "
                            "MultistoryFourRoomsEnv(grid_z=1, obs_type='hansen')"),

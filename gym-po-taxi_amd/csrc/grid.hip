@@ -1495,7 +1495,7 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
         const uint32_t el = (s_ae >> 16) + 1u;
         const bool tm_ = na_ == gl[q][i];
         const bool tr_ = el > (uint32_t)tlim;
-        const bool valid = env0 + i < B;
+        const bool valid = STG || env0 + i < B;  // STG launches have only complete tiles
         const bool f = valid && (tm_ || tr_);
         const float rw = tm_ ? r_goal : (blocked ? r_wall : r_step);
         tmm[q] |= (uint32_t)tm_ << i;
@@ -2732,7 +2732,10 @@ int GridBackend::build(const gp_grid_config* cfg) {
       fused_qpt = qpt <= 1 ? 1 : (qpt <= 2 ? 2 : 4);
       const int k = cfg->obs_kind;
       const char* ns = getenv("GP_NO_STAGING");  // tuning knob: direct output stores from the env waves
-      if (fused_qpt <= 2 && (k == GP_OBS_HANSEN || k == GP_OBS_TABLE) && !(ns && ns[0] == '1')) {
+      // staged outputs: <= 2 tiles per block, scalar obs, and only complete tiles (every block owns exactly
+      // fused_qpt full 2048-env tiles: the staged kernel drops the per-env bounds checks)
+      if (fused_qpt <= 2 && (k == GP_OBS_HANSEN || k == GP_OBS_TABLE) && !(ns && ns[0] == '1') &&
+          (int64_t)B == (int64_t)fused_qpt * G * FEPB) {
         int occ2 = 0;
         GP_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
             &occ2, grid_rollout_numpy<GP_OBS_HANSEN, 2, 8, true>, FTPB, d.lds.total + 2 * STG_TILE_BYTES));
