@@ -1379,18 +1379,17 @@ __device__ __forceinline__ void fused_resets(const GridDev& p, FusedShared& sh, 
 }
 
 
-// Effective action of env with action a and 53-bit uniform k: #{j : k > thr[a][j]} (integer form
-// of action_utils.py:84-90), on the high 32 bits with an exact 64-bit fallback on a tie.
+// Effective action of env with action a and 53-bit uniform k: min(#{j : k > thr[a][j]}, NA - 1) (integer
+// form of action_utils.py:84-90 with the reference's cumsum thresholds). The thresholds of a row are
+// non-decreasing (a cumulative sum), so the count is the first j with k <= thr[j]: NA - 1 compares as a
+// select chain (the last threshold never matters: k > thr[NA-2] already gives NA - 1 after the clamp).
 template <int NA>
 __device__ __forceinline__ uint32_t fused_effective_action(const uint64_t* s_thr, int a, uint64_t k) {
-  const ulonglong2* t = reinterpret_cast<const ulonglong2*>(s_thr + a * NA);
+  const uint64_t* t = s_thr + a * NA;
   uint32_t e = 0;
 #pragma unroll
-  for (int h = 0; h < NA / 2; ++h) {
-    const ulonglong2 v = t[h];
-    e += (k > v.x ? 1u : 0u) + (k > v.y ? 1u : 0u);
-  }
-  return min(e, (uint32_t)NA - 1);
+  for (int j = 0; j < NA - 1; ++j) e = k > t[j] ? (uint32_t)(j + 1) : e;
+  return e;
 }
 
 // The obs of the previous step's resetters (their provisional obs were stored with the step's
