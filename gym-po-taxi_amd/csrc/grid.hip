@@ -1469,7 +1469,15 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
     if (k + 1 < K) {
 #pragma unroll
       for (int q = 0; q < QPT; ++q)
-        load4f<int32_t>(act + (size_t)(k + 1) * B, (q * G + (int)blockIdx.x) * FEPB + tid * EPT, B, a_nxt[q]);
+      {
+        const int e0 = (q * G + (int)blockIdx.x) * FEPB + tid * EPT;
+        if constexpr (STG) {  // complete tiles: one unconditional 16-B load
+          const int4 v = *reinterpret_cast<const int4*>(act + (size_t)(k + 1) * B + e0);
+          a_nxt[q][0] = v.x; a_nxt[q][1] = v.y; a_nxt[q][2] = v.z; a_nxt[q][3] = v.w;
+        } else {
+          load4f<int32_t>(act + (size_t)(k + 1) * B, e0, B, a_nxt[q]);
+        }
+      }
     }
     // ---- 1. draws + transitions (the critical path) ----
     uint32_t fm[QPT], tmm[QPT], trm[QPT], bkm[QPT], excl[QPT], wex[QPT], wt[QPT];
