@@ -118,6 +118,16 @@ def test_ragged_batch_sizes(B, gpu_device):
     _run_vs_oracle(meta, B, 60, seed=B, action_seed=B + 1)
 
 
+@pytest.mark.parametrize("name,B,T", [("rooms_2_goal_mdp_randgoal", 2048 * 40, 40), ("rooms_4_hansen8", 2048 * 40, 40),
+                                       ("fr_goal_mdp_z2_randgoal", 2048 * 64, 30),
+                                       ("rooms_2_goal_mdp_randgoal", 1 << 20, 6)])
+def test_staged_fused_kernel_variants(name, B, T, gpu_device):
+    """Batch sizes of whole 2048-env tiles per block take the LDS-staged fused kernel (store waves, resetter
+    obs written by the control wave): random goals (two reset calls, coverage rounds), table obs, Hansen-8."""
+    meta, _ = load_case(name)
+    _run_vs_oracle(meta, B, T, seed=B % 97, action_seed=7)
+
+
 def test_rooms_random_goal_two_pass_large(gpu_device):
     meta, _ = load_case("rooms_2_goal_mdp_randgoal")
     _run_vs_oracle(meta, 50_000, 70, seed=3, action_seed=4)
