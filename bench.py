@@ -196,10 +196,17 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local if world > 1 else 0)
-    torch.cuda.set_device(dev)
+        # one rank per GPU; GP_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share devices)
+        backend = os.environ.get("GP_BENCH_BACKEND", "nccl")
+        dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
+        torch.cuda.set_device(dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    else:
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
 
     W = WORKLOADS[args.workload]
     args.envs = args.envs or W["envs"]
