@@ -1160,10 +1160,19 @@ __device__ __forceinline__ void stage_reset_obs(const GridDev& p, const FusedSha
         obs_value_r<OK>(p, tb, (int)(cell >> 16), (int)(cell & 0xFFFFu), dof);
   }
 }
+// The same with the slot (renv) and the direction offsets already in registers.
+template <int OK, bool STG>
+__device__ __forceinline__ void stage_reset_obs_r(const GridDev& p, const LTabs& tb, char* stg, int q, int slot,
+                                                  uint32_t cell, const int (&dof)[8]) {
+  if constexpr (STG)
+    reinterpret_cast<int32_t*>(stg + q * STG_TILE_BYTES)[slot] =
+        obs_value_r<OK>(p, tb, (int)(cell >> 16), (int)(cell & 0xFFFFu), dof);
+}
 
 template <int OK, int QPT, bool STG>
 __device__ __forceinline__ void ctrl_fast_finish(const GridDev& p, FusedShared& sh, const LTabs& tb, const u128 SB,
-                                                 const Stream& st, uint32_t b, uint32_t tq, uint32_t pre, char* stg) {
+                                                 const Stream& st, uint32_t b, uint32_t tq, uint32_t pre, char* stg,
+                                                 const int (&dof)[8]) {
   const int lane = threadIdx.x & 63;
   const bool rgoal = p.fixed_goal < 0;
   const uint32_t nsel = rgoal ? (uint32_t)p.n_goal_valid : (uint32_t)p.n_agent_valid;
@@ -1199,6 +1208,8 @@ __device__ __forceinline__ void ctrl_fast_finish(const GridDev& p, FusedShared& 
     const uint32_t ww = w - st.h0;
     const uint32_t n = extra ? used : (cellj && !buffered ? (ww >> 1) + 1u : 0u);
     const PcgJump jlo = t8[n & 255u], jhi = t8[256u + ((n >> 8) & 255u)];
+    // the env slot of this resetter (STG), loaded alongside the jump tables, off the dependent chain
+    const int slot = STG ? (int)sh.renv[q][min(r, (uint32_t)FEPB - 1u)] : 0;
     PcgJump J1 = jlo, J2 = jhi;
     u128 X0 = SB;
     if (extra && lane == 61) {
@@ -1217,7 +1228,7 @@ __device__ __forceinline__ void ctrl_fast_finish(const GridDev& p, FusedShared& 
       const uint32_t goal = rgoal ? (uint32_t)tb.gv((int)v) : (uint32_t)p.fixed_goal;
       const uint32_t agent = rgoal ? (uint32_t)p.fixed_agent : (uint32_t)tb.av((int)v);
       sh.cell[q * FEPB + r] = goal | (agent << 16);
-      stage_reset_obs<OK, STG>(p, sh, tb, stg, q, r, goal | (agent << 16));
+      stage_reset_obs_r<OK, STG>(p, tb, stg, q, slot, goal | (agent << 16), dof);
     } else if (extra) {
       if (lane == 61) { sh.ju[0] = hi64(X); sh.ju[1] = lo64(X); }
       if (lane == 62) { sh.ju[2] = hi64(X); sh.ju[3] = lo64(X); }
@@ -1703,6 +1714,9 @@ __device__ __forceinline__ void fused_ctrl(const GridDev& p_in, FusedShared& sh,
   for (int k = 0; k < K; ++k) {
     const uint32_t tag0 = (step_base + (uint32_t)k + 1u) * 4u;
     uint64_t* slots = p.fslot + (size_t)((step_base + (uint32_t)k) & 1u) * 3 * G;
+    int cdof[8];  // goal-direction offsets for the resetters' staged obs (read long before they are used)
+#pragma unroll
+    for (int d = 0; d < 8; ++d) cdof[d] = sh.dof[d];
     // speculative Lemire check of the RCOV-word windows of this block's tiles (call 1)
     uint32_t crej = 0;
     const uint32_t ll = lane & 31;
@@ -1824,7 +1838,7 @@ __device__ __forceinline__ void fused_ctrl(const GridDev& p_in, FusedShared& sh,
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
     }
     if (drawn) {
-      ctrl_fast_finish<OK, QPT, STG>(p, sh, tb, SB, st, b, tq, mypre, stg);  // cells + next state, before B2
+      ctrl_fast_finish<OK, QPT, STG>(p, sh, tb, SB, st, b, tq, mypre, stg, cdof);  // cells + next state, before B2
     } else if (known) {
       publish_next(tb, sh, SB, ncalls ? b : 0u, st.h0, st.u0, lane == 0);
     }
