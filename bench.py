@@ -103,6 +103,30 @@ def src_hash(workload):
     return h.hexdigest()[:12]
 
 
+def measured_hbm_peaks(dev, nbytes=1 << 31, reps=10):
+    """Measured HBM ceilings on this GPU (reported beside the spec peak): a device-to-device
+    copy (read + write bytes counted) and a write-only fill, 2 GiB buffers, HIP events, best of `reps`."""
+    import torch
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    a.fill_(1)
+    out = {}
+    for name, fn, moved in (("copy", lambda: b.copy_(a), 2 * nbytes), ("fill", lambda: b.fill_(7), nbytes)):
+        fn()
+        best = float("inf")
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            e1.synchronize()
+            best = min(best, e0.elapsed_time(e1) * 1e-3)
+        out[name] = moved / best / 1e9
+    del a, b
+    torch.cuda.empty_cache()
+    return out
+
+
 def cpu_baseline(workload="fourrooms", target_s=12.0):
     """The numpy oracle (the reference's algorithm restated, fixture-pinned) on one host core."""
     import numpy as np
@@ -311,6 +335,11 @@ def main():
         "lib_hash": lib_hash(),
     }
     if rank == 0:
+        if world == 1:
+            pk = measured_hbm_peaks(dev)
+            line["roofline"]["measured_copy_gbs"] = pk["copy"]
+            line["roofline"]["measured_fill_gbs"] = pk["fill"]
+            line["roofline"]["frac_of_measured_fill"] = achieved / pk["fill"]
         line["cpu_baseline"] = None if args.no_cpu_baseline else cpu_baseline(args.workload)
         print(json.dumps(line), flush=True)
     env.close()
