@@ -28,4 +28,10 @@ for W in ${WORKLOADS:-fourrooms taxi crooms anttag}; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$W -o bench -- python3 bench.py --workload $W --no-cpu-baseline > $O/prof_$W.log 2>&1 || { echo "PROF_FAIL $W"; tail -20 $O/prof_$W.log; exit 1; }
   for f in $(find $O/prof_$W -name "*kernel_stats.csv"); do cp $f $O/kernel_stats_$W.csv; done
 done
+
+# secondary line: FourRooms in rng_mode philox (counter-based draws, no per-step grid exchange)
+if [ -z "$SKIP_PHILOX" ]; then
+  timeout -k 10 300 python bench.py --mode philox --no-cpu-baseline > $O/bench_fourrooms_philox.log 2>&1 || { echo "BENCH_FAIL philox"; tail -20 $O/bench_fourrooms_philox.log; exit 1; }
+  python3 -c "import json; d=json.loads(open('$O/bench_fourrooms_philox.log').read().strip().splitlines()[-1]); r=d['roofline']; print('fourrooms-philox', 'value %.4e'%d['value'], 'frac %.3f'%r['frac'], r['kernel'])"
+fi
 echo EVIDENCE_OK
