@@ -2043,19 +2043,20 @@ __device__ __forceinline__ void philox_draws(const GridDev& p, int env, uint64_t
   ai = lemire_value(r.x[3], (uint32_t)max(p.n_agent_valid, 1));
 }
 
-template <int OK>
-__device__ __forceinline__ void counter_env_step(const GridDev& p, const uint64_t* thr, uint32_t& ae, int& goal, int a,
-                                                 uint64_t k53, uint32_t gi, uint32_t ai, float& r, uint8_t& tm,
-                                                 uint8_t& tr, float& rsum, uint32_t& eps, uint32_t& lens) {
-  Trans t = transition(p, GTabs{p}, ae, goal, a, k53, thr);
+template <int OK, class TB>
+__device__ __forceinline__ void counter_env_step(const GridDev& p, const TB& tb, const uint64_t* thr, uint32_t& ae,
+                                                 int& goal, int a, uint64_t k53, uint32_t gi, uint32_t ai, float& r,
+                                                 uint8_t& tm, uint8_t& tr, float& rsum, uint32_t& eps,
+                                                 uint32_t& lens) {
+  Trans t = transition(p, tb, ae, goal, a, k53, thr);
   int agent = t.agent, g = goal, el = t.elapsed;
   rsum += t.rew;
   if (t.term | t.trunc) {
     eps += 1;
     lens += (uint32_t)el;
     el = 0;
-    g = p.fixed_goal >= 0 ? p.fixed_goal : (int)p.goal_valid[gi];
-    agent = p.fixed_agent >= 0 ? p.fixed_agent : (int)p.agent_valid[ai];
+    g = p.fixed_goal >= 0 ? p.fixed_goal : (int)tb.gv((int)gi);
+    agent = p.fixed_agent >= 0 ? p.fixed_agent : (int)tb.av((int)ai);
   }
   ae = (uint32_t)agent | ((uint32_t)el << 16);
   goal = g;
@@ -2064,14 +2065,35 @@ __device__ __forceinline__ void counter_env_step(const GridDev& p, const uint64_
   tr = t.trunc;
 }
 
-template <int OK, bool REPLAY>
+template <bool LT>
+__device__ __forceinline__ auto make_tabs(const GridDev& p, const char* dyn) {
+  if constexpr (LT) return LTabs{p, dyn};
+  else return GTabs{p};
+}
+
+// LT: the lookup tables staged in LDS (K-step rollouts, when they fit) instead of read through the caches.
+template <int OK, bool REPLAY, bool LT = false>
 __global__ __launch_bounds__(TPB) void grid_rollout_counter(GridDev p, int K, uint64_t step0,
                                                             const int32_t* __restrict__ act, void* __restrict__ obs,
                                                             float* __restrict__ rew, uint8_t* __restrict__ term,
                                                             uint8_t* __restrict__ trunc) {
   __shared__ uint64_t s_thr[64];
+  extern __shared__ __attribute__((aligned(16))) char dyn[];
   if (threadIdx.x < p.nact * p.nact) s_thr[threadIdx.x] = p.thr[threadIdx.x];
+  if constexpr (LT) {
+    lds_copy(dyn, p.lds.move, p.move);
+    lds_copy(dyn, p.lds.hbase, p.hbase);
+    lds_copy(dyn, p.lds.hvec, p.hvec);
+    lds_copy(dyn, p.lds.t1, p.t1);
+    lds_copy(dyn, p.lds.t2, p.t2);
+    lds_copy(dyn, p.lds.coords, p.coords);
+    lds_copy(dyn, p.lds.window, p.window);
+    lds_copy(dyn, p.lds.gv, p.goal_valid);
+    lds_copy(dyn, p.lds.av, p.agent_valid);
+    lds_copy(dyn, p.lds.doff, p.doff);
+  }
   __syncthreads();
+  const auto tb = make_tabs<LT>(p, dyn);
   const int env0 = blockIdx.x * EPB + threadIdx.x * EPT;
   uint32_t ae4[4];
   load4<uint32_t>(p.ae, env0, p.B, ae4);
@@ -2108,7 +2130,7 @@ __global__ __launch_bounds__(TPB) void grid_rollout_counter(GridDev p, int K, ui
           philox_draws(p, env, step0 + k, k53, gi, ai);
         }
       }
-      counter_env_step<OK>(p, s_thr, ae4[i], g4[i], a4[i], k53, gi, ai, r[i], tm[i], tr[i], rsum, eps, lens);
+      counter_env_step<OK>(p, tb, s_thr, ae4[i], g4[i], a4[i], k53, gi, ai, r[i], tm[i], tr[i], rsum, eps, lens);
       nst += env < p.B;
     }
     store4<float>(rew + off, env0, p.B, r);
@@ -2117,7 +2139,7 @@ __global__ __launch_bounds__(TPB) void grid_rollout_counter(GridDev p, int K, ui
     int ag[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) ag[i] = (int)(ae4[i] & 0xFFFF);
-    write_obs4<OK>(p, GTabs{p}, env0, ag, g4, (uint8_t*)obs + (size_t)k * p.B * ow);
+    write_obs4<OK>(p, tb, env0, ag, g4, (uint8_t*)obs + (size_t)k * p.B * ow);
   }
   store4<uint32_t>(p.ae, env0, p.B, ae4);
   if (p.fixed_goal < 0) {
@@ -2473,8 +2495,12 @@ int GridBackend::rollout(int K, const void* act, void* obs, float* rew, uint8_t*
   int e = dispatch_obs(d.obs_kind, [&](auto okc) -> int {
     constexpr int OK = decltype(okc)::value;
     timer.begin(s);
-    hipLaunchKernelGGL((grid_rollout_counter<OK, false>), dim3(d.nblk), dim3(TPB), 0, s, d, K, philox_step,
-                       (const int32_t*)act, obs, rew, term, trunc);
+    if (d.lds.total > 0)  // tables in LDS (all but the PCG jump tables, which sit at the end of the layout)
+      hipLaunchKernelGGL((grid_rollout_counter<OK, false, true>), dim3(d.nblk), dim3(TPB), (size_t)d.lds.jt.off, s, d,
+                         K, philox_step, (const int32_t*)act, obs, rew, term, trunc);
+    else
+      hipLaunchKernelGGL((grid_rollout_counter<OK, false>), dim3(d.nblk), dim3(TPB), 0, s, d, K, philox_step,
+                         (const int32_t*)act, obs, rew, term, trunc);
     timer.end(s);
     return GP_OK;
   });
