@@ -838,25 +838,25 @@ __global__ __launch_bounds__(TPB) void grid_reset_init(GridDev p) {
 }
 
 // ------------------------------------------------------------------ kernel: fused numpy rollout ----
-// K numpy-exact steps in ONE persistent launch. Block b (512 threads = 8 waves, 4 envs per
-// thread) owns the 2048-env tiles tau = q*G + b (q < QPT); env state lives in registers for the
-// whole launch and the lookup tables in LDS. Per step (s0 = PCG64 state at the step start):
-//   1. every env e draws u64 #e of random(B) from its lane state S_e = jump(s0, e+1) and
-//      transitions (critical path: nothing else happens before the publish).
-//   2. per-wave reset counts by ballot bit-planes -> LDS -> barrier B1 -> thread 0 publishes ONE
-//      tagged 8-B granule per block {tag, Lemire-rejection bit, 12-bit reset count per tile}.
-//      The rejection bit covers a speculative window of RCOV choice() words per tile, checked
-//      by a spare wave per tile.
-//   3. wave 0 all-gathers the G block granules (4 per lane, the only inter-block exchange),
-//      scans them (DPP) into this block's tile prefixes, the total b and the rejection flag, and
-//      in the common case already derives the next state s0' = J_used(J_B(s0)). Meanwhile the
-//      other waves store rewards / flags / the obs of non-resetting envs (wave 0 stores its own
-//      after the gather, so its polling loads never wait behind its stores).
-//   4. barrier B2; resetters draw their choice() words (goal call, then agent call) at word
-//      position prefix + rank (+b). Extra check rounds extend the rejection coverage when b
-//      exceeds it (mass resets) or for the second call; a rejection anywhere switches to the
-//      exact stream walk (p ~ 1e-8/word).
-//   5. every lane state advances by J_used (J_B was applied in step 3's slack).
+// K numpy-exact steps in ONE persistent launch, one block per CU (G <= 256). Block b owns the 2048-env
+// tiles tau = q*G + b (q < QPT); env state lives in registers for the whole launch and the lookup tables
+// in LDS. Waves: 8 env waves (4 envs per thread per tile), 1 control wave, 2 store waves. Per step
+// (s0 = PCG64 state at the step start):
+//   1. env waves: every env e draws u64 #e of random(B) from its lane state S_e = jump(s0, e+1) and
+//      transitions (critical path); per-wave reset counts by ballot bit-planes -> LDS -> barrier B1.
+//   2. control wave: publishes ONE tagged 8-B granule per block {tag, Lemire-rejection bit, 12-bit
+//      reset count per tile} (the rejection bit covers a speculative window of RCOV choice() words per
+//      tile, checked before B1), all-gathers the G granules (4 per lane, the only inter-block exchange;
+//      xmode 0: block 0 aggregates and publishes per-tile words instead), scans them (DPP) into this
+//      block's tile prefixes, the total b and the rejection flag, and in the common case draws the
+//      resetters' cells and the next state s0' = J_used(J_B(s0)) with one jump chain per lane.
+//      Meanwhile (STG) the env waves list their resetters and write the step's outputs into the LDS
+//      staging area (no global stores during the exchange); without STG they store directly.
+//   3. barrier B2; env waves take their resetters' cells (slow cases: extra check rounds extend the
+//      rejection coverage for mass resets or a second reset call; a rejection anywhere switches to the
+//      exact stream walk, p ~ 1e-8/word) and advance every lane state by J_used.
+//   4. store waves (STG): copy the staged outputs to HBM while the env waves run step 5 and the next
+//      step's VALU-bound transitions.
 // Granule tags = ((global step + 1) * 4 + round) mod 2^15; slots alternate by step parity (a
 // block publishes step t+2 only after every block has published step t+1, i.e. finished
 // reading step t's slots), so a stale granule never carries the expected tag.
