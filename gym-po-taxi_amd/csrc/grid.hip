@@ -855,7 +855,7 @@ __global__ __launch_bounds__(TPB) void grid_reset_init(GridDev p) {
 //   3. barrier B2; env waves take their resetters' cells (slow cases: extra check rounds extend the
 //      rejection coverage for mass resets or a second reset call; a rejection anywhere switches to the
 //      exact stream walk, p ~ 1e-8/word) and advance every lane state by J_used.
-//   4. store waves (STG): copy the staged outputs to HBM while the env waves run step 5 and the next
+//   4. store waves (STG): copy the staged outputs to HBM while the env waves advance and run the next
 //      step's VALU-bound transitions.
 // Granule tags = ((global step + 1) * 4 + round) mod 2^15; slots alternate by step parity (a
 // block publishes step t+2 only after every block has published step t+1, i.e. finished
