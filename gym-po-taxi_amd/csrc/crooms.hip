@@ -216,8 +216,8 @@ __device__ __forceinline__ void write_obs(const CrDev& p, const uint8_t* lds, in
 __device__ __forceinline__ void reset_env(const CrDev& p, const uint8_t* lds, const Draws& d, double& ay, double& ax,
                                           double& vy, double& vx, uint32_t& g) {
   if (!p.goal_fixed) {
-    const int c = tab<uint16_t>(lds, p.off_valid)[d.gi];
-    g = (uint32_t)(c / p.W) | ((uint32_t)(c % p.W) << 16);
+    const uint32_t yx = tab<uint32_t>(lds, p.off_valid)[d.gi];  // y | x << 16: no integer divide
+    g = yx;
   }
   int cy, cx;
   double cs, hs;
@@ -225,8 +225,8 @@ __device__ __forceinline__ void reset_env(const CrDev& p, const uint8_t* lds, co
     cy = p.agent_y; cx = p.agent_x;
     cs = p.cell; hs = p.half_cell;  // grid_to_coord(..., cell_size)
   } else {
-    const int c = tab<uint16_t>(lds, p.off_valid)[d.ai];
-    cy = c / p.W; cx = c % p.W;
+    const uint32_t yx = tab<uint32_t>(lds, p.off_valid)[d.ai];
+    cy = (int)(yx & 0xFFFFu); cx = (int)(yx >> 16);
     cs = 1.0; hs = 0.5;             // the random branch ignores cell_size (crooms.py:240-244)
   }
   ay = (double)cy * cs + hs;
@@ -780,7 +780,10 @@ int CRoomsBackend::build(const gp_crooms_config* cfg) {
   // tables
   std::vector<uint8_t> wall(nc);
   for (int c = 0; c < nc; ++c) wall[c] = cells[c] == -1 ? 1 : 0;  // _out_of_bounds: grid == -1 (:333-338)
-  std::vector<uint16_t> valid(valid_h.begin(), valid_h.end());
+  // valid cells as (y | x << 16) (the goal's own packing), so a reset needs no integer divide
+  std::vector<uint32_t> valid(valid_h.size());
+  for (size_t i = 0; i < valid_h.size(); ++i)
+    valid[i] = (uint32_t)(valid_h[i] / W) | ((uint32_t)(valid_h[i] % W) << 16);
   std::vector<uint64_t> thr;
   if (d.nact) {
     thr.assign((size_t)d.nact * d.nact, 0);
@@ -887,7 +890,7 @@ int CRoomsBackend::build(const gp_crooms_config* cfg) {
   };
   d.off_thr = put(thr.data(), thr.size() * 8);
   d.off_wall = put(wall.data(), wall.size());
-  d.off_valid = put(valid.data(), valid.size() * 2);
+  d.off_valid = put(valid.data(), valid.size() * 4);
   d.off_t1 = put(t1.data(), t1.size() * 4);
   d.off_t2 = put(t2.data(), t2.size() * 4);
   d.off_hbase = put(hbase.data(), hbase.size() * 4);
