@@ -47,6 +47,9 @@ CASES = {
     "rooms_4_hansen8": (RO, dict(layout="4", obs_type="hansen8", time_limit=100), 128, 300, 1, 12, True),
     "rooms_4_grid3": (RO, dict(layout="4", obs_type="grid", time_limit=100), 128, 300, 2, 13, True),
     "rooms_8b_grid5": (RO, dict(layout="8b", obs_type="grid", obs_n=5, time_limit=100), 64, 300, 3, 14, True),
+    "rooms_10b_hansen": (RO, dict(layout="10b", obs_type="hansen", time_limit=120), 64, 300, 21, 22, True),
+    "rooms_16b_vhansen_randgoal": (RO, dict(layout="16b", obs_type="vector_hansen", goal_xy=None, time_limit=150),
+                                   64, 300, 23, 24, True),
     "rooms_16_vgh8": (RO, dict(layout="16", obs_type="vector_goal_hansen8", time_limit=100), 64, 300, 4, 15, True),
     "rooms_4b_room": (RO, dict(layout="4b", obs_type="room", time_limit=100), 64, 300, 5, 16, True),
     "rooms_10_goal_room_randgoal": (RO, dict(layout="10", obs_type="goal_room", goal_xy=None, time_limit=100),
