@@ -66,7 +66,7 @@ WORKLOADS = {
                            "MultistoryFourRoomsEnv(grid_z=1, obs_type='hansen')"),
     "taxi": dict(make=_taxi_onehot, envs=1 << 22, n_actions=5, mode="philox", bytes=4 + 320 + 4 + 1 + 1, state=8,
                  metric="env steps/sec, PO-Taxi 5x5 Hansen one-hot obs (uint8[320]) at 4M envs per GPU",
-                 dtype="uint8", kernel="taxi_rollout<16,false>", chunk=16,
+                 dtype="uint8", kernel="taxi_rollout<16,false>", chunk=4,
                  desc="configs[2]: PO-Taxi 5x5 (TAXI_MAP) Hansen obs one-hot uint8[B,320], {B} envs per GPU, "
                       "HansenTaxiVecEnv(one_hot=True)"),
     "crooms": dict(make=_crooms, envs=1 << 21, n_actions=None, mode="philox", bytes=8 + 8 + 4 + 1 + 1, state=40,
