@@ -71,7 +71,7 @@ WORKLOADS = {
                       "HansenTaxiVecEnv(one_hot=True)"),
     "crooms": dict(make=_crooms, envs=1 << 21, n_actions=None, mode="philox", bytes=8 + 8 + 4 + 1 + 1, state=40,
                    metric="env steps/sec, C-ROOMS layout 4 continuous (y,x) + N(0,0.2) action noise, 2M envs per GPU",
-                   dtype="f64 state / f32 I/O", kernel="crooms_rollout<GP_OBS_F32,false>",
+                   dtype="f64 state / f32 I/O", kernel="crooms_rollout<GP_OBS_F32,false>", chunk=128,
                    desc="configs[4]: C-ROOMS layout 4, yx actions f32 U[-1,1]^2, vector_mdp obs f32[B,2], {B} envs per "
                         "GPU, CRoomsEnv(obs_type='vector_mdp')"),
     "anttag": dict(make=_anttag, envs=1 << 21, n_actions=5, mode="philox", bytes=4 + 16 + 4 + 1 + 1, state=8,
