@@ -2003,7 +2003,9 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
     __builtin_amdgcn_s_setprio(3);  // the exchange is on every step's critical path
     fused_ctrl<OK, QPT, STG>(p, sh, tb, stg, K);
   } else if (wid > FENVW) {
-    __builtin_amdgcn_s_setprio(0);
+    // above the env waves: the store waves issue their few copy instructions right after B2 instead of
+    // trailing the VALU-bound transitions on their SIMD (+6% measured vs priority 0; 2 was no better)
+    __builtin_amdgcn_s_setprio(1);
     fused_store<OK, QPT, STG>(p, sh, tb, stg, K, obs, rew, term, trunc);
   } else {
     fused_env<OK, QPT, NA, STG>(p, sh, s_thr, tb, stg, K, act, obs, rew, term, trunc, rsum, eps, lens, nst);
