@@ -1884,15 +1884,19 @@ __device__ __forceinline__ void stage_plane(const char* src, char* dst, int env_
     // whole aligned tile (the common case): straight-line 16-B copies, immediate offsets
     const u32x4* s4 = reinterpret_cast<const u32x4*>(src) + sl;
     u32x4* d4 = reinterpret_cast<u32x4*>(dst + (size_t)env_base * esz) + sl;
+    // chunks of this plane: FEPB / 4 (4-byte elements) or FEPB / 16 (bytes); lane sl takes sl, sl + NL, ...
+    constexpr int N4 = FEPB / 4, N1 = FEPB / 16;
     if (esz == 4) {
 #pragma unroll
-      for (int j = 0; j < FEPB / 4 / NL; ++j) {
+      for (int j = 0; j < (N4 + NL - 1) / NL; ++j) {
+        if (N4 % NL != 0 && sl + j * NL >= N4) break;
         if (nt) __builtin_nontemporal_store(s4[j * NL], d4 + j * NL);
         else d4[j * NL] = s4[j * NL];
       }
     } else {
 #pragma unroll
-      for (int j = 0; j < FEPB / 16 / NL; ++j) {
+      for (int j = 0; j < (N1 + NL - 1) / NL; ++j) {
+        if (N1 % NL != 0 && sl + j * NL >= N1) break;
         if (nt) __builtin_nontemporal_store(s4[j * NL], d4 + j * NL);
         else d4[j * NL] = s4[j * NL];
       }
