@@ -127,12 +127,30 @@ def measured_hbm_peaks(dev, nbytes=1 << 31, reps=10):
     return out
 
 
+def cpu_model():
+    """`lscpu` model name of this host (reported with the CPU baseline)."""
+    try:
+        import subprocess
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                return line.split(":", 1)[1].strip()
+    except Exception:  # noqa: BLE001
+        pass
+    return None
+
+
 def cpu_baseline(workload="fourrooms", target_s=12.0, procs=None):
     """The numpy oracle (the reference's algorithm restated, fixture-pinned) on the host: one process on one
-    core, then `procs` independent processes (default min(16, cpu_count): the GPU box's CPU share), each on
-    its own 2^16-env batch, summed — the reference run as a CPU-parallel job of independent env batches."""
+    core, then P = os.cpu_count() independent processes, each on its own 2^16-env batch.
+    The aggregate is every process's env-steps over the wall span from the first process's start to the last
+    one's end (so processes that time-share fewer cores than P are not over-counted)."""
     one = _cpu_baseline_1(workload, target_s)
-    procs = procs or min(16, os.cpu_count() or 1)
+    procs = procs or (os.cpu_count() or 1)
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except Exception:  # noqa: BLE001
+        usable = None
     if procs <= 1:
         return one
     import multiprocessing as mp
@@ -141,10 +159,15 @@ def cpu_baseline(workload="fourrooms", target_s=12.0, procs=None):
     with ctx.Pool(procs) as pool:
         res = pool.starmap(_cpu_baseline_1, [(workload, target_s, 1 << 16)] * procs)
     wall = time.perf_counter() - t0
-    agg = sum(r["value"] for r in res)
+    span = max(r["t_end"] for r in res) - min(r["t_start"] for r in res)
+    agg = sum(r["env_steps"] for r in res) / span
     return {"value": agg, "unit": "env-steps/s", "cores": procs, "kind": "port",
-            "sample": f"{procs} processes x ({res[0]['sample']}), summed ({wall:.1f} s wall); "
-                      f"1 process on 2^18 envs: {one['value']:.4g} env-steps/s",
+            "cpu_model": cpu_model(), "cpus_usable": usable,
+            "sample": f"P = os.cpu_count() = {procs} processes (sched affinity: {usable} CPUs) x "
+                      f"({res[0]['sample']}); aggregate = total env-steps / {span:.1f} s span ({wall:.1f} s pool "
+                      f"wall); 1 process on 2^18 envs: {one['value']:.4g} env-steps/s. The oracle is the "
+                      f"reference's numpy step restated (fixture-pinned); per core it runs ~1.5x faster than the "
+                      f"reference itself (SURVEY.md §6: 5.0M vs 3.18M env-steps/s on one core)",
             "value_1core": one["value"]}
 
 
@@ -191,6 +214,7 @@ def _cpu_baseline_1(workload="fourrooms", target_s=12.0, B=1 << 18):
 def _time_oracle(ora, acts, name, B, target_s):
     ora.reset_seed(0)
     ora.step_seeded(acts[0])  # warm
+    t_start = time.time()
     t0 = time.perf_counter()
     n = 0
     while True:
@@ -200,23 +224,39 @@ def _time_oracle(ora, acts, name, B, target_s):
         if dt >= target_s or n >= 400:
             break
     return {"value": B * n / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "env_steps": B * n, "t_start": t_start, "t_end": time.time(),
             "sample": f"{name} (numpy{'' if 'build-defined' in name else ', reference-pinned'}), "
                       f"2^{B.bit_length() - 1} envs x {n} steps, 1 process ({dt:.1f} s)"}
 
 
-def load_pmc(cfg_key, workload):
-    """HBM traffic per launch from profiles/*pmc_*.json (rocprofv3 FETCH_SIZE/WRITE_SIZE passes,
-    tools/pmc_to_json.py), only if collected for the same kernel sources."""
+def load_pmc(cfg_key, workload, steps_per_launch):
+    """HBM traffic per launch of `steps_per_launch` steps from profiles/*pmc_*.json (rocprofv3 FETCH_SIZE /
+    WRITE_SIZE passes, tools/pmc_to_json.py), only from records of the same kernel sources and config.
+    A record at exactly this launch shape is used as is; otherwise, from records at two or more launch
+    shapes, the per-launch traffic T(K) = fixed + per_step * K is fitted (least squares) and evaluated at K.
+    Returns (bytes, source text) or (None, None)."""
     import glob
-    best = None
+    recs = {}
     for fn in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_*.json"))):
         try:
             d = json.load(open(fn))
         except Exception:  # noqa: BLE001
             continue
-        if d.get("src_hash") == src_hash(workload) and d.get("config") == cfg_key:
-            best = d
-    return best
+        if d.get("src_hash") == src_hash(workload) and d.get("config") == cfg_key and d.get("steps_per_launch"):
+            recs[float(d["steps_per_launch"])] = (d["hbm_bytes_per_launch"], os.path.basename(fn))
+    if not recs:
+        return None, None
+    for k, (v, fn) in recs.items():
+        if abs(k - steps_per_launch) < 1e-9:
+            return v, f"{fn} (PMC pass at {k:g} steps per launch)"
+    if len(recs) < 2:
+        return None, None
+    import numpy as np
+    ks = np.array(sorted(recs))
+    ts = np.array([recs[k][0] for k in ks])
+    per_step, fixed = np.polyfit(ks, ts, 1)
+    return float(fixed + per_step * steps_per_launch), (
+        f"fit T(K) = {fixed:.4g} + {per_step:.4g}*K bytes over PMC passes at K = {[float(k) for k in ks]}")
 
 
 def main():
@@ -272,15 +312,17 @@ def main():
     else:
         acts = torch.randint(0, W["n_actions"], (C, B), device=dev, dtype=torch.int32, generator=g)
     out = env._alloc_outputs(C)
+    # prepared launches (validated once, no per-call Python work beyond the C call): full chunks of C steps
+    # and, lazily, the one shorter chunk size a step count not divisible by C needs
+    plans = {C: env.rollout_plan(acts, out)[0]}
 
     def run(n):
         done = 0
         while done < n:
             k = min(C, n - done)
-            if k == C:
-                env.rollout(acts, out=out)
-            else:
-                env.rollout(acts[:k], out=tuple(o[:k] for o in out))
+            if k not in plans:
+                plans[k] = env.rollout_plan(acts[:k], tuple(o[:k] for o in out))[0]
+            plans[k]()
             done += k
 
     def barrier():
@@ -301,7 +343,8 @@ def main():
 
     # live roofline: HIP events bracketing every step-kernel launch on its stream
     env.set_profiling(True)
-    prof_steps = min(max(args.steps // 2, 50), 2000)
+    # whole launches of the timed region's shape (C steps each), so steps_per_launch is exactly C
+    prof_steps = C * max(3, min(2000 // C, max(args.steps // (2 * C), 1)))
     run(prof_steps)
     kms, nk = env.profile_read()
     rms, nr = env.profile_read_resolver()
@@ -321,8 +364,7 @@ def main():
     total_steps = (args.envs if args.strong else B * world) * args.steps
     cfg_key = (f"fourrooms_hansen4_B{B}_{args.mode}" if args.workload == "fourrooms" else
                f"{args.workload}_B{B}_{args.mode}")
-    pmc = load_pmc(cfg_key, args.workload)
-    traffic = pmc["hbm_bytes_per_launch"] if pmc else None
+    traffic, traffic_src = load_pmc(cfg_key, args.workload, steps_per_launch)
     line = {
         "metric": W["metric"],
         "value": total_steps / tmax,
@@ -343,6 +385,8 @@ def main():
                    "parallelism": f"independent env shards x{world}", "steps_per_launch_call": C},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_over_algorithmic": traffic / bytes_per_launch if traffic else None,
+                     "traffic_source": traffic_src,
                      "kernel": W.get("kernel") or (("grid_rollout_numpy<GP_OBS_HANSEN,2,4,true>" if steps_per_launch > 1.5
                                                    else "grid_step_numpy<GP_OBS_HANSEN>") if args.mode == "numpy"
                                                   else "grid_rollout_counter<GP_OBS_HANSEN,false>"),

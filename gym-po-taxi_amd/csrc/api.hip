@@ -329,6 +329,19 @@ int gp_metrics(gp_env* env, double out[4]) {
   return env->be->metrics(out);
 }
 
+int gp_check(gp_env* env) {
+  GP_REQUIRE_ENV();
+  return env->be->check();
+}
+
+int gp_query(const gp_env* env, const char* key, int64_t* value) {
+  if (!env || !env->be || !key || !value) {
+    gp_set_error("gp_query: null argument");
+    return GP_E_INVALID;
+  }
+  return env->be->query(key, value);
+}
+
 int gp_taxi_reset_distribution(const gp_env* env, double* out, int cap) {
   if (!env || !env->be) {
     gp_set_error("null env handle");

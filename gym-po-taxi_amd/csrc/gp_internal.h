@@ -1,5 +1,6 @@
 // gp_internal.h — handle layout shared by the per-kind backends (not part of the C ABI).
 #pragma once
+#include <cstring>
 #include <memory>
 #include <string>
 #include <vector>
@@ -62,6 +63,19 @@ struct EnvBackend {
   }
   virtual int valid_cells(int which, int32_t* out, int cap) const { return 0; }
   virtual int metrics(double out[4]) = 0;
+  // Syncs and reports device-side failures of earlier launches (GP_E_DEVICE); kinds without
+  // cross-block waits have none.
+  virtual int check() { return GP_OK; }
+  // Introspection (gp_query): kernel geometry of this handle.
+  virtual int query(const char* key, int64_t* v) const {
+    if (!strcmp(key, "num_envs")) *v = B;
+    else if (!strcmp(key, "rng_mode")) *v = rng_mode;
+    else {
+      gp_set_error("gp_query: unknown key '%s'", key);
+      return GP_E_INVALID;
+    }
+    return GP_OK;
+  }
   virtual int debug_stamps(unsigned long long* out, int cap) { return 0; }
   virtual int reset_distribution(double* out, int cap) const {
     gp_set_error("no reset distribution for this env kind");

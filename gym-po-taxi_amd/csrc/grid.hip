@@ -32,7 +32,7 @@ namespace {
 constexpr int TPB = 256;
 constexpr int EPT = 4;
 constexpr int EPB = TPB * EPT;
-constexpr uint32_t SPIN_LIMIT = 1u << 24;
+constexpr uint32_t SPIN_LIMIT = 1u << 24;  // default polls before a persistent wait gives up (GP_SPIN_LIMIT)
 constexpr int MAX_TPB2 = 1024;  // max tiles per K2 block (B <= 256 * 1024 * EPB)
 
 struct alignas(64) GridCtl {
@@ -103,12 +103,29 @@ struct GridDev {
   const GridDev* self;      // device copy of this struct (for out-of-line slow-path helpers)
   const PcgJump* jt8;       // [2][256] radix-256 jumps: d and 256*d steps (fused kernel: jumps < 2^16)
   int32_t xmode;            // fused exchange: 0 = block-0 aggregator + per-tile words, 1 = all-gather
+  uint32_t spin_limit;      // polls before a cross-block wait gives up and flags GridCtl::err
+  int32_t fault_block;      // test knob (GP_FAULT_BLOCK): this block never publishes (forces the timeout); -1 off
   // philox / replay
   uint32_t key0, key1;
   const uint64_t* rp_u;
   const int32_t* rp_goal;
   const int32_t* rp_agent;
 };
+
+// ------------------------------------------------------------------ cross-block waits ----
+// Every cross-block wait of the persistent numpy-mode kernels polls through spin_give_up: it gives up
+// after p.spin_limit polls (setting GridCtl::err bit 0, which the host turns into GP_E_DEVICE), and
+// as soon as any other wave has flagged, so that a grid that cannot make progress (blocks not
+// co-resident) still drains: every wave reaches the end of the kernel, the results are flagged invalid.
+__device__ __forceinline__ bool spin_give_up(const GridDev& p, uint32_t& spins) {
+  ++spins;
+  if ((spins & 63u) == 0 && __hip_atomic_load(&p.ctl->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return true;
+  if (spins > p.spin_limit) {
+    atomicOr(&p.ctl->err, 1u);
+    return true;
+  }
+  return false;
+}
 
 // ------------------------------------------------------------------ vector I/O helpers ----
 __device__ __forceinline__ bool full_aligned(const void* p, int env0, int B, int esz) {
@@ -723,7 +740,8 @@ __global__ __launch_bounds__(TPB) void grid_resolve_numpy(GridDev p, void* __res
     }
   }
   const uint32_t myrej = __syncthreads_or((int)rj) ? 1u : 0u;
-  if (threadIdx.x == 0) st_flag32(&p.rflag[blockIdx.x], ((epoch + 1u) << 1) | myrej);
+  if (threadIdx.x == 0 && (int)blockIdx.x != p.fault_block)
+    st_flag32(&p.rflag[blockIdx.x], ((epoch + 1u) << 1) | myrej);
   // wait for every predecessor block's flag (all K2 blocks are resident: gridDim <= 256)
   uint32_t prej = 0;
   for (int j = threadIdx.x; j < (int)blockIdx.x; j += TPB) {
@@ -732,10 +750,7 @@ __global__ __launch_bounds__(TPB) void grid_resolve_numpy(GridDev p, void* __res
     while ((f >> 1) != epoch + 1u) {
       __builtin_amdgcn_s_sleep(1);
       f = ld_flag(&p.rflag[j]);
-      if (++spins > SPIN_LIMIT) {
-        atomicOr(&C->err, 1u);
-        break;
-      }
+      if (spin_give_up(p, spins)) break;
     }
     prej |= f & 1u;
   }
@@ -958,8 +973,7 @@ __device__ __forceinline__ void gather_blocks(const GridDev& p, const uint64_t* 
     for (int j = 0; j < 4; ++j)
       if ((pend & (1u << j)) && (g[j] >> 49) == want) pend &= ~(1u << j);
     if (!__any((int)pend)) break;
-    if (++spins > SPIN_LIMIT) {
-      if (pend) atomicOr(&p.ctl->err, 1u);
+    if (spin_give_up(p, spins)) {  // flagged: the results of this launch are invalid (GP_E_DEVICE)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         if (pend & (1u << j)) g[j] = want << 49;
@@ -1000,7 +1014,7 @@ __device__ __noinline__ uint32_t coverage_round(const GridDev* __restrict__ gp, 
     }
   }
   const uint32_t any = __syncthreads_or((int)r) ? 1u : 0u;
-  if (threadIdx.x == 0)
+  if (threadIdx.x == 0 && (int)blockIdx.x != p.fault_block)
     __hip_atomic_store(&slots[blockIdx.x], bgran(tag, any, 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (wid == FENVW) {  // the control wave
     uint64_t g[4];
@@ -1113,7 +1127,19 @@ __device__ __forceinline__ void publish_next(const LTabs& tb, FusedShared& sh, c
       p_in.dbg[((size_t)blockIdx.x * 64 + k) * 16 + (i)] = t_;                                    \
     }                                                                                             \
   } while (0)
+// launch-level stamps (block, slot): 0 entry, 1 tables staged, 2 step loop done, 3 kernel end
+#define LSTAMP(i)                                                                                 \
+  do {                                                                                            \
+    if (threadIdx.x == 0) {                                                                       \
+      unsigned long long t_;                                                                      \
+      asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");               \
+      p_in.dbg[(size_t)256 * 64 * 16 + (size_t)blockIdx.x * 8 + (i)] = t_;                        \
+    }                                                                                             \
+  } while (0)
 #else
+#define LSTAMP(i) \
+  do {            \
+  } while (0)
 #define RSTAMP(i) \
   do {            \
   } while (0)
@@ -1749,7 +1775,7 @@ __device__ __forceinline__ void fused_ctrl(const GridDev& p_in, FusedShared& sh,
     uint64_t counts = 0;
 #pragma unroll
     for (int q = 0; q < QPT; ++q) counts |= (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)tq, q) << (12 * q);
-    if (lane == 0) {
+    if (lane == 0 && (int)blockIdx.x != p.fault_block) {
       __hip_atomic_store(&slots[blockIdx.x], bgran(tag0, wrej, counts), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       RSTAMP(6);
     }
@@ -1813,8 +1839,7 @@ __device__ __forceinline__ void fused_ctrl(const GridDev& p_in, FusedShared& sh,
         while ((w >> 49) != want) {
           __builtin_amdgcn_s_sleep(1);
           w = __hip_atomic_load(&tw[tau], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (++spins > SPIN_LIMIT) {
-            atomicOr(&p.ctl->err, 1u);
+          if (spin_give_up(p, spins)) {
             w = want << 49;
             break;
           }
@@ -1981,6 +2006,7 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
   extern __shared__ __attribute__((aligned(16))) char dyn[];
   const GridDev& p = p_in;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  LSTAMP(0);
   if (tid < NA * NA) s_thr[tid] = p.thr[tid];
   // stage the lookup tables in LDS (the fused path is only taken when they fit)
   lds_copy(dyn, p.lds.move, p.move);
@@ -2001,6 +2027,7 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
   const LTabs tb{p_in, dyn};
   char* stg = dyn + p.lds.total;  // output staging (STG): after the tables, 16-B aligned
   __syncthreads();
+  LSTAMP(1);
   float rsum = 0.f;
   uint32_t eps = 0, lens = 0, nst = 0;
   if (wid == FENVW) {
@@ -2014,6 +2041,7 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
   } else {
     fused_env<OK, QPT, NA, STG>(p, sh, s_thr, tb, stg, K, act, obs, rew, term, trunc, rsum, eps, lens, nst);
   }
+  LSTAMP(2);
   // metrics (the control wave contributes zeros)
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) {
@@ -2035,6 +2063,7 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
     m.length_sum += l;
     m.env_steps += n;
   }
+  LSTAMP(3);
 }
 
 // ------------------------------------------------------------------ kernels: counter modes ----
@@ -2231,6 +2260,16 @@ struct GridBackend : EnvBackend {
     return upload_rng();
   }
   int get_rng_state(RngHost* r) override;
+  int check() override;
+  int device_error(uint32_t flags);
+  int query(const char* key, int64_t* v) const override {
+    if (!strcmp(key, "fused_blocks")) *v = fused_G;
+    else if (!strcmp(key, "fused_tiles_per_block")) *v = fused_qpt;
+    else if (!strcmp(key, "fused_staged")) *v = fused_stg ? 1 : 0;
+    else if (!strcmp(key, "fused_tile_envs")) *v = FEPB;
+    else return EnvBackend::query(key, v);
+    return GP_OK;
+  }
   int reset(void* obs, hipStream_t s) override;
   int step(const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc, hipStream_t s) override;
   int rollout(int K, const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc, hipStream_t s) override;
@@ -2266,7 +2305,7 @@ struct GridBackend : EnvBackend {
 #ifdef GP_STAMPS
   int debug_stamps(unsigned long long* out, int cap) override {
     GP_HIP_CHECK(hipDeviceSynchronize());
-    const int n = std::min(cap, 256 * 64 * 16);
+    const int n = std::min(cap, 256 * 64 * 16 + 256 * 8);
     GP_HIP_CHECK(hipMemcpy(out, d.dbg, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost));
     return n;
   }
@@ -2319,6 +2358,7 @@ int GridBackend::upload_rng() {
   c.inc_lo = lo64(rng.inc);
   c.has_u32 = rng.has_u32;
   c.uinteger = rng.uinteger;
+  c.err = 0;  // a new stream position: earlier device errors no longer apply
   GP_HIP_CHECK(hipMemcpy(d.ctl, &c, sizeof(c), hipMemcpyHostToDevice));
   std::vector<PcgJump> jt = build_jump_tables(rng.inc);
   GP_HIP_CHECK(hipMemcpy(b_jt.p, jt.data(), jt.size() * sizeof(PcgJump), hipMemcpyHostToDevice));
@@ -2375,11 +2415,21 @@ int GridBackend::get_rng_state(RngHost* r) {
   r->inc = mk128(c.inc_hi, c.inc_lo);
   r->has_u32 = c.has_u32;
   r->uinteger = c.uinteger;
-  if (c.err) {
-    gp_set_error("device error flags 0x%x (spin timeout)", c.err);
-    return GP_E_HIP;
-  }
+  if (c.err) return device_error(c.err);
   return GP_OK;
+}
+
+int GridBackend::device_error(uint32_t flags) {
+  gp_set_error("device error flags 0x%x: a persistent kernel's cross-block wait timed out (blocks not co-resident?); "
+               "the outputs and env state since the last seed are invalid (reseed to clear)", flags);
+  return GP_E_DEVICE;
+}
+
+int GridBackend::check() {
+  GP_HIP_CHECK(hipDeviceSynchronize());
+  uint32_t err = 0;
+  GP_HIP_CHECK(hipMemcpy(&err, &d.ctl->err, sizeof(err), hipMemcpyDeviceToHost));
+  return err ? device_error(err) : GP_OK;
 }
 
 int GridBackend::metrics(double out[4]) {
@@ -2393,7 +2443,7 @@ int GridBackend::metrics(double out[4]) {
     out[2] += (double)x.length_sum;
     out[3] += (double)x.env_steps;
   }
-  return GP_OK;
+  return check();
 }
 
 template <class F>
@@ -2770,6 +2820,11 @@ int GridBackend::build(const gp_grid_config* cfg) {
     // bits 0-1: 1 = every block all-gathers the granules (default), 0 = block-0 aggregator; bit 4: plain
     // (not non-temporal) staged output stores; bits 2-3 (stamps builds only): output-store diagnostics
     d.xmode = xm ? atoi(xm) : 1;
+    // test knobs: a short spin limit and a block that never publishes force the device-error path
+    const char* sl = getenv("GP_SPIN_LIMIT");
+    d.spin_limit = sl && atol(sl) > 0 ? (uint32_t)atol(sl) : SPIN_LIMIT;
+    const char* fb = getenv("GP_FAULT_BLOCK");
+    d.fault_block = fb ? atoi(fb) : -1;
   }
   {
     hipDeviceProp_t prop;
@@ -2835,7 +2890,7 @@ int GridBackend::build(const gp_grid_config* cfg) {
   d.fjB = b_fjB.as<PcgJump>();
   d.fslot = b_fslot.as<uint64_t>();
 #ifdef GP_STAMPS
-  if ((e = b_dbg.alloc(sizeof(unsigned long long) * 256 * 64 * 16))) return e;
+  if ((e = b_dbg.alloc(sizeof(unsigned long long) * (256 * 64 * 16 + 256 * 8)))) return e;
   d.dbg = b_dbg.as<unsigned long long>();
 #endif
   if ((e = b_self.alloc(sizeof(GridDev))) || (e = b_jt8.alloc(sizeof(PcgJump) * 2 * 256))) return e;

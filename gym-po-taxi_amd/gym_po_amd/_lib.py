@@ -10,6 +10,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GYM_PO_AMD_LIB", os.path.join(_HERE, "libgympo_amd.so"))
 
 GP_OK = 0
+GP_E_DEVICE = -5
 GP_KIND_GRID, GP_KIND_TAXI, GP_KIND_CROOMS, GP_KIND_ANTTAG = 1, 2, 3, 4
 GP_RNG_NUMPY, GP_RNG_PHILOX, GP_RNG_REPLAY = 0, 1, 2
 RNG_MODES = {"numpy": GP_RNG_NUMPY, "philox": GP_RNG_PHILOX, "replay": GP_RNG_REPLAY}
@@ -82,6 +83,8 @@ SIGNATURES = {
     "gp_set_replay": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
     "gp_valid_cells": (ctypes.c_int, [_vp, ctypes.c_int, _i32p, ctypes.c_int]),
     "gp_metrics": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double)]),
+    "gp_check": (ctypes.c_int, [_vp]),
+    "gp_query": (ctypes.c_int, [_vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)]),
     "gp_taxi_reset_distribution": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
     "gp_set_profiling": (ctypes.c_int, [_vp, ctypes.c_int]),
     "gp_profile_read": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]),

@@ -166,19 +166,73 @@ class NativeVecEnv:
     def rollout(self, actions, out=None):
         """K steps in one call: actions [K, B(,2)] -> obs [K, B, ...], rew/term/trunc [K, B].
 
-        Philox mode runs the K steps in ONE fused launch (state in registers); numpy/replay
-        modes issue K step launches on the stream. `out` may supply preallocated buffers
-        (obs, rew, term(uint8), trunc(uint8))."""
+        Philox mode, and numpy mode on the grid envs (persistent kernel with a per-step grid
+        exchange), run the K steps in ONE fused launch with the env state in registers; replay
+        mode issues K step launches on the stream. `out` may supply preallocated buffers
+        (obs, rew, term(uint8), trunc(uint8)) shaped like `_alloc_outputs(K)`: they are checked
+        for shape, dtype, device and contiguity (ValueError otherwise)."""
         torch = _torch()
         K = int(actions.shape[0])
         a = self._as_actions(actions, K)
         if out is None:
             out = self._alloc_outputs(K)
+        else:
+            self._check_out(out, K)
         obs, rew, term, trunc = out
         check(lib().gp_rollout(self._handle, K, ctypes.c_void_p(a.data_ptr()), ctypes.c_void_p(obs.data_ptr()),
                                ctypes.c_void_p(rew.data_ptr()), ctypes.c_void_p(term.data_ptr()),
                                ctypes.c_void_p(trunc.data_ptr()), self._stream()), "gp_rollout")
         return self._post_obs(obs), rew, term.view(torch.bool), trunc.view(torch.bool)
+
+    def _check_out(self, out, K):
+        torch = _torch()
+        if not isinstance(out, (tuple, list)) or len(out) != 4:
+            raise ValueError("out must be (obs, rew, term, trunc)")
+        want = (((K,) + self._obs_shape(), self._obs_dtype), ((K, self.num_envs), torch.float32),
+                ((K, self.num_envs), torch.uint8), ((K, self.num_envs), torch.uint8))
+        for name, t, (shape, dt) in zip(("obs", "rew", "term", "trunc"), out, want):
+            if not isinstance(t, torch.Tensor):
+                raise ValueError(f"out {name}: expected a torch tensor")
+            if tuple(t.shape) != shape or t.dtype != dt or t.device != self.device or not t.is_contiguous():
+                raise ValueError(f"out {name}: need a contiguous {dt} tensor of shape {shape} on {self.device}, got "
+                                 f"{t.dtype} {tuple(t.shape)} on {t.device} (contiguous={t.is_contiguous()})")
+
+    def rollout_plan(self, actions, out=None):
+        """A prepared K-step rollout: validates `actions` [K, B(,2)] (already the env's action dtype, on its
+        device, contiguous) and the output buffers once, and returns a callable that enqueues the K steps on
+        the stream current at plan time (or the hipStream_t handle it is given) with no further Python work (the agent loop's allocation-free hot path; the
+        buffers are reused by every call). Returns (run, (obs, rew, term, trunc))."""
+        torch = _torch()
+        K = int(actions.shape[0])
+        a = self._as_actions(actions, K)
+        if a.data_ptr() != actions.data_ptr():
+            raise ValueError("rollout_plan: actions must already be a contiguous device tensor of the action dtype")
+        if out is None:
+            out = self._alloc_outputs(K)
+        else:
+            self._check_out(out, K)
+        fn, h = lib().gp_rollout, self._handle
+        args = [ctypes.c_void_p(x.data_ptr()) for x in (a,) + tuple(out)]
+        stream0 = torch.cuda.current_stream(self.device).cuda_stream
+        keep = (a, out)
+
+        def run(stream=None):
+            rc = fn(h, K, *args, stream0 if stream is None else stream)
+            if rc:
+                check(rc, "gp_rollout")
+            return keep
+        return run, (out[0], out[1], out[2].view(torch.bool), out[3].view(torch.bool))
+
+    def check(self):
+        """Sync and raise GymPoError if a device-side failure hit any launch since the last seed (the
+        asynchronous step/rollout calls cannot report it themselves; metrics() and rng_state check too)."""
+        check(lib().gp_check(self._handle), "gp_check")
+
+    def query(self, key):
+        """Handle introspection (gp_query), e.g. 'fused_blocks', 'fused_staged'."""
+        v = ctypes.c_int64()
+        check(lib().gp_query(self._handle, key.encode(), ctypes.byref(v)), "gp_query")
+        return v.value
 
     def step_raw(self, a, obs, rew, term, trunc, stream=None):
         """Allocation-free step into caller buffers (all device tensors; term/trunc uint8)."""
@@ -211,7 +265,8 @@ class NativeVecEnv:
         return np.array(buf[:n], dtype=np.int64)
 
     def metrics(self):
-        """{episodes, return_sum, length_sum, env_steps} accumulated on device since reset (syncs)."""
+        """{episodes, return_sum, length_sum, env_steps} accumulated on device since reset (syncs; raises
+        GymPoError if a device-side failure invalidated the run, see check())."""
         out = (ctypes.c_double * 4)()
         check(lib().gp_metrics(self._handle, out), "gp_metrics")
         return dict(episodes=out[0], return_sum=out[1], length_sum=out[2], env_steps=out[3])

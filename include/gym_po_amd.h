@@ -44,6 +44,10 @@ extern "C" {
 #define GP_E_HIP (-2)       /* HIP runtime error                                         */
 #define GP_E_UNSUPPORTED (-3)/* mode not available for this env kind                     */
 #define GP_E_STATE (-4)     /* call order (e.g. step before reset)                       */
+#define GP_E_DEVICE (-5)    /* a device-side failure of an earlier asynchronous launch (a persistent
+                               kernel's cross-block wait timed out): outputs and env state since the
+                               last seed are invalid; reported by gp_check / gp_metrics /
+                               gp_get_rng_state, cleared by reseeding                          */
 
 /* ---- env kinds ---- */
 #define GP_KIND_GRID 1   /* FourRooms (multistory) and ROOMS: discrete cell gridworlds */
@@ -172,8 +176,9 @@ int gp_reset(gp_env* env, void* obs, void* stream);
 int gp_step(gp_env* env, const void* actions, void* obs, float* rew, uint8_t* term, uint8_t* trunc,
             void* stream);
 
-/* K consecutive steps. actions [K,B(,2)], outputs [K,B,...]. Philox mode fuses the K steps in
- * one launch with the state in registers; numpy/replay modes issue K step launches. */
+/* K consecutive steps. actions [K,B(,2)], outputs [K,B,...]. Philox mode, and numpy mode on GRID
+ * (persistent kernel with a per-step grid exchange; 16-B aligned buffers, B % 4 == 0), fuse the K
+ * steps in one launch with the state in registers; other cases issue K step launches. */
 int gp_rollout(gp_env* env, int K, const void* actions, void* obs, float* rew, uint8_t* term, uint8_t* trunc,
                void* stream);
 
@@ -198,6 +203,16 @@ int gp_valid_cells(const gp_env* env, int which, int32_t* out, int cap);
  * length_sum, env_steps}. */
 int gp_metrics(gp_env* env, double out[4]);
 
+/* Syncs the handle's device and returns GP_E_DEVICE if any launch since the last seed failed on the
+ * device (numpy-mode GRID: a persistent kernel's cross-block wait timed out), else GP_OK. The
+ * asynchronous step/rollout calls cannot report such failures themselves; gp_metrics and
+ * gp_get_rng_state run the same check. (No reference counterpart: numpy steps are synchronous.) */
+int gp_check(gp_env* env);
+/* Introspection of a handle (host-only, no sync): key = "num_envs", "rng_mode", and for GRID
+ * "fused_blocks" (persistent grid size of the fused numpy rollout, 0 = not eligible),
+ * "fused_tiles_per_block", "fused_staged" (1 = LDS-staged outputs + store waves),
+ * "fused_tile_envs". Unknown keys return GP_E_INVALID. */
+int gp_query(const gp_env* env, const char* key, int64_t* value);
 /* Device-side start-state law of TAXI resets (host copy): P(state index k) over valid states. */
 int gp_taxi_reset_distribution(const gp_env* env, double* out, int cap);
 

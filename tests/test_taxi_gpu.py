@@ -48,7 +48,10 @@ def run_replay(kw, B, seed, acts, env=None, check=None):
     o_ref = ora.reset_seed(seed)
     env.set_replay(reset_states=ora.s.astype(np.int32))
     o, _ = env.reset()
-    np.testing.assert_array_equal(_np(o).astype(np.int64), np.asarray(o_ref).astype(np.int64))
+    o_ref = np.asarray(o_ref).astype(np.int64)
+    if env.one_hot:
+        o_ref = np.eye(env.no, dtype=np.int64)[o_ref]
+    np.testing.assert_array_equal(_np(o).astype(np.int64), o_ref)
     lpl = ora.nlocs * (ora.nlocs + 1)
     for t in range(acts.shape[0]):
         ro, rr, rd, rt = ora.step_seeded(acts[t])
@@ -207,3 +210,51 @@ def test_philox_passenger_destination_law(gpu_device):
     off = counts[~np.eye(L, dtype=bool)].astype(np.float64)
     assert _chi2_p(off, np.full(off.size, 1.0 / off.size)) > 1e-4
     assert int(_np(env.get_state()[2]).min()) == 1
+
+
+@pytest.mark.parametrize("name", ["taxi_hansen_b64", "taxi_ext_hansen"])
+def test_one_hot_replay_bit_exact_vs_reference_fixture(name, gpu_device):
+    """configs[2]'s one-hot encoding pinned to the reference: row t of the one-hot obs == eye(n_obs)[the
+    reference's Hansen obs] at every step (extended_taxi.py:366-372 gives the index; one-hot is the build's
+    encoding of it)."""
+    meta, data = load_case(name)
+    kw = dict(meta["kwargs"])
+    assert kw.get("hansen_obs")
+    acts = step_actions(meta)
+    env = make_env(kw, meta["num_envs"], rng_mode="replay", one_hot=True)
+    eye = np.eye(env.no, dtype=np.uint8)
+    for t, ref, got, ora, env in run_replay(kw, meta["num_envs"], meta["seed"], acts, env=env):
+        o, r, d, tr = got
+        np.testing.assert_array_equal(o, eye[data["obs"][t].astype(np.int64)], err_msg=f"t={t}")
+        np.testing.assert_array_equal(r, data["rew"][t], err_msg=f"t={t}")
+        np.testing.assert_array_equal(d.astype(bool), data["term"][t], err_msg=f"t={t}")
+        np.testing.assert_array_equal(tr.astype(bool), data["trunc"][t], err_msg=f"t={t}")
+
+
+def test_one_hot_4m_envs_rollout_properties(gpu_device):
+    """configs[2] at full size (2^22 envs, one-hot uint8[B, 320], the bench's 4-step launches): every row is
+    one-hot, its index equals the scalar Hansen obs of a same-seed scalar env, and the start states follow
+    the exact argmax-multinomial reset law (chi-square)."""
+    import torch
+    from gym_po_amd import HansenTaxiVecEnv
+    B, K = 1 << 22, 4
+    a = HansenTaxiVecEnv(B, device=gpu_device, rng_mode="philox")
+    b = HansenTaxiVecEnv(B, device=gpu_device, rng_mode="philox", one_hot=True)
+    oa, _ = a.reset(seed=21)
+    ob, _ = b.reset(seed=21)
+    assert ob.shape == (B, 320) and ob.dtype == torch.uint8
+    assert torch.equal(ob.sum(-1, dtype=torch.int32), torch.ones(B, dtype=torch.int32, device=gpu_device))
+    assert torch.equal(ob.argmax(-1).to(torch.int32), oa.to(torch.int32))
+    s = _np(b.get_state()[0])
+    law = b.reset_distribution
+    idx = np.searchsorted(b.valid_states, s)
+    assert np.array_equal(b.valid_states[idx], s), "reset into an invalid state"
+    assert _chi2_p(np.bincount(idx, minlength=len(law)).astype(np.float64), law) > 1e-4
+    acts = torch.randint(0, 5, (K, B), dtype=torch.int32, device=gpu_device)
+    oa, ra, da, ta = a.rollout(acts)
+    ob, rb, db, tb = b.rollout(acts)
+    for k in range(K):
+        assert torch.equal(ob[k].sum(-1, dtype=torch.int32), torch.ones(B, dtype=torch.int32, device=gpu_device))
+        assert torch.equal(ob[k].argmax(-1).to(torch.int32), oa[k].to(torch.int32))
+    assert torch.equal(ra, rb) and torch.equal(da, db) and torch.equal(ta, tb)
+    assert int(oa.min()) >= 0 and int(oa.max()) < 320

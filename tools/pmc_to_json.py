@@ -1,6 +1,10 @@
 """Turn rocprofv3 FETCH_SIZE / WRITE_SIZE passes into profiles/pmc_<config>.json for bench.py.
 
-    python tools/pmc_to_json.py <pmc_root> <kernel_substring> <config_key> <out.json> <workload>
+    python tools/pmc_to_json.py <pmc_root> <kernel_substring> <config_key> <out.json> <workload> <steps_per_launch>
+
+Every profiled dispatch must have the same launch shape (run bench.py with --chunk C and --steps/--warmup
+multiples of C): the record is keyed on steps_per_launch, and bench.py only reuses it for lines of that
+shape (or fits T(K) = fixed + per_step*K over records at several shapes).
 
 Per MI355X_MICROARCH.md (HBM section): FETCH_SIZE / WRITE_SIZE are in KiB per dispatch; on gfx950
 FETCH_SIZE reports half of the bytes of a wide coalesced streaming read, so it is doubled.
@@ -14,6 +18,7 @@ import os
 import sys
 
 root, pat, cfg, out, workload = sys.argv[1:6]
+steps_per_launch = float(sys.argv[6])
 vals = {"FETCH_SIZE": [], "WRITE_SIZE": []}
 for fn in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
     with open(fn) as f:
@@ -30,6 +35,7 @@ with open(os.path.join(here, "gym-po-taxi_amd", "gym_po_amd", "libgympo_amd.so")
 sys.path.insert(0, here)
 import bench  # noqa: E402
 d = {"config": cfg, "kernel": pat, "lib_hash": h, "src_hash": bench.src_hash(workload),
+     "steps_per_launch": steps_per_launch,
      "dispatches": {"FETCH_SIZE": len(vals["FETCH_SIZE"]), "WRITE_SIZE": len(vals["WRITE_SIZE"])},
      "fetch_size_kib_raw": fetch_kib, "write_size_kib_raw": write_kib,
      "hbm_bytes_per_launch": (2.0 * fetch_kib + write_kib) * 1024.0,

@@ -18,7 +18,7 @@ import torch  # noqa: E402
 from gym_po_amd import MultistoryFourRoomsEnv, _lib  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
-K = 64
+K = int(sys.argv[2]) if len(sys.argv) > 2 else 64
 env = MultistoryFourRoomsEnv(B, 1, obs_type="hansen")
 env.reset(seed=0)
 acts = torch.randint(0, 4, (K, B), device="cuda", dtype=torch.int32)
@@ -29,10 +29,31 @@ L = _lib.lib()
 fn = L.gp_debug_stamps
 fn.restype = ctypes.c_int
 fn.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
-buf = (ctypes.c_ulonglong * (256 * 64 * 16))()
-n = fn(env._handle, buf, 256 * 64 * 16)
-a = np.frombuffer(buf, dtype=np.uint64).reshape(256, 64, 16).astype(np.int64)
-G = min(256, (B + 2047) // 2048)
+NS = 256 * 64 * 16
+buf = (ctypes.c_ulonglong * (NS + 256 * 8))()
+n = fn(env._handle, buf, NS + 256 * 8)
+raw = np.frombuffer(buf, dtype=np.uint64).astype(np.int64)
+a = raw[:NS].reshape(256, 64, 16)
+G = int(env.query("fused_blocks"))
+# launch-level view of the last launch: entry, tables staged, step loop done, kernel end (per block)
+L4 = raw[NS:].reshape(256, 8)[:G, :4] * 10
+t0 = L4[:, 0].min()
+print(f"launch (K={K}, G={G}): entry spread {L4[:, 0].max() - t0} ns; entry->tables staged median "
+      f"{np.median(L4[:, 1] - L4[:, 0]):.0f} max {np.max(L4[:, 1] - L4[:, 0])} ns; first entry -> last staged "
+      f"{L4[:, 1].max() - t0} ns")
+s0 = a[:G, 0, 0] * 10
+print(f"  first entry -> step 0 start: min {s0.min() - t0} max {s0.max() - t0} ns; "
+      f"loop done -> kernel end median {np.median(L4[:, 3] - L4[:, 2]):.0f} max {np.max(L4[:, 3] - L4[:, 2])} ns")
+print(f"  first entry -> last kernel end {L4[:, 3].max() - t0} ns = {(L4[:, 3].max() - t0) / K:.0f} ns/step; "
+      f"last step start -> last loop done {L4[:, 2].max() - (a[:G, min(K, 64) - 1, 0] * 10).max()} ns")
+env.set_profiling(True)
+for _ in range(5):
+    env.rollout(acts)
+ms, nk = env.profile_read()
+env.set_profiling(False)
+print(f"  event-timed kernel: {ms / nk * 1e3:.1f} us per launch of K={K} ({ms / nk / K * 1e6:.0f} ns/step)")
+if K < 8:
+    sys.exit(0)
 a = a[:G, 2:K - 2] * 10  # ns
 def rep(name, d):
     per_step_max = d.max(0)
