@@ -22,6 +22,11 @@ import os
 import sys
 import time
 
+# Kernel arguments in device memory (a HIP runtime setting, read when HIP initialises: set before torch loads).
+# The fused kernel's parameter block is ~600 B; where the runtime keeps kernel arguments in host memory,
+# every wave of the 256 persistent blocks reads them across PCIe at launch: +1.5-8 µs per launch, by box
+# (DESIGN.md §5). An explicit setting in the environment wins.
+os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "gym-po-taxi_amd"))
 sys.path.insert(0, ROOT)
@@ -312,6 +317,8 @@ def main():
     else:
         acts = torch.randint(0, W["n_actions"], (C, B), device=dev, dtype=torch.int32, generator=g)
     out = env._alloc_outputs(C)
+    for o in out:  # first touch at allocation, not inside the timed region
+        o.zero_()
     # prepared launches (validated once, no per-call Python work beyond the C call): full chunks of C steps
     # and, lazily, the one shorter chunk size a step count not divisible by C needs
     plans = {C: env.rollout_plan(acts, out)[0]}
