@@ -242,6 +242,10 @@ struct LTabs {
     return reinterpret_cast<const T*>(dyn + t.off)[i];
   }
   __device__ __forceinline__ uint16_t move(int i) const { return at<uint16_t>(p.lds.move, i); }
+  // move-table entry at byte offset `b` (= (cell * NA + action) * 2)
+  __device__ __forceinline__ uint16_t move_b(uint32_t b) const {
+    return *reinterpret_cast<const uint16_t*>(dyn + p.lds.move.off + b);
+  }
   __device__ __forceinline__ uint32_t hbase(int i) const { return at<uint32_t>(p.lds.hbase, i); }
   __device__ __forceinline__ int32_t doff(int i) const { return at<int32_t>(p.lds.doff, i); }
   __device__ __forceinline__ uint8_t hvec(int i) const { return at<uint8_t>(p.lds.hvec, i); }
@@ -893,6 +897,25 @@ constexpr int R_ENV = 0, R_CTRL = 1, R_PASS = 2;  // fused_resets roles: env wav
 template <int OK, int QPT>
 constexpr bool fused_staged() { return QPT <= 2 && (OK == GP_OBS_HANSEN || OK == GP_OBS_TABLE); }
 constexpr uint32_t TAG_MASK = 0x7FFFu;
+// Tuning switches of the fused kernel (A/B builds: tools/build_variant.sh):
+//  GP_TRIMS 1: VALU trims of the transitions (thresholds pre-shifted so the full 64-bit draw is compared,
+//    actions turned into threshold-row offsets while waiting at B2).
+//  GP_ALIGNBIT 1: the draw's 64-bit rotate as two v_alignbit_b32.
+//  GP_ACC 1: the episode statistics from the step's masks (popcounts) and, for the episode lengths, from
+//    the elapsed counters at the launch's start and end, instead of per-env accumulations.
+#ifndef GP_TRIMS
+#define GP_TRIMS 1
+#endif
+#ifndef GP_ACC
+#define GP_ACC 1
+#endif
+//  GP_VPIN 1: the stream increment and the goal-direction offsets pinned to VGPRs (SGPR pressure).
+#ifndef GP_VPIN
+#define GP_VPIN 1
+#endif
+#ifndef GP_ALIGNBIT
+#define GP_ALIGNBIT 0
+#endif
 
 struct FusedShared {
   uint32_t wcnt[FMAXQ][FENVW];   // per-env-wave reset counts of each tile
@@ -1444,6 +1467,59 @@ __device__ __forceinline__ void fused_resets(const GridDev& p, FusedShared& sh, 
 // form of action_utils.py:84-90 with the reference's cumsum thresholds). The thresholds of a row are
 // non-decreasing (a cumulative sum), so the count is the first j with k <= thr[j]: NA - 1 compares as a
 // select chain (the last threshold never matters: k > thr[NA-2] already gives NA - 1 after the clamp).
+// A (uniform) value pinned to a VGPR: the opaque move keeps the compiler from re-materialising it in the
+// SGPR file, whose pressure spills values to VGPR lanes in the fused loop.
+__device__ __forceinline__ uint32_t vgpr_u32(uint32_t x) {
+#if GP_VPIN
+  uint32_t v;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "v"(x));
+  return v;
+#else
+  return __builtin_amdgcn_readfirstlane(x);
+#endif
+}
+__device__ __forceinline__ int32_t vgpr_u32(int32_t x) { return (int32_t)vgpr_u32((uint32_t)x); }
+
+// PCG64 XSL-RR output with the 64-bit rotate as two v_alignbit_b32 (same value as pcg_output).
+__device__ __forceinline__ uint64_t pcg_output_ab(u128 s) {
+  const uint64_t hi = hi64(s), lo = lo64(s);
+  const uint32_t xh = (uint32_t)(hi >> 32) ^ (uint32_t)(lo >> 32), xl = (uint32_t)hi ^ (uint32_t)lo;
+  const uint32_t r = (uint32_t)(hi >> 58);
+  const bool sw = (r & 32u) != 0;  // a rotate by >= 32 first swaps the halves
+  const uint32_t H = sw ? xl : xh, L = sw ? xh : xl;
+  const uint32_t olo = __builtin_amdgcn_alignbit(H, L, r), ohi = __builtin_amdgcn_alignbit(L, H, r);
+  return ((uint64_t)ohi << 32) | olo;
+}
+// A 53-bit threshold t as a threshold on the full 64-bit draw x: (x >> 11) > t  <=>  x > (t << 11) | 0x7FF
+// (t >= 2^53, a cumulative sum of 1.0, is never exceeded: saturate).
+__device__ __forceinline__ uint64_t thr_on_u64(uint64_t t) {
+  return t >= (1ull << 53) ? ~0ull : ((t << 11) | 0x7FFull);
+}
+// Sanitised action -> byte offset of its threshold row in s_thr (numpy negative indexing; out-of-range
+// actions, which raise in the reference, are clamped).
+template <int NA>
+__device__ __forceinline__ int32_t action_row(int32_t a) {
+  if (a < 0) a += NA;
+  return min(max(a, 0), NA - 1) * NA * 8;
+}
+// Effective action x 2 (the byte offset of its entry in a move-table row) from the 64-bit draw x and the
+// pre-shifted thresholds of row `boff` (16-B loads: rows are 32/64-B aligned).
+template <int NA>
+__device__ __forceinline__ uint32_t fused_effx_row(const uint64_t* s_thr, int boff, uint64_t x) {
+  const ulonglong2* t = reinterpret_cast<const ulonglong2*>(reinterpret_cast<const char*>(s_thr) + boff);
+  uint64_t th[NA];
+#pragma unroll
+  for (int j = 0; j < NA / 2; ++j) {
+    const ulonglong2 v = t[j];
+    th[2 * j] = v.x;
+    th[2 * j + 1] = v.y;
+  }
+  uint32_t e = 0;
+#pragma unroll
+  for (int j = 0; j < NA - 1; ++j) e = x > th[j] ? (uint32_t)(2 * (j + 1)) : e;
+  return e;
+}
+
 template <int NA>
 __device__ __forceinline__ uint32_t fused_effective_action(const uint64_t* s_thr, int a, uint64_t k) {
   const uint64_t* t = s_thr + a * NA;
@@ -1495,12 +1571,15 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
   const uint32_t step_base = C->step;
   const size_t ow = (size_t)p.obs_width * ((OK == GP_OBS_HANSEN_VEC || OK == GP_OBS_WINDOW) ? 1 : 4);
   const PcgJump jB_unused{0, 1, 0, 0};
+  constexpr bool TRIMS = GP_TRIMS;
   uint32_t ae[QPT][4];
   int gl[QPT][4];
-  int32_t a_cur[QPT][4];
+  int32_t a_cur[QPT][4];  // TRIMS: threshold-row byte offsets (action_row) instead of raw actions
+  // GP_ACC: valid-env masks (partial tiles), goal / wall-bump counts; rewards and lengths at the end
+  uint32_t vmask[QPT], ngoal = 0, nwall = 0;
   u128 S[QPT];  // lane draw state: jump(s0, e0 + 1)
   uint32_t pc[QPT][4], pfm[QPT];  // previous step's resetters: new cells (goal | agent << 16), masks
-  int dof[8];                     // goal-direction offsets (wave-uniform) for the staged Hansen obs
+  int dof[8];                     // goal-direction offsets (uniform, in VGPRs) for the staged Hansen obs
   const PcgJump jl = p.flt4[tid];
   PcgJump jtile[QPT];
 #pragma unroll
@@ -1519,11 +1598,28 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
       for (int i = 0; i < 4; ++i) gl[q][i] = fixed_goal;
     }
     load4f<int32_t>(act, env0, B, a_cur[q]);
+    if constexpr (TRIMS) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a_cur[q][i] = action_row<NA>(a_cur[q][i]);
+    }
     jtile[q] = p.ftj[min(tau, nt - 1)];
+    vmask[q] = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) vmask[q] |= (STG || env0 + i < B) ? 1u << i : 0u;
+    if constexpr (GP_ACC) {
+      // episode lengths ended in this launch = steps taken + elapsed at the start - elapsed at the end
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if ((vmask[q] >> i) & 1u) lens += ae[q][i] >> 16;
+    }
   }
 #pragma unroll
   for (int d = 0; d < 8; ++d)
-    dof[d] = (OK == GP_OBS_HANSEN && d < p.obs_dirs) ? __builtin_amdgcn_readfirstlane(tb.doff(d)) : 0x7FFFFFFF;
+    dof[d] = (OK == GP_OBS_HANSEN && d < p.obs_dirs) ? vgpr_u32(tb.doff(d)) : 0x7FFFFFFF;
+  // The stream increment as VGPR operands: uniform, but SGPRs are the scarce file in this loop (kept there,
+  // it was spilled to VGPR lanes and re-read by v_readlane + v_mov in every draw).
+  const u128 incv = mk128(((uint64_t)vgpr_u32((uint32_t)(hi64(st.inc) >> 32)) << 32) | vgpr_u32((uint32_t)hi64(st.inc)),
+                          ((uint64_t)vgpr_u32((uint32_t)(lo64(st.inc) >> 32)) << 32) | vgpr_u32((uint32_t)lo64(st.inc)));
 #pragma unroll
   for (int q = 0; q < QPT; ++q) S[q] = apply_jump(compose_jump(jl, jtile[q]), st.s0);
   for (int k = 0; k < K; ++k) {
@@ -1553,16 +1649,22 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
       u128 s = S[q];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        if (i) s = pcg_step(s, st.inc);
-        const uint64_t k53 = pcg_output(s) >> 11;
-        int a = a_cur[q][i];
-        if (a < 0) a += NA;                 // numpy negative indexing of action_matrix[action]
-        a = min(max(a, 0), NA - 1);         // (out-of-range actions raise in the reference; clamped here)
-        const uint32_t eff = fused_effective_action<NA>(s_thr, a, k53);
+        if (i) s = pcg_step(s, incv);
         const uint32_t s_ae = ae[q][i];
-        const int agent = (int)(s_ae & 0xFFFFu);
-        const uint32_t m = tb.move(agent * NA + (int)eff);
-        const int na_ = (int)(m & 0x7FFFu);
+        uint32_t m;
+        if constexpr (TRIMS) {
+          const uint32_t effx =
+              fused_effx_row<NA>(s_thr, a_cur[q][i], GP_ALIGNBIT ? pcg_output_ab(s) : pcg_output(s));
+          m = tb.move_b(((s_ae & 0xFFFFu) << (NA == 4 ? 3 : 4)) + effx);
+        } else {
+          const uint64_t k53 = pcg_output(s) >> 11;
+          int a = a_cur[q][i];
+          if (a < 0) a += NA;                 // numpy negative indexing of action_matrix[action]
+          a = min(max(a, 0), NA - 1);         // (out-of-range actions raise in the reference; clamped here)
+          const uint32_t eff = fused_effective_action<NA>(s_thr, a, k53);
+          m = tb.move((int)(s_ae & 0xFFFFu) * NA + (int)eff);
+        }
+        const int na_ = (int)__builtin_amdgcn_ubfe(m, 0, 15);
         const bool blocked = (m >> 15) != 0;
         const uint32_t el = (s_ae >> 16) + 1u;
         const bool tm_ = na_ == gl[q][i];
@@ -1577,15 +1679,27 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
         const int ag = f && fixed_agent >= 0 ? fixed_agent : na_;
         ae[q][i] = (uint32_t)ag | ((f ? 0u : el) << 16);
         if (f && fixed_goal >= 0) gl[q][i] = fixed_goal;
-        if (valid) {
-          rsum += rw;
-          nst += 1;
-        }
-        if (f) {
-          eps += 1;
-          lens += el;
+        if constexpr (!GP_ACC) {
+          if (valid) {
+            rsum += rw;
+            nst += 1;
+          }
+          if (f) {
+            eps += 1;
+            lens += el;
+          }
         }
       }
+      if constexpr (GP_ACC) {
+        const uint32_t vm = STG ? 0xFu : vmask[q];
+        eps += (uint32_t)__builtin_popcount(fm[q]);
+        ngoal += (uint32_t)__builtin_popcount(tmm[q] & vm);
+        nwall += (uint32_t)__builtin_popcount(bkm[q] & ~tmm[q] & vm);
+      }
+    }
+    // the per-wave reset counts after both tiles' transitions (their VALU chains interleave: -2.5% per step)
+#pragma unroll
+    for (int q = 0; q < QPT; ++q) {
       wave_count_prefix((uint32_t)__builtin_popcount(fm[q]), wex[q], wt[q]);
       if (lane == 0) sh.wcnt[q][wid] = wt[q];
     }
@@ -1689,6 +1803,14 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
 #pragma unroll
       for (int q = 0; q < QPT; ++q) S[q] = apply_jump(jB, S[q]);  // first half of the advance (J_B)
     }
+    if constexpr (TRIMS) {  // the next step's actions -> threshold rows, while the exchange runs
+      if (k + 1 < K) {
+#pragma unroll
+        for (int q = 0; q < QPT; ++q)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) a_nxt[q][i] = action_row<NA>(a_nxt[q][i]);
+      }
+    }
     STAMP(13);
     lds_barrier();  // B2: the exchange result is in LDS
     STAMP(4);
@@ -1713,6 +1835,20 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
     STAMP(5);
   }
   if (!STG && K > 0) flush_reset_obs<OK, QPT>(p, tb, (uint8_t*)obs + (size_t)(K - 1) * B * ow, tid, pc, pfm);
+  if constexpr (GP_ACC) {
+    uint32_t nv = 0;
+#pragma unroll
+    for (int q = 0; q < QPT; ++q) {
+      nv += (uint32_t)__builtin_popcount(vmask[q]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if ((vmask[q] >> i) & 1u) lens -= ae[q][i] >> 16;
+    }
+    const uint32_t steps = nv * (uint32_t)K;
+    lens += steps;
+    nst += steps;
+    rsum += (float)ngoal * r_goal + (float)nwall * r_wall + (float)(steps - ngoal - nwall) * r_step;
+  }
 #pragma unroll
   for (int q = 0; q < QPT; ++q) {
     const int env0 = (q * G + (int)blockIdx.x) * FEPB + tid * EPT;
@@ -2043,7 +2179,7 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
   // The launch prologue: the lookup-table image into LDS in one copy loop (the fused path is only taken
   // when it fits) and the small shared words, then a block barrier. (Letting each role issue its own first
   // global loads before this copy, to overlap their latency, measured slower: 17.2 vs 16.1 µs at K = 1.)
-  if (tid < NA * NA) s_thr[tid] = p.thr[tid];
+  if (tid < NA * NA) s_thr[tid] = GP_TRIMS ? thr_on_u64(p.thr[tid]) : p.thr[tid];
   lds_image_copy(dyn, p.limg, p.lds.total);
   if (tid < 4) sh.jB[tid] = (&p.fjB->a_hi)[tid];
   if (tid == 0) sh.rdone = 0;
