@@ -910,6 +910,14 @@ constexpr uint32_t TAG_MASK = 0x7FFFu;
 #define GP_ACC 1
 #endif
 //  GP_VPIN 1: the stream increment and the goal-direction offsets pinned to VGPRs (SGPR pressure).
+//  GP_ILV 1: the transitions loop runs env-slot-major (the tiles' independent draw chains interleave).
+//  GP_CELLENV 1 (staged kernel): resetter cells stored by env slot, taken with one 16-B LDS load per tile.
+#ifndef GP_ILV
+#define GP_ILV 1
+#endif
+#ifndef GP_CELLENV
+#define GP_CELLENV 1
+#endif
 #ifndef GP_VPIN
 #define GP_VPIN 1
 #endif
@@ -932,7 +940,7 @@ struct FusedShared {
   uint16_t renv[2][FEPB];        // STG: env (in tile) of resetter rank r of tile q
   uint32_t pos[FEPB];            // slow path: accepted-word positions of one tile's resetters
   uint32_t pos2[FEPB];
-  uint32_t cell[FMAXQ * FEPB];   // resetter cells (goal | agent << 16) by tile and rank
+  alignas(16) uint32_t cell[FMAXQ * FEPB];  // resetter cells (goal | agent << 16) by tile and rank (or env slot)
 };
 
 __device__ __forceinline__ uint64_t bgran(uint32_t tag, uint32_t rej, uint64_t counts) {
@@ -1300,7 +1308,7 @@ __device__ __forceinline__ void ctrl_fast_finish(const GridDev& p, FusedShared& 
       const uint32_t v = lemire_value(word, nsel);
       const uint32_t goal = rgoal ? (uint32_t)tb.gv((int)v) : (uint32_t)p.fixed_goal;
       const uint32_t agent = rgoal ? (uint32_t)p.fixed_agent : (uint32_t)tb.av((int)v);
-      sh.cell[q * FEPB + r] = goal | (agent << 16);
+      sh.cell[q * FEPB + ((STG && GP_CELLENV) ? (uint32_t)slot : r)] = goal | (agent << 16);
       stage_reset_obs_r<OK, STG>(p, tb, stg, q, slot, goal | (agent << 16), dof);
     } else if (extra) {
       if (lane == 61) { sh.ju[0] = hi64(X); sh.ju[1] = lo64(X); }
@@ -1349,7 +1357,7 @@ __device__ __forceinline__ void ctrl_draw_cells(const GridDev& p, FusedShared& s
     const uint32_t v = draw_cells(tb.jt8(), tb.jt(), SB, st.h0, st.u0, wg, wa, mode, ng, na);
     const uint32_t goal = rgoal ? (uint32_t)tb.gv((int)(v & 0xFFFFu)) : (uint32_t)p.fixed_goal;
     const uint32_t agent = ragent ? (uint32_t)tb.av((int)(v >> 16)) : (uint32_t)p.fixed_agent;
-    sh.cell[q * FEPB + r] = goal | (agent << 16);
+    sh.cell[q * FEPB + ((STG && GP_CELLENV) ? (uint32_t)sh.renv[q][r] : r)] = goal | (agent << 16);
     stage_reset_obs<OK, STG>(p, sh, tb, stg, q, r, goal | (agent << 16));
   }
 }
@@ -1375,13 +1383,18 @@ __device__ __forceinline__ void fused_resets(const GridDev& p, FusedShared& sh, 
       // the resetters' new cells (independent LDS loads); their obs are written in the next step's
       // output phase, off the critical path (pc / pfm)
       // (STG: the control wave wrote their final obs into the LDS staging area when it drew them)
-      uint32_t r = excl[q];
       uint32_t c[4];
+      if constexpr (STG && GP_CELLENV) {  // by env slot: this thread's 4 envs in one 16-B load
+        const uint4 v = reinterpret_cast<const uint4*>(sh.cell + q * FEPB)[threadIdx.x];
+        c[0] = v.x; c[1] = v.y; c[2] = v.z; c[3] = v.w;
+      } else {
+        uint32_t r = excl[q];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const uint32_t bit = (fm[q] >> i) & 1u;
-        c[i] = sh.cell[q * FEPB + min(r, (uint32_t)FEPB - 1u)];
-        r += bit;
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t bit = (fm[q] >> i) & 1u;
+          c[i] = sh.cell[q * FEPB + min(r, (uint32_t)FEPB - 1u)];
+          r += bit;
+        }
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -1642,13 +1655,19 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
     }
     // ---- 1. draws + transitions (the critical path) ----
     uint32_t fm[QPT], tmm[QPT], trm[QPT], bkm[QPT], excl[QPT], wex[QPT], wt[QPT];
+    u128 sd[QPT];  // draw states of the tiles' current env slots
 #pragma unroll
     for (int q = 0; q < QPT; ++q) {
-      const int env0 = (q * G + (int)blockIdx.x) * FEPB + tid * EPT;
       fm[q] = tmm[q] = trm[q] = bkm[q] = 0;
-      u128 s = S[q];
+      sd[q] = S[q];
+    }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+    for (int o = 0; o < QPT * 4; ++o) {
+      // GP_ILV: slot-major (q fastest) so that the tiles' dependent draw chains interleave
+      const int q = GP_ILV ? o % QPT : o / 4, i = GP_ILV ? o / QPT : o % 4;
+      const int env0 = (q * G + (int)blockIdx.x) * FEPB + tid * EPT;
+      {
+        u128& s = sd[q];
         if (i) s = pcg_step(s, incv);
         const uint32_t s_ae = ae[q][i];
         uint32_t m;
@@ -1690,7 +1709,10 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
           }
         }
       }
-      if constexpr (GP_ACC) {
+    }
+    if constexpr (GP_ACC) {
+#pragma unroll
+      for (int q = 0; q < QPT; ++q) {
         const uint32_t vm = STG ? 0xFu : vmask[q];
         eps += (uint32_t)__builtin_popcount(fm[q]);
         ngoal += (uint32_t)__builtin_popcount(tmm[q] & vm);
