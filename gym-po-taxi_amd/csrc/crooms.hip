@@ -11,9 +11,14 @@
 //
 // RNG: the reference draws numpy ziggurat normals (data-dependent word counts) and choice() from one
 // stream, so no parallel kernel can follow it word for word. GP_RNG_PHILOX draws the same laws from a
-// counter-based Philox4x32-10 keyed by the seed (Box-Muller normals, Lemire cell indices, 53-bit
-// uniforms compared against the integer action-failure thresholds); GP_RNG_REPLAY takes the values
-// the reference's stream produced (how parity is tested).
+// counter-based Philox4x32-10 keyed by the seed: normals by Box-Muller on a 53-bit u1 (one Philox block per
+// pair; the radius reaches sqrt(-2 ln 2^-53) = 8.57 sigma, no tail cut) in float32 hardware arithmetic
+// (GP_CR_NORMAL_F64=1: float64 log / sqrt / sincospi, 2.4x slower rollouts), Lemire cell indices, 53-bit
+// uniforms compared against the integer action-failure thresholds. GP_RNG_REPLAY takes the values the
+// reference's stream produced (how parity is tested). numpy's own normal algorithm (the 256-layer ziggurat,
+// zig_normal below) is restated too and checked bit for bit against numpy over numpy's words
+// (gp_standard_normal_words); as the philox sampler its rare rejection path, taken by ~1.5% of the normals
+// but by some lane of nearly every wave, made the rollout 2.7x slower than Box-Muller, which is branch-free.
 //
 // Kernels: a persistent, grid-stride rollout kernel (tables staged in LDS once per block, 512-env
 // tiles, K steps per tile, 2 envs per thread).
@@ -23,6 +28,7 @@
 #include <vector>
 
 #include "gp_internal.h"
+#include "ziggurat_tables.h"
 
 #pragma clang fp contract(off)
 
@@ -34,6 +40,13 @@ constexpr int EPB = TPB * EPT;
 constexpr int WAVES = TPB / 64;
 constexpr uint32_t TAG_NOISE = 0x63726f6fu;  // 'croo'
 constexpr uint32_t TAG_DRAW = 0x6d733121u;
+#ifndef GP_CR_NORMAL_F64
+#define GP_CR_NORMAL_F64 0
+#endif
+// Minimum waves per SIMD of the rollout kernel (caps its VGPRs at 512 / waves; tuning knob).
+#ifndef GP_CR_WAVES
+#define GP_CR_WAVES 2
+#endif
 constexpr double MAX_VELOCITY = 5.0;        // crooms.py:170
 
 struct alignas(32) CrSlot {
@@ -82,16 +95,135 @@ __device__ __forceinline__ void stage_tables(const CrDev& p, uint8_t* lds) {
 }
 
 // ---- draws ----
-// Box-Muller on two 32-bit words: z0 = r cos(2 pi u2), z1 = r sin(2 pi u2), r = sqrt(-2 ln u1), u1 in (0,1].
-// Hardware transcendentals (float32 accuracy, which is all the law needs): v_log_f32 = log2,
-// v_sin/cos_f32 take revolutions, i.e. sin(2 pi u2) directly.
-__device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, double& z0, double& z1) {
-  const float u1 = ((float)(a >> 8) + 1.0f) * 5.9604644775390625e-08f;  // (k+1) 2^-24, in (0, 1]
-  const float r = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));  // sqrt(-2 ln u1)
-  const float u2 = (float)(b >> 8) * 5.9604644775390625e-08f;           // k 2^-24, in [0, 1)
+// numpy's random_standard_normal (numpy/random/src/distributions/distributions.c, numpy 2.2): the 256-layer
+// ziggurat on 64-bit words. `r` is the normal's first word; `next` yields the words it consumes after that
+// (a rejected layer draw or the tail, ~1% of normals). Operation for operation as numpy (no FMA
+// contraction in this file), so over numpy's word stream it returns numpy's values (checked bit for bit
+// against numpy by gp_standard_normal_words; exp / log1p are the device libm's, so a tail value may differ
+// from glibc's in the last bit).
+// Compact float64 exp and log1p for the ziggurat's slow path (GP_ZIG_OCML=0, default; the device libm's
+// versions with GP_ZIG_OCML=1). Both within ~1 ulp over the ranges used (exp: [-6.7, 0]; log1p(-u): u in
+// [0, 1 - 2^-53]); explicit fma (this file disables contraction).
+#ifndef GP_ZIG_OCML
+#define GP_ZIG_OCML 0
+#endif
+__device__ __forceinline__ double zexp(double y) {
+#if GP_ZIG_OCML
+  return exp(y);
+#else
+  const double k = rint(y * 1.4426950408889634);               // y = k ln2 + r, |r| <= ln2 / 2
+  const double r = fma(-k, 1.9082149292705877e-10, fma(-k, 0.6931471803691238, y));  // Cody-Waite ln2 hi / lo
+  double q = 1.6059043836821613e-10;                           // 1/13!, Horner to 1/0!
+  q = fma(q, r, 2.08767569878681e-09);
+  q = fma(q, r, 2.505210838544172e-08);
+  q = fma(q, r, 2.755731922398589e-07);
+  q = fma(q, r, 2.7557319223985893e-06);
+  q = fma(q, r, 2.48015873015873e-05);
+  q = fma(q, r, 0.0001984126984126984);
+  q = fma(q, r, 0.001388888888888889);
+  q = fma(q, r, 0.008333333333333333);
+  q = fma(q, r, 0.041666666666666664);
+  q = fma(q, r, 0.16666666666666666);
+  q = fma(q, r, 0.5);
+  q = fma(q, r, 1.0);
+  q = fma(q, r, 1.0);
+  return ldexp(q, (int)k);
+#endif
+}
+__device__ __forceinline__ double zlog1p_neg(double u) {  // log1p(-u) = log(v), v = 1 - u (exact for u = k 2^-53)
+#if GP_ZIG_OCML
+  return log1p(-u);
+#else
+  const double v = 1.0 - u;
+  int e;
+  double m = frexp(v, &e);                                     // v = m 2^e, m in [0.5, 1)
+  if (m < 0.7071067811865476) {
+    m = m * 2.0;
+    e -= 1;
+  }
+  const double sn = (m - 1.0) / (m + 1.0), s2 = sn * sn;       // log m = 2 atanh(s), |s| <= 0.1716
+  double q = 1.0 / 23.0;
+  q = fma(q, s2, 1.0 / 21.0);
+  q = fma(q, s2, 1.0 / 19.0);
+  q = fma(q, s2, 1.0 / 17.0);
+  q = fma(q, s2, 1.0 / 15.0);
+  q = fma(q, s2, 1.0 / 13.0);
+  q = fma(q, s2, 1.0 / 11.0);
+  q = fma(q, s2, 1.0 / 9.0);
+  q = fma(q, s2, 1.0 / 7.0);
+  q = fma(q, s2, 1.0 / 5.0);
+  q = fma(q, s2, 1.0 / 3.0);
+  const double lm = fma(2.0 * sn * s2, q, 2.0 * sn);
+  return fma((double)e, 0.6931471803691238, fma((double)e, 1.9082149292705877e-10, lm));
+#endif
+}
+
+struct ZigTabs {
+  const uint64_t* ki;
+  const double* wi;
+  const double* fi;
+};
+__device__ __forceinline__ double u53_of(uint64_t w) { return (double)(w >> 11) * (1.0 / 9007199254740992.0); }
+template <class NEXT>
+__device__ __forceinline__ double zig_slow(const ZigTabs& t, uint64_t r, NEXT& next) {
+  for (;;) {
+    const int idx = (int)(r & 0xff);
+    r >>= 8;
+    const uint64_t sign = r & 1u, rabs = (r >> 1) & 0x000fffffffffffffull;
+    double x = (double)rabs * t.wi[idx];
+    if (sign) x = -x;
+    if (rabs < t.ki[idx]) return x;
+    if (idx == 0) {
+      for (;;) {
+        const double xx = -GP_ZIG_INV_R * zlog1p_neg(u53_of(next()));
+        const double yy = -zlog1p_neg(u53_of(next()));
+        if (yy + yy > xx * xx) return ((rabs >> 8) & 1u) ? -(GP_ZIG_R + xx) : GP_ZIG_R + xx;
+      }
+    }
+    if ((t.fi[idx - 1] - t.fi[idx]) * u53_of(next()) + t.fi[idx] < zexp(-0.5 * x * x)) return x;
+    r = next();
+  }
+}
+// The fast path (~99% of draws): one word, two table loads; false = the slow path must finish the draw.
+__device__ __forceinline__ bool zig_fast(const ZigTabs& t, uint64_t r, double& z) {
+  const int idx = (int)(r & 0xff);
+  const uint64_t rr = r >> 8, rabs = (rr >> 1) & 0x000fffffffffffffull;
+  const double x = (double)rabs * t.wi[idx];
+  z = (rr & 1u) ? -x : x;
+  return rabs < t.ki[idx];
+}
+template <class NEXT>
+__device__ __forceinline__ double zig_normal(const ZigTabs& t, uint64_t r, NEXT& next) {
+  double z;
+  if (zig_fast(t, r, z)) return z;
+  return zig_slow(t, r, next);
+}
+// The philox-mode normal pair: Box-Muller on u1 = K 2^-53 in (0, 1] (K = 53 bits of w1, plus 1) and the angle
+// u2 from w2: r = sqrt(-2 ln u1), (z0, z1) = r (cos 2 pi u2, sin 2 pi u2); |z| reaches 8.57 (the former
+// 24-bit u1 stopped at 5.77). Float32 hardware arithmetic: ln u1 = ln2 (p - 53 + log2 m) with K = m 2^p,
+// m in [1, 2) taken to 24 bits (v_log_f32 is log2), v_sqrt_f32, v_sin / v_cos_f32 of a 24-bit angle in
+// revolutions; GP_CR_NORMAL_F64: the same in float64 (device libm).
+__device__ __forceinline__ void box_muller_pair(uint64_t w1, uint64_t w2, double& z0, double& z1) {
+#if GP_CR_NORMAL_F64
+  const double u1 = (double)((w1 >> 11) + 1u) * 0x1p-53;
+  const double u2 = (double)(w2 >> 11) * 0x1p-53;
+  const double r = sqrt(-2.0 * log(u1));
+  double sn, cs;
+  sincospi(2.0 * u2, &sn, &cs);
+  z0 = r * cs;
+  z1 = r * sn;
+#else
+  const uint64_t K = (w1 >> 11) + 1u;
+  const int pw = 63 - __builtin_clzll(K);
+  const float m = (float)(uint32_t)((K << (63 - pw)) >> 40) * 0x1p-23f;
+  const float l2 = (float)(pw - 53) + __builtin_amdgcn_logf(m);                      // log2 u1 <= 0
+  const float r = __builtin_amdgcn_sqrtf(-1.3862943611198906f * l2);                  // sqrt(-2 ln u1)
+  const float u2 = (float)(uint32_t)(w2 >> 40) * 0x1p-24f;                            // revolutions
   z0 = (double)(r * __builtin_amdgcn_cosf(u2));
   z1 = (double)(r * __builtin_amdgcn_sinf(u2));
+#endif
 }
+
 
 struct Draws {
   uint64_t k53;      // action-failure uniform
@@ -99,26 +231,37 @@ struct Draws {
 };
 
 // Gaussian noise of env-step (env, step): pair 0 = action noise N(0, action_std) (crooms.py:178,
-// :194-195), pair 1 = wall noise N(0, 0.5) (:324). Replay: the values numpy returned.
+// :194-195), pair 1 = wall noise N(0, 0.5) (:324). Replay: the values numpy returned. Philox: ONE block of
+// counter (env, step, TAG_NOISE) per env-step (kept in blk / have by the caller) serves both pairs with
+// disjoint bits: pair 0 = box_muller_pair(x1:x0 -> 53-bit u1, x3:x2 -> 24-bit angle); pair 1 takes the bits
+// pair 0 leaves: u1 = (x2 + 1) 2^-32 (radius to 6.66 sigma), a 19-bit angle (x0 & 0x7FF, x3 & 0xFF). The
+// wall noise is clipped to its cell (|n| <= cell / 2, i.e. |z| <= 1 at the default cell), so its far
+// tail never reaches an observation.
+__device__ __forceinline__ void box_muller_wall(const Philox4& r, double& z0, double& z1) {
+  const float l2 = __builtin_amdgcn_logf(((float)r.x[2] + 1.0f) * 0x1p-32f);            // log2 u1 (u1 in (0, 1])
+  const float rad = __builtin_amdgcn_sqrtf(-1.3862943611198906f * l2);
+  const float u2 = (float)(((r.x[0] & 0x7FFu) << 8) | (r.x[3] & 0xFFu)) * 0x1p-19f;  // revolutions
+  z0 = (double)(rad * __builtin_amdgcn_cosf(u2));
+  z1 = (double)(rad * __builtin_amdgcn_sinf(u2));
+}
 template <bool REPLAY>
 __device__ __forceinline__ void draw_normals(const CrDev& p, int env, uint64_t step, int pair, double scale,
-                                             double& y, double& x, Philox4* blk = nullptr, bool* have = nullptr) {
+                                             double& y, double& x, Philox4& blk, bool& have) {
   if constexpr (REPLAY) {
     const double* src = pair == 0 ? p.rp_noise : p.rp_wall;
     const double2 v = *reinterpret_cast<const double2*>(src + 2 * (size_t)env);
     y = v.x;
     x = v.y;
   } else {
-    // one Philox block per env-step serves both pairs (the caller keeps it in blk / have)
-    Philox4 r;
-    if (have && *have) {
-      r = *blk;
-    } else {
-      r = philox4x32_10((uint32_t)env, (uint32_t)step, (uint32_t)(step >> 32), TAG_NOISE, p.key0, p.key1);
-      if (have) { *blk = r; *have = true; }
+    if (!have) {
+      blk = philox4x32_10((uint32_t)env, (uint32_t)step, (uint32_t)(step >> 32), TAG_NOISE, p.key0, p.key1);
+      have = true;
     }
     double z0, z1;
-    box_muller(r.x[2 * pair], r.x[2 * pair + 1], z0, z1);
+    if (pair == 0)
+      box_muller_pair(((uint64_t)blk.x[1] << 32) | blk.x[0], ((uint64_t)blk.x[3] << 32) | blk.x[2], z0, z1);
+    else
+      box_muller_wall(blk, z0, z1);
     y = scale * z0;
     x = scale * z1;
   }
@@ -253,11 +396,13 @@ __device__ __forceinline__ StepOut crooms_env_step(const CrDev& p, const uint8_t
   d.gi = d.ai = 0;
   // _sample_action (crooms.py:175-198) * action_power (:288)
   double my, mx;
+  // the action noise (one draw site for both action kinds, so the sampler is inlined once)
   Philox4 nblk;
   bool nhave = false;
+  double ny = 0.0, nx = 0.0;
+  if (live && (p.action_kind == 0 || p.action_std != 0.0))
+    draw_normals<REPLAY>(p, env, step, 0, p.action_std, ny, nx, nblk, nhave);
   if (p.action_kind == 0) {
-    double ny = 0.0, nx = 0.0;
-    if (live) draw_normals<REPLAY>(p, env, step, 0, p.action_std, ny, nx, &nblk, &nhave);
     my = a0 + ny;
     mx = a1 + nx;
   } else {
@@ -274,8 +419,6 @@ __device__ __forceinline__ StepOut crooms_env_step(const CrDev& p, const uint8_t
     my = (double)DY[o8];
     mx = (double)DX[o8];
     if (p.action_std != 0.0) {
-      double ny = 0.0, nx = 0.0;
-      if (live) draw_normals<REPLAY>(p, env, step, 0, p.action_std, ny, nx, &nblk, &nhave);
       my = my + ny;
       mx = mx + nx;
     }
@@ -305,7 +448,7 @@ __device__ __forceinline__ StepOut crooms_env_step(const CrDev& p, const uint8_t
     const double cy = floor(per_cell(p, ay)) * p.cell + p.half_cell;
     const double cx = floor(per_cell(p, ax)) * p.cell + p.half_cell;
     double wy = 0.0, wx = 0.0;
-    if (live) draw_normals<REPLAY>(p, env, step, 1, 0.5, wy, wx, &nblk, &nhave);
+    if (live) draw_normals<REPLAY>(p, env, step, 1, 0.5, wy, wx, nblk, nhave);
     ay = fmin(fmax(cy + wy, cy - p.half_cell), (cy + p.half_cell) - 1e-8);
     ax = fmin(fmax(cx + wx, cx - p.half_cell), (cx + p.half_cell) - 1e-8);
     vy = 0.0;
@@ -358,7 +501,7 @@ __device__ void cr_metrics(const CrDev& p, float rsum, uint32_t eps, uint32_t le
 
 // ---- the rollout kernel: K steps for every env; 2 consecutive envs per thread ----
 template <int OK, bool REPLAY>
-__global__ __launch_bounds__(TPB) void crooms_rollout(CrDev p, int K, uint64_t step0, const void* __restrict__ act,
+__global__ __launch_bounds__(TPB, GP_CR_WAVES) void crooms_rollout(CrDev p, int K, uint64_t step0, const void* __restrict__ act,
                                                       void* __restrict__ obs, float* __restrict__ rew,
                                                       uint8_t* __restrict__ term, uint8_t* __restrict__ trunc) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -930,6 +1073,117 @@ int CRoomsBackend::build(const gp_crooms_config* cfg) {
 }
 
 }  // namespace
+
+// ---- diagnostics of the normal sampler (C ABI below) ----
+namespace {
+__device__ const uint64_t d_zig[768] = {GP_ZIG_KI_LIST, GP_ZIG_WI_LIST, GP_ZIG_FI_LIST};
+
+// numpy's standard_normal over a caller word stream, one lane, in order (numpy consumes the words
+// sequentially and a normal may take several).
+__global__ void zig_words_kernel(const uint64_t* __restrict__ w, int64_t nw, double* __restrict__ out, int64_t n,
+                                 int64_t* __restrict__ used) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const ZigTabs t{d_zig, reinterpret_cast<const double*>(d_zig + 256), reinterpret_cast<const double*>(d_zig + 512)};
+  int64_t pos = 0;
+  auto next = [&]() -> uint64_t { return pos < nw ? w[pos++] : 0ull; };
+  for (int64_t i = 0; i < n; ++i) {
+    if (pos >= nw) {
+      out[i] = __builtin_nan("");
+      continue;
+    }
+    const uint64_t r = w[pos++];
+    out[i] = zig_normal(t, r, next);
+  }
+  *used = pos;
+}
+
+// n normals of the philox-mode sampler (counter (i, 0, 0, TAG_NOISE) for the pair 2i, 2i+1, as
+// draw_normals): exceedance counts |z| > thr[j] and the sum / sum of squares, without storing them.
+constexpr int ZT_MAX = 8;
+__global__ __launch_bounds__(256) void zig_tail_kernel(uint32_t k0, uint32_t k1, uint64_t npairs, const double* __restrict__ thr,
+                                                       int nthr, unsigned long long* __restrict__ counts,
+                                                       double* __restrict__ mom) {
+  __shared__ uint64_t zt[768];
+  __shared__ double sthr[ZT_MAX];
+  for (int i = threadIdx.x; i < 768; i += blockDim.x) zt[i] = d_zig[i];
+  if (threadIdx.x < ZT_MAX) sthr[threadIdx.x] = threadIdx.x < nthr ? thr[threadIdx.x] : 1e300;
+  __syncthreads();
+  ZigTabs t;  // (member-wise: a braced initializer of LDS addresses is folded into an invalid static one)
+  t.ki = zt;
+  t.wi = reinterpret_cast<const double*>(zt + 256);
+  t.fi = reinterpret_cast<const double*>(zt + 512);
+  unsigned long long c[ZT_MAX] = {};
+  double s1 = 0.0, s2 = 0.0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < npairs; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t e = (uint32_t)i, s0 = (uint32_t)(i >> 32);
+    const Philox4 r = philox4x32_10(e, s0, 0u, TAG_NOISE, k0, k1);
+    double z0, z1;
+    box_muller_pair(((uint64_t)r.x[1] << 32) | r.x[0], ((uint64_t)r.x[3] << 32) | r.x[2], z0, z1);
+    s1 += z0 + z1;
+    s2 += z0 * z0 + z1 * z1;
+#pragma unroll
+    for (int j = 0; j < ZT_MAX; ++j) c[j] += (fabs(z0) > sthr[j] ? 1u : 0u) + (fabs(z1) > sthr[j] ? 1u : 0u);
+  }
+#pragma unroll
+  for (int j = 0; j < ZT_MAX; ++j) {
+    unsigned long long v = c[j];
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(&counts[j], v);
+  }
+  for (int d = 32; d >= 1; d >>= 1) {
+    s1 += __shfl_xor(s1, d, 64);
+    s2 += __shfl_xor(s2, d, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(&mom[0], s1);
+    atomicAdd(&mom[1], s2);
+  }
+}
+}  // namespace
+
+extern "C" int gp_standard_normal_words(const uint64_t* words, int64_t nwords, double* out, int64_t n, int64_t* used,
+                                        void* stream) {
+  if (!words || !out || !used || nwords < 0 || n < 0) {
+    gp_set_error("gp_standard_normal_words: bad argument");
+    return GP_E_INVALID;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  DevBuf u;
+  int e;
+  if ((e = u.alloc(sizeof(int64_t)))) return e;
+  hipLaunchKernelGGL(zig_words_kernel, dim3(1), dim3(64), 0, s, words, nwords, out, n, u.as<int64_t>());
+  GP_HIP_CHECK(hipGetLastError());
+  GP_HIP_CHECK(hipMemcpyAsync(used, u.p, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  GP_HIP_CHECK(hipStreamSynchronize(s));
+  return GP_OK;
+}
+
+extern "C" int gp_normal_tail_counts(uint64_t key, int64_t n, const double* thr, int nthr, uint64_t* counts,
+                                     double moments[2], void* stream) {
+  if (n < 2 || !thr || !counts || !moments || nthr < 1 || nthr > ZT_MAX) {
+    gp_set_error("gp_normal_tail_counts: bad argument (1 <= nthr <= %d, n >= 2)", ZT_MAX);
+    return GP_E_INVALID;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  DevBuf dthr, dc, dm;
+  int e;
+  if ((e = dthr.alloc(sizeof(double) * ZT_MAX)) || (e = dc.alloc(sizeof(uint64_t) * ZT_MAX)) ||
+      (e = dm.alloc(sizeof(double) * 2)))
+    return e;
+  GP_HIP_CHECK(hipMemcpy(dthr.p, thr, sizeof(double) * nthr, hipMemcpyHostToDevice));
+  int dev = 0, cus = 256;
+  GP_HIP_CHECK(hipGetDevice(&dev));
+  GP_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  hipLaunchKernelGGL(zig_tail_kernel, dim3(cus * 8), dim3(256), 0, s, (uint32_t)key, (uint32_t)(key >> 32),
+                     (uint64_t)n / 2, dthr.as<double>(), nthr, dc.as<unsigned long long>(), dm.as<double>());
+  GP_HIP_CHECK(hipGetLastError());
+  GP_HIP_CHECK(hipStreamSynchronize(s));
+  std::vector<uint64_t> c(ZT_MAX);
+  GP_HIP_CHECK(hipMemcpy(c.data(), dc.p, sizeof(uint64_t) * ZT_MAX, hipMemcpyDeviceToHost));
+  GP_HIP_CHECK(hipMemcpy(moments, dm.p, sizeof(double) * 2, hipMemcpyDeviceToHost));
+  for (int j = 0; j < nthr; ++j) counts[j] = c[j];
+  return GP_OK;
+}
 
 std::unique_ptr<EnvBackend> make_crooms_backend(const gp_crooms_config* cfg, int64_t B, int device, int rng_mode,
                                                 int* err) {

@@ -95,6 +95,11 @@ SIGNATURES = {
                                            ctypes.POINTER(ctypes.c_uint64)]),
     "gp_argmax_multinomial_distribution": (ctypes.c_int, [ctypes.c_int, ctypes.c_int,
                                                           ctypes.POINTER(ctypes.c_double)]),
+    "gp_standard_normal_words": (ctypes.c_int, [_vp, ctypes.c_int64, _vp, ctypes.c_int64,
+                                                ctypes.POINTER(ctypes.c_int64), _vp]),
+    "gp_normal_tail_counts": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_int64, ctypes.POINTER(ctypes.c_double),
+                                             ctypes.c_int, ctypes.POINTER(ctypes.c_uint64),
+                                             ctypes.POINTER(ctypes.c_double), _vp]),
 }
 
 _lib = None
@@ -129,6 +134,8 @@ def lib():
         _bind_torch_hip_runtime()
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if not hasattr(L, name) and "GYM_PO_AMD_LIB" in os.environ:
+                continue  # an explicitly chosen older build (in-call A/B tooling): bind what it has
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

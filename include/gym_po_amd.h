@@ -213,6 +213,19 @@ int gp_check(gp_env* env);
  * "fused_tiles_per_block", "fused_staged" (1 = LDS-staged outputs + store waves),
  * "fused_tile_envs". Unknown keys return GP_E_INVALID. */
 int gp_query(const gp_env* env, const char* key, int64_t* value);
+/* ---- the normal sampler of rng_mode=philox (C-ROOMS noise), diagnostics ----
+ * Replaces numpy's Generator.standard_normal (numpy/random/src/distributions/distributions.c,
+ * random_standard_normal; the reference draws rng.normal at gym_po/envs/rooms/crooms.py:175-178, :324).
+ * gp_standard_normal_words: numpy's algorithm (256-layer ziggurat) over the caller's u64 word stream, in
+ *   order, on one device lane: words device u64[nwords], out device f64[n] (NaN once the words run out),
+ *   *used (host) = words consumed. Over numpy's raw PCG64 words it returns numpy's normals.
+ * gp_normal_tail_counts: n normals of the philox-mode sampler keyed by `key` (gp_seed's Philox key words),
+ *   never stored: counts[j] = #{|z| > thr[j]} (host arrays, nthr <= 8), moments = {sum z, sum z^2}. Syncs. */
+int gp_standard_normal_words(const uint64_t* words, int64_t nwords, double* out, int64_t n, int64_t* used,
+                             void* stream);
+int gp_normal_tail_counts(uint64_t key, int64_t n, const double* thr, int nthr, uint64_t* counts,
+                          double moments[2], void* stream);
+
 /* Device-side start-state law of TAXI resets (host copy): P(state index k) over valid states. */
 int gp_taxi_reset_distribution(const gp_env* env, double* out, int cap);
 

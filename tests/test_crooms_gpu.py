@@ -5,7 +5,10 @@ reference's own numpy stream produced (captured from the fixture-pinned oracle r
 with float64 I/O every output must equal the reference bit-for-bit; with float32 I/O (BASELINE
 configs[4]) the observation must be the float64 reference observation rounded once to float32, i.e.
 |obs - ref| <= 2^-24 |ref| (<= 1e-6 for the coordinates of every layout) — tolerance written below.
-Philox mode is checked in law (Box-Muller normals) and for rollout/step consistency.
+Philox mode is checked in law and for rollout/step consistency: its normals (Box-Muller on a 53-bit u1,
+csrc/crooms.hip box_muller_pair) are checked for their tail mass out to 6.5 sigma over 2^36 draws. numpy's
+own normal algorithm (random_standard_normal, the 256-layer ziggurat), restated on the device, is checked
+bit for bit against numpy over numpy's raw words.
 """
 import numpy as np
 import pytest
@@ -202,3 +205,57 @@ def test_philox_reset_cells_uniform(gpu_device):
     gc = g.cpu().numpy()
     gidx = np.searchsorted(env.valid_states, gc[:, 0] * W + gc[:, 1])
     assert chisquare(np.bincount(gidx, minlength=len(env.valid_states))).pvalue > 1e-4
+
+
+def test_device_ziggurat_matches_numpy_words(gpu_device):
+    """gp_standard_normal_words over numpy's raw PCG64 words returns numpy's standard_normal and consumes the
+    words numpy consumed. Exact except the layer-0 tail (|z| > r = 3.654..., ~0.03% of draws), whose value
+    goes through the device libm's log1p: within 2 ulp there (tolerance written here)."""
+    import ctypes
+    import torch
+    from gym_po_amd import _lib as L
+    from oracle.ziggurat import R, standard_normals
+    n, seed = 200000, 4242
+    want = np.random.Generator(np.random.PCG64(seed)).standard_normal(n)
+    words = np.random.PCG64(seed).random_raw(2 * n)
+    _, used_want = standard_normals(words, n)
+    dw = torch.from_numpy(words.view(np.int64)).to(gpu_device)
+    out = torch.empty(n, dtype=torch.float64, device=gpu_device)
+    used = ctypes.c_int64()
+    L.check(L.lib().gp_standard_normal_words(ctypes.c_void_p(dw.data_ptr()), len(words),
+                                             ctypes.c_void_p(out.data_ptr()), n, ctypes.byref(used),
+                                             ctypes.c_void_p(torch.cuda.current_stream(gpu_device).cuda_stream)),
+            "gp_standard_normal_words")
+    got = out.cpu().numpy()
+    assert used.value == used_want
+    tail = np.abs(want) > R
+    assert tail.sum() > 10
+    assert np.array_equal(got[~tail], want[~tail])
+    ulp = np.spacing(np.abs(want[tail]))
+    assert np.all(np.abs(got[tail] - want[tail]) <= 2 * ulp)
+
+
+def test_philox_normal_tail_mass(gpu_device):
+    """The philox-mode sampler has the normal law's tails: exceedance counts of |z| beyond 3..6.5 sigma over
+    2^36 draws within 6 Poisson standard deviations of n * erfc(t / sqrt 2) (the former float32 Box-Muller
+    could not exceed 5.77 sigma), and the first two moments within 6 standard errors."""
+    import ctypes
+    import math
+    import torch
+    from gym_po_amd import _lib as L
+    from oracle.philox import philox_key
+    n = 1 << 36
+    thr = [3.0, 4.0, 5.0, 6.0, 6.5]
+    k0, k1 = philox_key(11)
+    counts = (ctypes.c_uint64 * len(thr))()
+    mom = (ctypes.c_double * 2)()
+    torch.cuda.synchronize(gpu_device)
+    L.check(L.lib().gp_normal_tail_counts((k1 << 32) | k0, n, (ctypes.c_double * len(thr))(*thr), len(thr), counts,
+                                          mom, ctypes.c_void_p(torch.cuda.current_stream(gpu_device).cuda_stream)),
+            "gp_normal_tail_counts")
+    for t, c in zip(thr, counts):
+        lam = n * math.erfc(t / math.sqrt(2.0))
+        assert abs(c - lam) <= 6 * math.sqrt(lam) + 1, (t, c, lam)
+    assert counts[3] > 0  # beyond 6 sigma (expected ~136)
+    mean, var = mom[0] / n, mom[1] / n
+    assert abs(mean) < 6 / math.sqrt(n) and abs(var - 1.0) < 6 * math.sqrt(2.0 / n)

@@ -1,5 +1,6 @@
 """CPU checks of the oracle pieces that have no reference fixture: Philox4x32-10 (pinned to the
 published Random123 known-answer vectors) and the build-defined grid Ant-Tag spec."""
+import pytest
 import numpy as np
 
 from oracle.anttag import AntTagOracle
@@ -49,3 +50,19 @@ def test_anttag_reset_law_and_rules():
         d2 = (o[:, 0] - ora.target // 10) ** 2 + (o[:, 1] - ora.target % 10) ** 2
         assert (d2[vis] < 9).all() and (d2[~vis] >= 9).all()
         assert (r[d] == 1.0).all() and (r[~d] == 0.0).all()
+
+
+@pytest.mark.parametrize("seed", [0, 99, 31337])
+def test_ziggurat_oracle_matches_numpy(seed):
+    """oracle.ziggurat restates numpy's random_standard_normal: over numpy's raw PCG64 words it returns
+    numpy's normals bit for bit and consumes exactly the words numpy consumed."""
+    from oracle.ziggurat import standard_normals
+    n = 60000
+    g = np.random.Generator(np.random.PCG64(seed))
+    want = g.standard_normal(n)
+    words = np.random.PCG64(seed).random_raw(2 * n)
+    got, used = standard_normals(words, n)
+    assert np.array_equal(got, want)
+    ref = np.random.PCG64(seed)
+    ref.advance(used)
+    assert ref.state == g.bit_generator.state
