@@ -368,6 +368,46 @@ def main():
 
     m = shard.allreduce_metrics(env.metrics(), dev)  # RCCL: the only collective (episode statistics)
 
+    # SURVEY.md §8(d)'s primary curve is STRONG scaling (1M envs split over the N GPUs); `value` is the
+    # contract's weak-scaling number (1M envs per GPU). With N > 1 each rank also times its strong-scaling
+    # shard (2^20 / N envs, same kernel path, same warmup / step counts) and the line carries it.
+    strong = None
+    if world > 1 and not args.strong and args.workload == "fourrooms":
+        Bs = shard.shard_size(args.envs, world, rank, True)
+        env_s = W["make"](Bs, dev, args.mode)
+        shard.seed_shard(env_s, 0, rank, world)
+        env_s.reset()
+        Cs = max(1, min(args.chunk, args.steps))
+        acts_s = torch.randint(0, W["n_actions"], (Cs, Bs), device=dev, dtype=torch.int32, generator=g)
+        out_s = env_s._alloc_outputs(Cs)
+        for o in out_s:
+            o.zero_()
+        plan_s = env_s.rollout_plan(acts_s, out_s)[0]
+        plans_s = {Cs: plan_s}
+
+        def run_s(n):
+            done = 0
+            while done < n:
+                k = min(Cs, n - done)
+                if k not in plans_s:
+                    plans_s[k] = env_s.rollout_plan(acts_s[:k], tuple(o[:k] for o in out_s))[0]
+                plans_s[k]()
+                done += k
+        run_s(args.warmup)
+        torch.cuda.synchronize(dev)
+        barrier()
+        torch.cuda.synchronize(dev)
+        t0s = time.perf_counter()
+        run_s(args.steps)
+        torch.cuda.synchronize(dev)
+        barrier()
+        torch.cuda.synchronize(dev)
+        ts = shard.max_over_ranks(time.perf_counter() - t0s, dev)
+        env_s.metrics()  # raises on a device-side failure
+        env_s.close()
+        strong = {"global_envs": args.envs, "envs_per_gpu": Bs, "value": args.envs * args.steps / ts,
+                  "ms_per_step": ts / args.steps * 1e3, "scaling": "strong"}
+
     total_steps = (args.envs if args.strong else B * world) * args.steps
     cfg_key = (f"fourrooms_hansen4_B{B}_{args.mode}" if args.workload == "fourrooms" else
                f"{args.workload}_B{B}_{args.mode}")
@@ -408,6 +448,8 @@ def main():
                      "mean_length": m["length_sum"] / max(m["episodes"], 1)},
         "lib_hash": lib_hash(),
     }
+    if strong is not None:
+        line["strong"] = strong
     if rank == 0:
         if world == 1:
             pk = measured_hbm_peaks(dev)

@@ -96,3 +96,17 @@ def test_bench_kernel_random_goal_staged_k_steps(gpu_device):
     o_g = _reset_obs(env, 77)
     np.testing.assert_array_equal(o_g.astype(np.int64), np.asarray(ora.reset_seed(77)).astype(np.int64))
     _check_chunks(env, ora, (24, 40), action_seed=5, n_act=8)
+
+
+@pytest.mark.parametrize("B", [1 << 17, 1 << 18])
+def test_strong_scaling_shard_sizes_staged_bit_exact(B, gpu_device):
+    """The per-GPU shard of a strong-scaling run (1M envs over 8 / 4 GPUs): 2^17 / 2^18 envs take the same
+    staged kernel with one 2048-env tile per block (64 / 128 blocks), K = 20 then 128 steps per launch."""
+    from gym_po_amd import MultistoryFourRoomsEnv
+    env = MultistoryFourRoomsEnv(B, grid_z=1, obs_type="hansen", device=gpu_device)
+    G, q, stg, tile = _staged_geometry(env)
+    assert G * q * tile == B and stg, (G, q, stg, tile)
+    ora = gridworld.FourRoomsOracle(B, 1, obs_type="hansen")
+    o_g = _reset_obs(env, 31)
+    np.testing.assert_array_equal(o_g.astype(np.int64), np.asarray(ora.reset_seed(31)).astype(np.int64))
+    _check_chunks(env, ora, (20, 128), action_seed=3, n_act=4)
