@@ -55,7 +55,7 @@ struct GridLdsTab {
 };
 struct GridLds {  // where the fused kernel stages the lookup tables in dynamic LDS
   int32_t total;
-  GridLdsTab move, hbase, hvec, t1, t2, coords, window, gv, av, doff, jt, jt8;
+  GridLdsTab move, hbase, hvec, t1, t2, coords, window, gv, av, doff, jt, jt8, ofix;
 };
 
 struct GridDev {
@@ -101,6 +101,7 @@ struct GridDev {
   unsigned long long* dbg;  // GP_STAMPS diagnostic builds: [G][64][8] s_memtime stamps
   GridLds lds;
   const char* limg;         // [lds.total] the tables laid out exactly as staged in LDS (one copy loop)
+  const int32_t* ofix;      // Hansen obs of each agent cell for the fixed goal (empty otherwise)
   const GridDev* self;      // device copy of this struct (for out-of-line slow-path helpers)
   const PcgJump* jt8;       // [2][256] radix-256 jumps: d and 256*d steps (fused kernel: jumps < 2^16)
   int32_t xmode;            // fused exchange: 0 = block-0 aggregator + per-tile words, 1 = all-gather
@@ -233,6 +234,8 @@ struct GTabs {
   __device__ __forceinline__ uint8_t window(int i) const { return p.window[i]; }
   __device__ __forceinline__ uint16_t gv(int i) const { return p.goal_valid[i]; }
   __device__ __forceinline__ uint16_t av(int i) const { return p.agent_valid[i]; }
+  __device__ __forceinline__ bool has_ofix() const { return p.ofix != nullptr; }
+  __device__ __forceinline__ int32_t ofix(int i) const { return p.ofix[i]; }
 };
 struct LTabs {
   const GridDev& p;
@@ -258,6 +261,8 @@ struct LTabs {
   __device__ __forceinline__ uint16_t av(int i) const { return at<uint16_t>(p.lds.av, i); }
   __device__ __forceinline__ const PcgJump* jt() const { return reinterpret_cast<const PcgJump*>(dyn + p.lds.jt.off); }
   __device__ __forceinline__ const PcgJump* jt8() const { return reinterpret_cast<const PcgJump*>(dyn + p.lds.jt8.off); }
+  __device__ __forceinline__ bool has_ofix() const { return p.lds.ofix.bytes > 0; }
+  __device__ __forceinline__ int32_t ofix(int i) const { return at<int32_t>(p.lds.ofix, i); }
 };
 
 // ------------------------------------------------------------------ observation builders ----
@@ -341,6 +346,7 @@ __device__ __forceinline__ int32_t obs_value(const GridDev& p, const TB& tb, int
 template <int OK, class TB>
 __device__ __forceinline__ int32_t obs_value_r(const GridDev& p, const TB& tb, int a, int g, const int (&dof)[8]) {
   if constexpr (OK == GP_OBS_HANSEN) {
+    if (tb.has_ofix()) return tb.ofix(a);  // fixed goal: the obs is a function of the agent cell (one lookup)
     int mult = 1;
     const int diff = g - a;
 #pragma unroll
@@ -917,6 +923,10 @@ constexpr uint32_t TAG_MASK = 0x7FFFu;
 #endif
 #ifndef GP_CELLENV
 #define GP_CELLENV 1
+#endif
+//  GP_STORE_PRIO: scheduling priority of the store waves (1: above the env waves).
+#ifndef GP_STORE_PRIO
+#define GP_STORE_PRIO 1
 #endif
 #ifndef GP_VPIN
 #define GP_VPIN 1
@@ -2216,7 +2226,7 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
   } else if (wid > FENVW) {
     // above the env waves: the store waves issue their few copy instructions right after B2 instead of
     // trailing the VALU-bound transitions on their SIMD (+6% measured vs priority 0; 2 was no better)
-    __builtin_amdgcn_s_setprio(1);
+    __builtin_amdgcn_s_setprio(GP_STORE_PRIO);
     fused_store<OK, QPT, STG>(p, sh, tb, stg, K, obs, rew, term, trunc);
   } else {
     fused_env<OK, QPT, NA, STG>(p, sh, s_thr, tb, stg, K, act, obs, rew, term, trunc, rsum, eps, lens, nst);
@@ -2408,7 +2418,7 @@ struct GridBackend : EnvBackend {
   std::vector<uint16_t> goal_valid_h, agent_valid_h;
   DevBuf b_move, b_thr, b_gv, b_av, b_hbase, b_doff, b_hvec, b_t1, b_t2, b_coords, b_window, b_jt, b_lt4, b_lt2,
       b_tja, b_tjw, b_ae, b_goal, b_ctl, b_tcount, b_tlist, b_rflag, b_mslot, b_ftj, b_flt4, b_fjB, b_fslot, b_dbg, b_self, b_jt8,
-      b_limg;
+      b_limg, b_ofix;
   int fused_G = 0, fused_qpt = 0;  // fused numpy rollout geometry (0 = not eligible)
   bool fused_stg = false;          // outputs staged in LDS and written by the store waves
   // replay pointers for the next step
@@ -2593,7 +2603,8 @@ int GridBackend::refresh_lds_image() {
   if ((e = put(d.lds.move, d.move)) || (e = put(d.lds.hbase, d.hbase)) || (e = put(d.lds.hvec, d.hvec)) ||
       (e = put(d.lds.t1, d.t1)) || (e = put(d.lds.t2, d.t2)) || (e = put(d.lds.coords, d.coords)) ||
       (e = put(d.lds.window, d.window)) || (e = put(d.lds.gv, d.goal_valid)) || (e = put(d.lds.av, d.agent_valid)) ||
-      (e = put(d.lds.doff, d.doff)) || (e = put(d.lds.jt, d.jt)) || (e = put(d.lds.jt8, d.jt8)))
+      (e = put(d.lds.doff, d.doff)) || (e = put(d.lds.jt, d.jt)) || (e = put(d.lds.jt8, d.jt8)) ||
+      (e = put(d.lds.ofix, d.ofix)))
     return e;
   GP_HIP_CHECK(hipDeviceSynchronize());
   return GP_OK;
@@ -2918,6 +2929,20 @@ int GridBackend::build(const gp_grid_config* cfg) {
       hbase[c] = hb;
     }
   }
+  // Hansen obs with a fixed goal: a table over the agent cell (obs_value's goal multiplier folded in)
+  std::vector<int32_t> ofix;
+  if (cfg->obs_kind == GP_OBS_HANSEN && d.fixed_goal >= 0) {
+    ofix.assign(nc, 0);
+    for (int c = 0; c < nc; ++c) {
+      int mult = 1;
+      if ((unsigned)d.fixed_goal < (unsigned)nc) {
+        const int diff = d.fixed_goal - c;
+        for (int i = cfg->obs_dirs - 1; i >= 0; --i)
+          if (diff == doff[i]) mult = i + 1;
+      }
+      ofix[c] = (int32_t)hbase[c] * mult;
+    }
+  }
   std::vector<uint8_t> window;
   if (cfg->obs_kind == GP_OBS_WINDOW) {
     const int n = cfg->obs_n, h = n / 2;
@@ -2969,6 +2994,7 @@ int GridBackend::build(const gp_grid_config* cfg) {
   int e;
   if ((e = b_move.upload(move)) || (e = b_thr.upload(thr)) || (e = b_gv.upload(goal_valid_h)) ||
       (e = b_av.upload(agent_valid_h)) || (e = b_hbase.upload(hbase)) || (e = b_doff.upload(doff)) ||
+      (e = b_ofix.upload(ofix)) ||
       (e = b_hvec.upload(hvec)) || (e = b_coords.upload(coords)) || (e = b_window.upload(window)) ||
       (e = b_t1.upload(t1)) || (e = b_t2.upload(t2)))
     return e;
@@ -3001,6 +3027,7 @@ int GridBackend::build(const gp_grid_config* cfg) {
     put(d.lds.gv, goal_valid_h.size() * sizeof(uint16_t));
     put(d.lds.av, agent_valid_h.size() * sizeof(uint16_t));
     put(d.lds.doff, doff.size() * sizeof(int32_t));
+    put(d.lds.ofix, ofix.size() * sizeof(int32_t));
     put(d.lds.jt, sizeof(PcgJump) * JT_LEVELS * JT_RADIX);
     put(d.lds.jt8, sizeof(PcgJump) * 2 * 256);
     d.lds.total = off <= LDS_TABLE_BUDGET ? off : 0;
@@ -3060,6 +3087,7 @@ int GridBackend::build(const gp_grid_config* cfg) {
   d.agent_valid = b_av.as<uint16_t>();
   d.hbase = b_hbase.as<uint32_t>();
   d.doff = b_doff.as<int32_t>();
+  d.ofix = ofix.empty() ? nullptr : b_ofix.as<int32_t>();
   d.hvec = b_hvec.as<uint8_t>();
   d.t1 = t1.empty() ? nullptr : b_t1.as<int32_t>();
   d.t2 = t2.empty() ? nullptr : b_t2.as<int32_t>();

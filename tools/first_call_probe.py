@@ -2,8 +2,8 @@
 with the timed call repeated: how much slower the first timed call is than the following ones, and why.
 
     python tools/first_call_probe.py [variant...]
-variants: plain (as bench.py), prerun (the 20-step plan launched once before the warmup), spin (10 ms of host
-spinning on the GPU's idle before the timed call is NOT done: only reported).
+variants: plain (as bench.py), prerun (the 20-step plan launched once before the warmup), touchacts / touchouts /
+touchall (the action / output buffers read / rewritten once after setup).
 """
 import os
 import sys
@@ -31,6 +31,11 @@ for variant in sys.argv[1:] or ["plain", "prerun"]:
     plans[W] = env.rollout_plan(acts[:W], tuple(o[:W] for o in out))[0]
     if variant == "prerun":
         plans[C]()
+    if variant in ("touchacts", "touchall"):
+        acts.view(torch.uint8).max()
+    if variant in ("touchouts", "touchall"):
+        for o in out:
+            o.zero_()
     plans[W]()
     ts = []
     for rep in range(6):
