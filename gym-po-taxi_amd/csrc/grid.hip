@@ -55,7 +55,7 @@ struct GridLdsTab {
 };
 struct GridLds {  // where the fused kernel stages the lookup tables in dynamic LDS
   int32_t total;
-  GridLdsTab move, hbase, hvec, t1, t2, coords, window, gv, av, doff, jt, jt8, ofix, ngt, mv32;
+  GridLdsTab move, hbase, hvec, t1, t2, coords, window, gv, av, doff, jt, jt8, ofix, avo;
 };
 
 struct GridDev {
@@ -102,9 +102,7 @@ struct GridDev {
   GridLds lds;
   const char* limg;         // [lds.total] the tables laid out exactly as staged in LDS (one copy loop)
   const int32_t* ofix;      // Hansen obs of each agent cell for the fixed goal (empty otherwise)
-  const uint8_t* ngt;       // fixed goal: 1 where some action's move from the cell lands on the goal
-  const uint32_t* mv32;     // [ncells * nact] move table for the early-count kernel: dest | ngt[dest] << 15 | blocked << 16
-  int32_t fa16;             // fixed agent | ngt[fixed agent] << 15 (-1: random agent)
+  const uint32_t* avo;      // with ofix: {agent_valid[j], ofix[agent_valid[j]]} pairs (one load per drawn agent)
   const GridDev* self;      // device copy of this struct (for out-of-line slow-path helpers)
   const PcgJump* jt8;       // [2][256] radix-256 jumps: d and 256*d steps (fused kernel: jumps < 2^16)
   int32_t xmode;            // fused exchange: 0 = block-0 aggregator + per-tile words, 1 = all-gather
@@ -266,12 +264,8 @@ struct LTabs {
   __device__ __forceinline__ const PcgJump* jt8() const { return reinterpret_cast<const PcgJump*>(dyn + p.lds.jt8.off); }
   __device__ __forceinline__ bool has_ofix() const { return p.lds.ofix.bytes > 0; }
   __device__ __forceinline__ int32_t ofix(int i) const { return at<int32_t>(p.lds.ofix, i); }
-  __device__ __forceinline__ bool has_ngt() const { return p.lds.ngt.bytes > 0; }
-  __device__ __forceinline__ uint8_t ngt(int i) const { return at<uint8_t>(p.lds.ngt, i); }
-  // u32 move-table entry at byte offset `b` (= (cell * NA + action) * 4)
-  __device__ __forceinline__ uint32_t mv32_b(uint32_t b) const {
-    return *reinterpret_cast<const uint32_t*>(dyn + p.lds.mv32.off + b);
-  }
+  __device__ __forceinline__ bool has_avo() const { return p.lds.avo.bytes > 0; }
+  __device__ __forceinline__ uint2 avo(int i) const { return at<uint2>(p.lds.avo, i); }
 };
 
 // ------------------------------------------------------------------ observation builders ----
@@ -934,13 +928,6 @@ constexpr uint32_t TAG_MASK = 0x7FFFu;
 #define GP_CELLENV 1
 #endif
 //  GP_STORE_PRIO: scheduling priority of the store waves (1: above the env waves).
-//  GP_EARLY 1 (staged kernel): the step's reset counts are published BEFORE the transitions: an env can only
-//    terminate this step if it is truncated (known from its elapsed counter) or stands on a cell from which
-//    some move reaches its goal; only those few envs have their draw and move resolved first, and the full
-//    transitions then run while the granule exchange is in flight.
-#ifndef GP_EARLY
-#define GP_EARLY 0
-#endif
 #ifndef GP_STORE_PRIO
 #define GP_STORE_PRIO 1
 #endif
@@ -962,17 +949,10 @@ struct FusedShared {
   uint32_t nh, nu;               // next step's has_uint32 / uinteger
   uint32_t drawn;                // the control wave drew this step's resetter cells before B2
   uint32_t rdone;                // env waves done listing their resetters in renv (monotone)
-  uint32_t ecnt;                 // GP_EARLY: env waves done with their early reset counts (monotone)
-  uint32_t sfree;                // GP_EARLY: store waves done reading a step's staging area (monotone)
   int32_t dof[8];                // goal-direction cell offsets (Hansen goal multiplier)
   uint16_t renv[2][FEPB];        // STG: env (in tile) of resetter rank r of tile q
-  union {
-    struct {
-      uint32_t pos[FEPB];        // slow path: accepted-word positions of one tile's resetters
-      uint32_t pos2[FEPB];
-    };
-    uint4 ures[FENVW][64][2];    // GP_EARLY: each env wave's near-goal envs to resolve (outside the reset phase)
-  };
+  uint32_t pos[FEPB];            // slow path: accepted-word positions of one tile's resetters
+  uint32_t pos2[FEPB];
   alignas(16) uint32_t cell[FMAXQ * FEPB];  // resetter cells (goal | agent << 16) by tile and rank (or env slot)
 };
 
@@ -1271,7 +1251,7 @@ __device__ __forceinline__ void stage_reset_obs(const GridDev& p, const FusedSha
 #pragma unroll
     for (int d = 0; d < 8; ++d) dof[d] = (OK == GP_OBS_HANSEN && d < p.obs_dirs) ? sh.dof[d] : 0x7FFFFFFF;
     reinterpret_cast<int32_t*>(stg + q * STG_TILE_BYTES)[sh.renv[q][r]] =
-        obs_value_r<OK>(p, tb, (int)((cell >> 16) & 0x7FFFu), (int)(cell & 0xFFFFu), dof);
+        obs_value_r<OK>(p, tb, (int)(cell >> 16), (int)(cell & 0xFFFFu), dof);
   }
 }
 // The same with the slot (renv) and the direction offsets already in registers.
@@ -1280,16 +1260,9 @@ __device__ __forceinline__ void stage_reset_obs_r(const GridDev& p, const LTabs&
                                                   uint32_t cell, const int (&dof)[8]) {
   if constexpr (STG)
     reinterpret_cast<int32_t*>(stg + q * STG_TILE_BYTES)[slot] =
-        obs_value_r<OK>(p, tb, (int)((cell >> 16) & 0x7FFFu), (int)(cell & 0xFFFFu), dof);
+        obs_value_r<OK>(p, tb, (int)(cell >> 16), (int)(cell & 0xFFFFu), dof);
 }
 
-// GP_EARLY (staged kernel, fixed goal): a resetter's cell word carries its new cell's near-goal flag in bit 31,
-// which lands in bit 15 of the agent state word (c >> 16).
-template <bool STG>
-__device__ __forceinline__ uint32_t cell_flag(const LTabs& tb, uint32_t agent) {
-  if constexpr (STG && GP_EARLY && GP_TRIMS) return tb.has_ngt() ? (uint32_t)tb.ngt((int)agent) << 31 : 0u;
-  return 0u;
-}
 template <int OK, int QPT, bool STG>
 __device__ __forceinline__ void ctrl_fast_finish(const GridDev& p, FusedShared& sh, const LTabs& tb, const u128 SB,
                                                  const Stream& st, uint32_t b, uint32_t tq, uint32_t pre, char* stg,
@@ -1346,11 +1319,16 @@ __device__ __forceinline__ void ctrl_fast_finish(const GridDev& p, FusedShared& 
     if (cellj) {
       const uint32_t word = buffered ? st.u0 : ((ww & 1u) ? (uint32_t)(x >> 32) : (uint32_t)x);
       const uint32_t v = lemire_value(word, nsel);
-      const uint32_t goal = rgoal ? (uint32_t)tb.gv((int)v) : (uint32_t)p.fixed_goal;
-      const uint32_t agent = rgoal ? (uint32_t)p.fixed_agent : (uint32_t)tb.av((int)v);
-      const uint32_t cw = goal | (agent << 16) | cell_flag<STG>(tb, agent);
-      sh.cell[q * FEPB + ((STG && GP_CELLENV) ? (uint32_t)slot : r)] = cw;
-      stage_reset_obs_r<OK, STG>(p, tb, stg, q, slot, cw, dof);
+      if (OK == GP_OBS_HANSEN && STG && !rgoal && tb.has_avo()) {  // uniform: agent and its obs in one load
+        const uint2 e = tb.avo((int)v);
+        sh.cell[q * FEPB + (GP_CELLENV ? (uint32_t)slot : r)] = (uint32_t)p.fixed_goal | (e.x << 16);
+        reinterpret_cast<int32_t*>(stg + q * STG_TILE_BYTES)[slot] = (int32_t)e.y;
+      } else {
+        const uint32_t goal = rgoal ? (uint32_t)tb.gv((int)v) : (uint32_t)p.fixed_goal;
+        const uint32_t agent = rgoal ? (uint32_t)p.fixed_agent : (uint32_t)tb.av((int)v);
+        sh.cell[q * FEPB + ((STG && GP_CELLENV) ? (uint32_t)slot : r)] = goal | (agent << 16);
+        stage_reset_obs_r<OK, STG>(p, tb, stg, q, slot, goal | (agent << 16), dof);
+      }
     } else if (extra) {
       if (lane == 61) { sh.ju[0] = hi64(X); sh.ju[1] = lo64(X); }
       if (lane == 62) { sh.ju[2] = hi64(X); sh.ju[3] = lo64(X); }
@@ -1398,9 +1376,8 @@ __device__ __forceinline__ void ctrl_draw_cells(const GridDev& p, FusedShared& s
     const uint32_t v = draw_cells(tb.jt8(), tb.jt(), SB, st.h0, st.u0, wg, wa, mode, ng, na);
     const uint32_t goal = rgoal ? (uint32_t)tb.gv((int)(v & 0xFFFFu)) : (uint32_t)p.fixed_goal;
     const uint32_t agent = ragent ? (uint32_t)tb.av((int)(v >> 16)) : (uint32_t)p.fixed_agent;
-    const uint32_t cw = goal | (agent << 16) | cell_flag<STG>(tb, agent);
-    sh.cell[q * FEPB + ((STG && GP_CELLENV) ? (uint32_t)sh.renv[q][r] : r)] = cw;
-    stage_reset_obs<OK, STG>(p, sh, tb, stg, q, r, cw);
+    sh.cell[q * FEPB + ((STG && GP_CELLENV) ? (uint32_t)sh.renv[q][r] : r)] = goal | (agent << 16);
+    stage_reset_obs<OK, STG>(p, sh, tb, stg, q, r, goal | (agent << 16));
   }
 }
 
@@ -1584,31 +1561,6 @@ __device__ __forceinline__ uint32_t fused_effective_action(const uint64_t* s_thr
   return e;
 }
 
-// Can an env on `cell` with goal `goal` terminate this step, i.e. does some effective action's move land on
-// the goal? Fixed goal: one byte of the ngt table; otherwise the cell's move-table row (NA 15-bit cells,
-// blocked moves stay) compared with the goal, two 16-bit fields per word.
-template <int NA, bool TABLE = true>
-__device__ __forceinline__ bool near_goal(const LTabs& tb, uint32_t cell, int goal) {
-  if (TABLE && tb.has_ngt()) return tb.ngt((int)cell) != 0;
-  const char* row = tb.dyn + tb.p.lds.move.off + cell * (uint32_t)(NA * 2);
-  uint32_t w[NA / 2];
-  if constexpr (NA == 4) {
-    const uint2 v = *reinterpret_cast<const uint2*>(row);
-    w[0] = v.x; w[1] = v.y;
-  } else {
-    const uint4 v = *reinterpret_cast<const uint4*>(row);
-    w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
-  }
-  const uint32_t gg = ((uint32_t)goal & 0xFFFFu) * 0x10001u;
-  bool any = false;
-#pragma unroll
-  for (int j = 0; j < NA / 2; ++j) {
-    const uint32_t v = (w[j] ^ gg) & 0x7FFF7FFFu;  // a zero 15-bit field <=> that move lands on the goal
-    any |= ((v + 0x7FFF7FFFu) & 0x80008000u) != 0x80008000u;
-  }
-  return any && (uint32_t)goal < 0x8000u;
-}
-
 // The obs of the previous step's resetters (their provisional obs were stored with the step's
 // outputs): written during the next step's exchange wait.
 template <int OK, int QPT>
@@ -1620,8 +1572,7 @@ __device__ __forceinline__ void flush_reset_obs(const GridDev& p, const LTabs& t
     const int env0 = (q * (int)gridDim.x + (int)blockIdx.x) * FEPB + tid * EPT;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      if ((pfm[q] >> i) & 1u)
-        write_obs<OK>(p, tb, env0 + i, (int)((pc[q][i] >> 16) & 0x7FFFu), (int)(pc[q][i] & 0xFFFFu), ob);
+      if ((pfm[q] >> i) & 1u) write_obs<OK>(p, tb, env0 + i, (int)(pc[q][i] >> 16), (int)(pc[q][i] & 0xFFFFu), ob);
     pfm[q] = 0;
   }
 }
@@ -1653,9 +1604,6 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
   const size_t ow = (size_t)p.obs_width * ((OK == GP_OBS_HANSEN_VEC || OK == GP_OBS_WINDOW) ? 1 : 4);
   const PcgJump jB_unused{0, 1, 0, 0};
   constexpr bool TRIMS = GP_TRIMS;
-  constexpr bool EARLY = STG && GP_EARLY && GP_TRIMS;
-  // early counts need the near-goal flags, i.e. a fixed goal (block-uniform: every role takes the same barriers)
-  const bool early = EARLY && tb.has_ngt();
   uint32_t ae[QPT][4];
   int gl[QPT][4];
   int32_t a_cur[QPT][4];  // TRIMS: threshold-row byte offsets (action_row) instead of raw actions
@@ -1687,10 +1635,6 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
       for (int i = 0; i < 4; ++i) a_cur[q][i] = action_row<NA>(a_cur[q][i]);
     }
     jtile[q] = p.ftj[min(tau, nt - 1)];
-    if (EARLY && tb.has_ngt()) {  // the near-goal flags of the starting cells (bit 15 of the state word)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) ae[q][i] |= (uint32_t)tb.ngt((int)(ae[q][i] & 0x7FFFu)) << 15;
-    }
     vmask[q] = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) vmask[q] |= (STG || env0 + i < B) ? 1u << i : 0u;
@@ -1728,89 +1672,6 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
         }
       }
     }
-    // ---- 0. GP_EARLY: this step's reset counts first (published by the control wave while the full
-    // transitions below run). An env resets iff it is truncated (elapsed counter) or its move lands on the
-    // goal, which needs its draw only when it stands on a near-goal cell: those few envs are compacted into
-    // a per-wave list and resolved one per lane (draw state = jt8[slot] applied to the lane state, i.e. the
-    // same value the transitions compute by pcg_step), then counted per tile. ----
-    if (early) {
-      // truncation from the elapsed counter, near-goal from bit 15 of the state word (set by the previous
-      // step's move-table entry or the resetter's cell word): two compares per env, the masks are ballots
-      uint32_t cnt[QPT];
-      uint64_t um[QPT * 4];
-      uint32_t n = 0;
-#pragma unroll
-      for (int q = 0; q < QPT; ++q) {
-        cnt[q] = 0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const uint64_t trb = __ballot((ae[q][i] >> 16) + 1u > (uint32_t)tlim);
-          const uint64_t ngb = __ballot((ae[q][i] & 0x8000u) != 0u);
-          um[q * 4 + i] = ngb & ~trb;
-          cnt[q] += (uint32_t)__builtin_popcountll(trb);
-          n += (uint32_t)__builtin_popcountll(um[q * 4 + i]);
-        }
-      }
-      STAMP(15);
-      uint4* ent = &sh.ures[wid][0][0];
-      for (uint32_t base = 0; base < n; base += 64) {  // wave-uniform; normally one pass or none
-        uint32_t idx0 = 0;
-#pragma unroll
-        for (int q = 0; q < QPT; ++q)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const uint64_t mk = um[q * 4 + i];
-            if (!mk) continue;  // wave-uniform
-            const uint32_t idx =
-                idx0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u)) -
-                base;
-            if (((mk >> lane) & 1u) && idx < 64u) {
-              ent[idx * 2] = make_uint4((uint32_t)lo64(S[q]), (uint32_t)(lo64(S[q]) >> 32), (uint32_t)hi64(S[q]),
-                                        (uint32_t)(hi64(S[q]) >> 32));
-              ent[idx * 2 + 1] = make_uint4((uint32_t)a_cur[q][i], (ae[q][i] & 0x7FFFu) | ((uint32_t)gl[q][i] << 16),
-                                            (uint32_t)i | ((uint32_t)q << 2), 0u);
-            }
-            idx0 += (uint32_t)__builtin_popcountll(mk);
-          }
-        wave_lds_sync();
-        bool tm = false;
-        uint32_t eq = 0;
-        if ((uint32_t)lane < n - base) {
-          const uint4 e0 = ent[lane * 2], e1 = ent[lane * 2 + 1];
-          const u128 s0 = mk128(((uint64_t)e0.w << 32) | e0.z, ((uint64_t)e0.y << 32) | e0.x);
-          eq = e1.z >> 2;
-          const ulonglong2* jp = reinterpret_cast<const ulonglong2*>(tb.jt8() + (e1.z & 3u));
-          const ulonglong2 ja = jp[0], jc = jp[1];  // one PcgJump {a_hi, a_lo, c_hi, c_lo}: both halves at once
-          uint64_t th[NA];
-          {
-            const ulonglong2* t2 = reinterpret_cast<const ulonglong2*>(reinterpret_cast<const char*>(s_thr) + e1.x);
-#pragma unroll
-            for (int j = 0; j < NA / 2; ++j) {
-              const ulonglong2 v = t2[j];
-              th[2 * j] = v.x;
-              th[2 * j + 1] = v.y;
-            }
-          }
-          const u128 x = apply_jump(PcgJump{ja.x, ja.y, jc.x, jc.y}, s0);
-          const uint64_t xo = pcg_output(x);
-          uint32_t effx = 0;
-#pragma unroll
-          for (int j = 0; j < NA - 1; ++j) effx = xo > th[j] ? (uint32_t)(2 * (j + 1)) : effx;
-          const uint32_t m = tb.mv32_b(((e1.y & 0x7FFFu) << (NA == 4 ? 4 : 5)) + 2 * effx);
-          tm = __builtin_amdgcn_ubfe(m, 0, 15) == (e1.y >> 16);
-        }
-#pragma unroll
-        for (int q = 0; q < QPT; ++q) cnt[q] += (uint32_t)__builtin_popcountll(__ballot(tm && eq == (uint32_t)q));
-        wave_lds_sync();
-      }
-      if (lane == 0) {
-#pragma unroll
-        for (int q = 0; q < QPT; ++q) sh.wcnt[q][wid] = cnt[q];
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-      if (lane == 0) __hip_atomic_fetch_add(&sh.ecnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      STAMP(14);
-    }
     // ---- 1. draws + transitions (the critical path) ----
     uint32_t fm[QPT], tmm[QPT], trm[QPT], bkm[QPT], excl[QPT], wex[QPT], wt[QPT];
     u128 sd[QPT];  // draw states of the tiles' current env slots
@@ -1832,18 +1693,17 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
         if constexpr (TRIMS) {
           const uint32_t effx =
               fused_effx_row<NA>(s_thr, a_cur[q][i], GP_ALIGNBIT ? pcg_output_ab(s) : pcg_output(s));
-          if constexpr (EARLY) m = tb.mv32_b(((s_ae & 0x7FFFu) << (NA == 4 ? 4 : 5)) + 2 * effx);
-          else m = tb.move_b(((s_ae & 0x7FFFu) << (NA == 4 ? 3 : 4)) + effx);
+          m = tb.move_b(((s_ae & 0xFFFFu) << (NA == 4 ? 3 : 4)) + effx);
         } else {
           const uint64_t k53 = pcg_output(s) >> 11;
           int a = a_cur[q][i];
           if (a < 0) a += NA;                 // numpy negative indexing of action_matrix[action]
           a = min(max(a, 0), NA - 1);         // (out-of-range actions raise in the reference; clamped here)
           const uint32_t eff = fused_effective_action<NA>(s_thr, a, k53);
-          m = tb.move((int)(s_ae & 0x7FFFu) * NA + (int)eff);
+          m = tb.move((int)(s_ae & 0xFFFFu) * NA + (int)eff);
         }
         const int na_ = (int)__builtin_amdgcn_ubfe(m, 0, 15);
-        const bool blocked = EARLY ? ((m >> 16) & 1u) != 0 : (m >> 15) != 0;
+        const bool blocked = (m >> 15) != 0;
         const uint32_t el = (s_ae >> 16) + 1u;
         const bool tm_ = na_ == gl[q][i];
         const bool tr_ = el > (uint32_t)tlim;
@@ -1854,10 +1714,8 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
         bkm[q] |= (uint32_t)blocked << i;
         trm[q] |= (uint32_t)tr_ << i;
         fm[q] |= (uint32_t)f << i;
-        // EARLY: m's low half is the new cell with its near-goal flag (fa16: the fixed agent's)
-        const uint32_t ag = EARLY ? (f && fixed_agent >= 0 ? (uint32_t)p.fa16 : (m & 0xFFFFu))
-                                  : (uint32_t)(f && fixed_agent >= 0 ? fixed_agent : na_);
-        ae[q][i] = ag | ((f ? 0u : el) << 16);
+        const int ag = f && fixed_agent >= 0 ? fixed_agent : na_;
+        ae[q][i] = (uint32_t)ag | ((f ? 0u : el) << 16);
         if (f && fixed_goal >= 0) gl[q][i] = fixed_goal;
         if constexpr (!GP_ACC) {
           if (valid) {
@@ -1884,17 +1742,10 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
 #pragma unroll
     for (int q = 0; q < QPT; ++q) {
       wave_count_prefix((uint32_t)__builtin_popcount(fm[q]), wex[q], wt[q]);
-      if (!early && lane == 0) sh.wcnt[q][wid] = wt[q];
+      if (lane == 0) sh.wcnt[q][wid] = wt[q];
     }
     STAMP(1);
-    if (early) {  // every env wave's early count is in LDS (long since, normally)
-      const uint32_t want = (uint32_t)FENVW * (uint32_t)(k + 1);
-      while (__hip_atomic_load(&sh.ecnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want)
-        __builtin_amdgcn_s_sleep(1);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-    } else {
-      lds_barrier();  // B1: per-wave reset counts are in LDS
-    }
+    lds_barrier();  // B1: per-wave reset counts are in LDS
     STAMP(2);
 #pragma unroll
     for (int q = 0; q < QPT; ++q) {
@@ -1929,23 +1780,17 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
     if constexpr (STG) {
       // into the LDS staging area; the store waves move it to HBM during the next VALU phases, so
       // no global store competes with the exchange (resetters' obs: written by the control wave)
-      if (early) {  // the store waves have read the previous step's staging (no B1 any more)
-        const uint32_t want = (uint32_t)FSTW * (uint32_t)k;
-        while (__hip_atomic_load(&sh.sfree, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want)
-          __builtin_amdgcn_s_sleep(1);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-      }
       int32_t obv[QPT][4];
       if (OK == GP_OBS_HANSEN && tb.has_ofix()) {  // uniform: the fixed-goal table, all loads in flight together
 #pragma unroll
         for (int q = 0; q < QPT; ++q)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) obv[q][i] = tb.ofix((int)(ae[q][i] & 0x7FFFu));
+          for (int i = 0; i < 4; ++i) obv[q][i] = tb.ofix((int)(ae[q][i] & 0xFFFFu));
       } else {
 #pragma unroll
         for (int q = 0; q < QPT; ++q)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) obv[q][i] = obs_value_r<OK>(p, tb, (int)(ae[q][i] & 0x7FFFu), gl[q][i], dof);
+          for (int i = 0; i < 4; ++i) obv[q][i] = obs_value_r<OK>(p, tb, (int)(ae[q][i] & 0xFFFFu), gl[q][i], dof);
       }
 #pragma unroll
       for (int q = 0; q < QPT; ++q) {
@@ -1993,7 +1838,7 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
         for (int i = 0; i < 4; ++i) {
           tm[i] = (uint8_t)((tmm[q] >> i) & 1u);
           tr[i] = (uint8_t)((trm[q] >> i) & 1u);
-          ag[i] = (int)(ae[q][i] & 0x7FFFu);
+          ag[i] = (int)(ae[q][i] & 0xFFFFu);
           rw[i] = tm[i] ? r_goal : (((bkm[q] >> i) & 1u) ? r_wall : r_step);
         }
         store4f<float>(rew + off, env0, B, rw);
@@ -2060,8 +1905,6 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
 #pragma unroll
   for (int q = 0; q < QPT; ++q) {
     const int env0 = (q * G + (int)blockIdx.x) * FEPB + tid * EPT;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) ae[q][i] &= 0xFFFF7FFFu;  // the near-goal flag lives only inside a launch
     store4f<uint32_t>(p.ae, env0, B, ae[q]);
     if (rgoal) {
       uint16_t gg[4];
@@ -2077,8 +1920,6 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
 template <int OK, int QPT, bool STG>
 __device__ __forceinline__ void fused_ctrl(const GridDev& p_in, FusedShared& sh, const LTabs& tb, char* stg, int K) {
   constexpr int NC = (QPT + 1) / 2;  // checker states per lane (32 lanes per tile)
-  constexpr bool EARLY = STG && GP_EARLY && GP_TRIMS;
-  const bool early = EARLY && tb.has_ngt();
   const GridDev& p = p_in;
   const int tid = threadIdx.x, lane = tid & 63;
   GridCtl* C = p.ctl;
@@ -2141,14 +1982,7 @@ __device__ __forceinline__ void fused_ctrl(const GridDev& p_in, FusedShared& sh,
     }
     const uint32_t wrej = __any((int)crej) ? 1u : 0u;
     const u128 SB = apply_jump(jB, st.s0);  // state after random(B): base of the word stream
-    if (early) {  // the env waves' early reset counts
-      const uint32_t want = (uint32_t)FENVW * (uint32_t)(k + 1);
-      while (__hip_atomic_load(&sh.ecnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want)
-        __builtin_amdgcn_s_sleep(1);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-    } else {
-      lds_barrier();  // B1
-    }
+    lds_barrier();  // B1
     // ---- 2. publish this block's granule ----
     uint32_t tq = 0;
     if (lane < QPT) {
@@ -2243,11 +2077,6 @@ __device__ __forceinline__ void fused_ctrl(const GridDev& p_in, FusedShared& sh,
       const uint32_t want = (uint32_t)FENVW * (uint32_t)(k + 1);
       while (__hip_atomic_load(&sh.rdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want)
         __builtin_amdgcn_s_sleep(1);
-      if (early) {  // and the store waves are done with the previous step's staging
-        const uint32_t wants = (uint32_t)FSTW * (uint32_t)k;
-        while (__hip_atomic_load(&sh.sfree, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < wants)
-          __builtin_amdgcn_s_sleep(1);
-      }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
     }
     if (drawn) {
@@ -2348,8 +2177,6 @@ __device__ __forceinline__ void fused_store(const GridDev& p, FusedShared& sh, c
   const uint32_t step_base = p.ctl->step;
   const Stream st{};
   const PcgJump jB{0, 1, 0, 0};
-  constexpr bool EARLY = STG && GP_EARLY && GP_TRIMS;
-  const bool early = EARLY && tb.has_ngt();
   uint32_t du[QPT][4], dp[QPT] = {};
   int di[QPT][4];
   int32_t dov[QPT][4];
@@ -2358,62 +2185,14 @@ __device__ __forceinline__ void fused_store(const GridDev& p, FusedShared& sh, c
   for (int k = 0; k < K; ++k) {
     const uint32_t tag0 = (step_base + (uint32_t)k + 1u) * 4u;
     uint64_t* slots = p.fslot + (size_t)((step_base + (uint32_t)k) & 1u) * 3 * G;
-    if (!early) lds_barrier();  // B1
+    lds_barrier();  // B1
     lds_barrier();  // B2
     fused_resets<OK, QPT, R_PASS>(p, sh, tb, st, (u128)0, jB, slots, tag0, du, di, dc, dc, du, dp);
-    if constexpr (EARLY) {
-      // the whole step's staging into registers (10 chunks of 16 B per lane and tile), then the area is
-      // released to the env waves and the control wave (sfree) and the stores drain from registers
-      size_t off = (size_t)k * B;
-#ifdef GP_STAMPS
-      if (p.xmode & 8) off = 0;
-#endif
-      char* dsts[4] = {(char*)obs + off * 4, (char*)(rew + off), (char*)(term + off), (char*)(trunc + off)};
-      const bool a16 = ((((uintptr_t)dsts[0]) | ((uintptr_t)dsts[1]) | ((uintptr_t)dsts[2]) | ((uintptr_t)dsts[3])) & 15) == 0;
-      if (a16) {
-        constexpr int NL = FSTW * 64, NCH = STG_TILE_BYTES / 16 / NL;  // 10
-        static_assert(STG_TILE_BYTES % (16 * NL) == 0 && (FEPB * 4) % (16 * NL) == 0 && FEPB % (16 * NL) == 0,
-                      "staging planes split evenly over the store lanes");
-        u32x4 v[QPT][NCH];
-#pragma unroll
-        for (int q = 0; q < QPT; ++q)
-#pragma unroll
-          for (int j = 0; j < NCH; ++j) v[q][j] = reinterpret_cast<const u32x4*>(stg + q * STG_TILE_BYTES)[sl + j * NL];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-        if ((sl & 63) == 0) __hip_atomic_fetch_add(&sh.sfree, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#ifdef GP_STAMPS
-        if (p.xmode & 4) continue;
-#endif
-#pragma unroll
-        for (int q = 0; q < QPT; ++q) {
-          const size_t e0 = (size_t)(q * G + (int)blockIdx.x) * FEPB;
-#pragma unroll
-          for (int j = 0; j < NCH; ++j) {
-            // chunk c of the tile: [0, FEPB/4) obs, then rewards, then the two flag planes
-            const int c = sl + j * NL;
-            constexpr int O4 = FEPB / 4, R4 = FEPB / 2, T4 = FEPB / 2 + FEPB / 16;
-            char* d = j < O4 / NL ? dsts[0] + e0 * 4 + (size_t)c * 16
-                    : j < R4 / NL ? dsts[1] + e0 * 4 + (size_t)(c - O4) * 16
-                    : j < T4 / NL ? dsts[2] + e0 + (size_t)(c - R4) * 16
-                                  : dsts[3] + e0 + (size_t)(c - T4) * 16;
-            if (nt) __builtin_nontemporal_store(v[q][j], reinterpret_cast<u32x4*>(d));
-            else *reinterpret_cast<u32x4*>(d) = v[q][j];
-          }
-        }
-        continue;
-      }
-    }
     if constexpr (STG) {
       size_t off = (size_t)k * B;
-      auto release = [&]() {  // GP_EARLY: staging read (the copies below wait for their LDS loads)
-        if constexpr (EARLY) {
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-          if ((sl & 63) == 0) __hip_atomic_fetch_add(&sh.sfree, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-      };
 #ifdef GP_STAMPS
       if (p.xmode & 8) off = 0;  // diagnostic: every step writes the first step's slice
-      if (p.xmode & 4) { release(); continue; }  // diagnostic: no output stores
+      if (p.xmode & 4) continue;  // diagnostic: no output stores
 #endif
 #pragma unroll
       for (int q = 0; q < QPT; ++q) {
@@ -2431,7 +2210,6 @@ __device__ __forceinline__ void fused_store(const GridDev& p, FusedShared& sh, c
         if (tau >= p.fnt) continue;
         stage_plane(stg + q * STG_TILE_BYTES, (char*)obs + off * 4, tau * FEPB, B, 4, sl, nt);
       }
-      release();
     }
   }
 }
@@ -2457,7 +2235,7 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
   if (tid < NA * NA) s_thr[tid] = GP_TRIMS ? thr_on_u64(p.thr[tid]) : p.thr[tid];
   lds_image_copy(dyn, p.limg, p.lds.total);
   if (tid < 4) sh.jB[tid] = (&p.fjB->a_hi)[tid];
-  if (tid == 0) { sh.rdone = 0; sh.ecnt = 0; sh.sfree = 0; }
+  if (tid == 0) sh.rdone = 0;
   if (tid < 8) sh.dof[tid] = (OK == GP_OBS_HANSEN && p.doff && tid < p.obs_dirs) ? p.doff[tid] : 0x7FFFFFFF;
   __syncthreads();
   LSTAMP(1);
@@ -2661,7 +2439,7 @@ struct GridBackend : EnvBackend {
   std::vector<uint16_t> goal_valid_h, agent_valid_h;
   DevBuf b_move, b_thr, b_gv, b_av, b_hbase, b_doff, b_hvec, b_t1, b_t2, b_coords, b_window, b_jt, b_lt4, b_lt2,
       b_tja, b_tjw, b_ae, b_goal, b_ctl, b_tcount, b_tlist, b_rflag, b_mslot, b_ftj, b_flt4, b_fjB, b_fslot, b_dbg, b_self, b_jt8,
-      b_limg, b_ofix, b_ngt, b_mv32;
+      b_limg, b_ofix, b_avo;
   int fused_G = 0, fused_qpt = 0;  // fused numpy rollout geometry (0 = not eligible)
   bool fused_stg = false;          // outputs staged in LDS and written by the store waves
   // replay pointers for the next step
@@ -2847,7 +2625,7 @@ int GridBackend::refresh_lds_image() {
       (e = put(d.lds.t1, d.t1)) || (e = put(d.lds.t2, d.t2)) || (e = put(d.lds.coords, d.coords)) ||
       (e = put(d.lds.window, d.window)) || (e = put(d.lds.gv, d.goal_valid)) || (e = put(d.lds.av, d.agent_valid)) ||
       (e = put(d.lds.doff, d.doff)) || (e = put(d.lds.jt, d.jt)) || (e = put(d.lds.jt8, d.jt8)) ||
-      (e = put(d.lds.ofix, d.ofix)) || (e = put(d.lds.ngt, d.ngt)) || (e = put(d.lds.mv32, d.mv32)))
+      (e = put(d.lds.ofix, d.ofix)) || (e = put(d.lds.avo, d.avo)))
     return e;
   GP_HIP_CHECK(hipDeviceSynchronize());
   return GP_OK;
@@ -3172,25 +2950,6 @@ int GridBackend::build(const gp_grid_config* cfg) {
       hbase[c] = hb;
     }
   }
-  // fixed goal: the cells from which some effective action's move lands on the goal (the fused kernel's early
-  // reset count resolves only envs on such cells; an off-grid goal is never reached)
-  std::vector<uint8_t> ngt;
-  if (d.fixed_goal >= 0) {
-    ngt.assign(nc, 0);
-    if (d.fixed_goal < nc)
-      for (int c = 0; c < nc; ++c)
-        for (int a = 0; a < nact; ++a)
-          if ((move[(size_t)c * nact + a] & 0x7FFF) == d.fixed_goal) ngt[c] = 1;
-  }
-  // the early-count kernel's move table: the near-goal flag of the destination rides in bit 15, so the
-  // transitions produce next step's flag with the new cell (agent state word: cell | flag << 15 | elapsed << 16)
-  std::vector<uint32_t> mv32((size_t)nc * nact);
-  for (size_t j = 0; j < mv32.size(); ++j) {
-    const uint32_t dest = move[j] & 0x7FFFu;
-    mv32[j] = dest | ((!ngt.empty() && ngt[dest]) ? 0x8000u : 0u) | ((uint32_t)(move[j] >> 15) << 16);
-  }
-  d.fa16 = d.fixed_agent < 0 ? -1
-                             : (d.fixed_agent | ((!ngt.empty() && d.fixed_agent < nc && ngt[d.fixed_agent]) ? 0x8000 : 0));
   // Hansen obs with a fixed goal: a table over the agent cell (obs_value's goal multiplier folded in)
   std::vector<int32_t> ofix;
   if (cfg->obs_kind == GP_OBS_HANSEN && d.fixed_goal >= 0) {
@@ -3203,6 +2962,14 @@ int GridBackend::build(const gp_grid_config* cfg) {
           if (diff == doff[i]) mult = i + 1;
       }
       ofix[c] = (int32_t)hbase[c] * mult;
+    }
+  }
+  std::vector<uint32_t> avo;
+  if (!ofix.empty()) {
+    avo.resize(2 * agent_valid_h.size());
+    for (size_t j = 0; j < agent_valid_h.size(); ++j) {
+      avo[2 * j] = agent_valid_h[j];
+      avo[2 * j + 1] = (uint32_t)ofix[agent_valid_h[j]];
     }
   }
   std::vector<uint8_t> window;
@@ -3256,7 +3023,7 @@ int GridBackend::build(const gp_grid_config* cfg) {
   int e;
   if ((e = b_move.upload(move)) || (e = b_thr.upload(thr)) || (e = b_gv.upload(goal_valid_h)) ||
       (e = b_av.upload(agent_valid_h)) || (e = b_hbase.upload(hbase)) || (e = b_doff.upload(doff)) ||
-      (e = b_ofix.upload(ofix)) || (e = b_ngt.upload(ngt)) || (e = b_mv32.upload(mv32)) ||
+      (e = b_ofix.upload(ofix)) || (e = b_avo.upload(avo)) ||
       (e = b_hvec.upload(hvec)) || (e = b_coords.upload(coords)) || (e = b_window.upload(window)) ||
       (e = b_t1.upload(t1)) || (e = b_t2.upload(t2)))
     return e;
@@ -3290,8 +3057,7 @@ int GridBackend::build(const gp_grid_config* cfg) {
     put(d.lds.av, agent_valid_h.size() * sizeof(uint16_t));
     put(d.lds.doff, doff.size() * sizeof(int32_t));
     put(d.lds.ofix, ofix.size() * sizeof(int32_t));
-    put(d.lds.ngt, ngt.size());
-    put(d.lds.mv32, GP_EARLY ? mv32.size() * sizeof(uint32_t) : 0);
+    put(d.lds.avo, avo.size() * sizeof(uint32_t));
     put(d.lds.jt, sizeof(PcgJump) * JT_LEVELS * JT_RADIX);
     put(d.lds.jt8, sizeof(PcgJump) * 2 * 256);
     d.lds.total = off <= LDS_TABLE_BUDGET ? off : 0;
@@ -3352,8 +3118,7 @@ int GridBackend::build(const gp_grid_config* cfg) {
   d.hbase = b_hbase.as<uint32_t>();
   d.doff = b_doff.as<int32_t>();
   d.ofix = ofix.empty() ? nullptr : b_ofix.as<int32_t>();
-  d.ngt = ngt.empty() ? nullptr : b_ngt.as<uint8_t>();
-  d.mv32 = b_mv32.as<uint32_t>();
+  d.avo = avo.empty() ? nullptr : b_avo.as<uint32_t>();
   d.hvec = b_hvec.as<uint8_t>();
   d.t1 = t1.empty() ? nullptr : b_t1.as<int32_t>();
   d.t2 = t2.empty() ? nullptr : b_t2.as<int32_t>();
