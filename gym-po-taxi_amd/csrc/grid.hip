@@ -2731,7 +2731,7 @@ int GridBackend::step(const void* act, void* obs, float* rew, uint8_t* term, uin
       timer2.begin(s);
       hipLaunchKernelGGL(grid_resolve_numpy<OK>, dim3(gp), dim3(TPB), 0, s, d, obs, 0, (uint32_t)B);
       timer2.end(s);
-      // keep the fused kernels' step counter meaningful for mixed use
+      // (the fused kernels' tags continue from GridCtl::step: the two-kernel path never touches their slots)
     } else if (rng_mode == GP_RNG_PHILOX) {
       timer.begin(s);
       hipLaunchKernelGGL((grid_rollout_counter<OK, false>), dim3(d.nblk), dim3(TPB), 0, s, d, 1, philox_step,

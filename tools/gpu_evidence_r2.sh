@@ -5,6 +5,7 @@
 #  3. bench lines: headline at the driver config (--steps 20 --warmup 5, with CPU baseline) and steady state
 #     (--steps 2000), the other workloads at their defaults (with CPU baselines);
 #  4. rocprofv3 --kernel-trace --stats of the headline at both shapes.
+# FR_ONLY=1: only the headline (FourRooms) parts, after a change to its kernel alone.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/ev2
@@ -23,7 +24,7 @@ pmc() {  # workload chunk steps warmup tag
 }
 pmc fourrooms 128 256 128 fr128 || exit 1
 pmc fourrooms 20 200 100 fr20 || exit 1
-for W in taxi crooms anttag; do pmc $W ${CH[$W]} 256 128 $W || exit 1; done
+if [ -z "$FR_ONLY" ]; then for W in taxi crooms anttag; do pmc $W ${CH[$W]} 256 128 $W || exit 1; done; fi
 echo PMC_OK
 i=0
 for C in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVE_CYCLES" \
@@ -36,9 +37,9 @@ echo SQ_OK
 timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_fourrooms_driver.log 2>&1 || { echo BENCH_FAIL driver; tail -30 $O/bench_fourrooms_driver.log; exit 1; }
 tail -n 1 $O/bench_fourrooms_driver.log | cut -c 1-400
 timeout -k 10 300 python bench.py --steps 2000 --warmup 200 --no-cpu-baseline > $O/bench_fourrooms_steady.log 2>&1 || { echo BENCH_FAIL steady; tail -30 $O/bench_fourrooms_steady.log; exit 1; }
-for W in taxi crooms anttag; do
+if [ -z "$FR_ONLY" ]; then for W in taxi crooms anttag; do
   timeout -k 10 400 python bench.py --workload $W > $O/bench_$W.log 2>&1 || { echo "BENCH_FAIL $W"; tail -30 $O/bench_$W.log; exit 1; }
-done
+done; fi
 for f in $O/bench_*.log; do python3 -c "import json,sys; d=json.loads(open('$f').read().strip().splitlines()[-1]); r=d['roofline']; print('$f'.split('/')[-1], 'value %.4e'%d['value'], 'ms/step %.5f'%d['ms_per_step'], 'frac %.3f'%r['frac'], 'traffic/alg', r.get('traffic_over_algorithmic'))"; done
 echo BENCH_OK
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_driver -o bench -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/prof_driver.log 2>&1 || { echo PROF_FAIL; tail -20 $O/prof_driver.log; exit 1; }
