@@ -350,6 +350,15 @@ int gp_taxi_reset_distribution(const gp_env* env, double* out, int cap) {
   return env->be->reset_distribution(out, cap);
 }
 
+int gp_taxi_render(gp_env* env, int n, int hansen_highlight, uint8_t* out, int32_t dims[4], void* stream) {
+  GP_REQUIRE_ENV();
+  if (!dims) {
+    gp_set_error("gp_taxi_render: dims is required");
+    return GP_E_INVALID;
+  }
+  return env->be->render(n, hansen_highlight, out, dims, (hipStream_t)stream);
+}
+
 int gp_set_profiling(gp_env* env, int enable) {
   GP_REQUIRE_ENV();
   env->be->timer.on = enable != 0;

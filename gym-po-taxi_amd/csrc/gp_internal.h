@@ -81,6 +81,11 @@ struct EnvBackend {
     gp_set_error("no reset distribution for this env kind");
     return GP_E_UNSUPPORTED;
   }
+  // rgb_array frames of envs 0..n-1, tiled (gp_taxi_render)
+  virtual int render(int n, int hansen, uint8_t* out, int32_t dims[4], hipStream_t s) {
+    gp_set_error("rendering is not available for this env kind (the reference does not render it either)");
+    return GP_E_UNSUPPORTED;
+  }
   size_t obs_elem_size() const { return obs_dtype == GP_DTYPE_U8 ? 1 : (obs_dtype == GP_DTYPE_F64 ? 8 : 4); }
   virtual size_t rollout_action_bytes_per_env() const { return 4; }
 };

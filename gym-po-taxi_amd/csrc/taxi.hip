@@ -361,6 +361,82 @@ __global__ void taxi_set_state(TaxiDev p, const int32_t* s, const int32_t* elaps
   p.st[env] = u;
 }
 
+// ------------------------------------------------------------------ rendering ----
+// TaxiVecEnv.render (extended_taxi.py:289-309) -> str_map_to_img (:121-143) -> tile_images (render_utils.py:63-88):
+// one thread per pixel of the tiled frame. Frame k (env k) sits at tile (k / TW, k % TW); its char map is the
+// bordered map with 'D' (destination), 'T' (taxi), 'P' (waiting passenger), 'F' (taxi with passenger) and
+// "TP" -> 'T' where the waiting passenger shares the taxi's cell (the reference's '<U1' array truncates it).
+struct TaxiRender {
+  const uint32_t* st;    // packed env state (s | nd << 12 | elapsed << 16)
+  const uint8_t* desc;   // [DR][DC] bordered char map
+  const int32_t* lrc;    // [L][2] bordered (row, col) of each location
+  int32_t DR, DC, C, L, pseudo, n, TW, rows, cols, hansen;
+};
+__global__ void taxi_render_kernel(TaxiRender p, uint8_t* out) {
+  const int pix = blockIdx.x * TPB + threadIdx.x;
+  if (pix >= p.rows * p.cols) return;
+  const int y = pix / p.cols, x = pix - y * p.cols;
+  const int ty = y / p.DR, tx = x / p.DC, r = y - ty * p.DR, c = x - tx * p.DC;
+  const int k = ty * p.TW + tx;
+  uint8_t rgb[3] = {0, 0, 0};  // padding frames are black
+  if (k < p.n) {
+    const int s = (int)(p.st[k] & 0xFFFu);
+    const int d = s % p.L, t = s / p.L, pp = t % (p.L + 1), t2 = t / (p.L + 1);
+    const int tr = t2 / p.C + 1, tc = p.pseudo ? 2 * (t2 % p.C) + 1 : t2 % p.C + 1;
+    char ch = (char)p.desc[r * p.DC + c];
+    if (r == p.lrc[2 * d] && c == p.lrc[2 * d + 1]) ch = 'D';
+    const bool at_taxi = r == tr && c == tc;
+    if (at_taxi) ch = 'T';
+    if (pp < p.L) {
+      const int pr = p.lrc[2 * pp], pc = p.lrc[2 * pp + 1];
+      if (r == pr && c == pc) ch = (pr == tr && pc == tc) ? 'T' : 'P';
+    } else if (at_taxi) {
+      ch = 'F';
+    }
+    switch (ch) {  // render_utils.py:11-24 palette
+      case '|': break;                                          // WALL black
+      case 'P': rgb[0] = 128; rgb[2] = 128; break;              // PASSENGER purple
+      case 'T': rgb[0] = 128; rgb[1] = 128; break;              // TAXI yellow
+      case 'F': rgb[1] = 128; break;                            // FULL_TAXI green
+      case 'D': rgb[2] = 128; break;                            // DESTINATION blue
+      case ' ': rgb[0] = rgb[1] = rgb[2] = 96; break;           // FLOOR gray_mid_dark
+      case ':': rgb[1] = 128; rgb[2] = 128; break;              // FAKE_WALL teal
+      default: rgb[0] = rgb[1] = rgb[2] = 191; break;           // LOC gray_light
+    }
+    // Hansen highlight (:136-142): the taxi's four orthogonal neighbours +64, wrapping
+    if (p.hansen && ((r == tr && (c == tc - 1 || c == tc + 1)) || (c == tc && (r == tr - 1 || r == tr + 1))))
+      for (int j = 0; j < 3; ++j) rgb[j] = (uint8_t)(rgb[j] + 64);
+  }
+  uint8_t* o = out + (size_t)pix * 3;
+  o[0] = rgb[0]; o[1] = rgb[1]; o[2] = rgb[2];
+}
+
+// cv2.resize(..., INTER_AREA) outside the decimation case (OpenCV resizeGeneric_ with area coefficients, 11-bit
+// fixed point; restated, see oracle/render.py): per destination pixel and channel.
+struct ResizeArea {
+  const uint8_t* src;
+  const int32_t* xofs;   // [dw] source column
+  const int16_t* xa;     // [dw][2]
+  const int32_t* yofs;   // [dh] source row
+  const int16_t* yb;     // [dh][2]
+  int32_t sh, sw, ch, dh, dw, dpitch;
+};
+__global__ void resize_area_kernel(ResizeArea p, uint8_t* dst) {
+  const int i = blockIdx.x * TPB + threadIdx.x;
+  if (i >= p.dh * p.dw * p.ch) return;
+  const int k = i % p.ch, t = i / p.ch, dx = t % p.dw, dy = t / p.dw;
+  const int x0 = p.xofs[dx], x1 = min(x0 + 1, p.sw - 1);
+  const int y0 = min(max(p.yofs[dy], 0), p.sh - 1), y1 = min(max(p.yofs[dy] + 1, 0), p.sh - 1);
+  const int a0 = p.xa[2 * dx], a1 = p.xa[2 * dx + 1];
+  const uint8_t* r0 = p.src + (size_t)y0 * p.sw * p.ch;
+  const uint8_t* r1 = p.src + (size_t)y1 * p.sw * p.ch;
+  const int S0 = r0[x0 * p.ch + k] * a0 + r0[x1 * p.ch + k] * a1;  // HResizeLinear (int)
+  const int S1 = r1[x0 * p.ch + k] * a0 + r1[x1 * p.ch + k] * a1;
+  const int b0 = p.yb[2 * dy], b1 = p.yb[2 * dy + 1];
+  const int v = (((b0 * (S0 >> 4)) >> 16) + ((b1 * (S1 >> 4)) >> 16) + 2) >> 2;  // VResizeLinear<uchar>
+  dst[(size_t)dy * p.dpitch + (size_t)dx * p.ch + k] = (uint8_t)min(max(v, 0), 255);
+}
+
 // ------------------------------------------------------------------ host backend ----
 struct TaxiBackend : EnvBackend {
   TaxiDev d{};
@@ -512,6 +588,27 @@ struct TaxiBackend : EnvBackend {
     for (int k = 0; k < (int)law.size() && k < cap; ++k) out[k] = law[k];
     return (int)law.size();
   }
+  // rendering: bordered map + location coordinates on the device
+  DevBuf b_rdesc, b_rlocs;
+  int rDR = 0, rDC = 0, rC = 0, rpseudo = 0;
+  int render(int n, int hansen, uint8_t* out, int32_t dims[4], hipStream_t s) override {
+    if (n < 1 || n > B || n > 65536) {
+      gp_set_error("taxi render: n=%d outside [1, min(num_envs, 65536)]", n);
+      return GP_E_INVALID;
+    }
+    const int TH = (int)std::ceil(std::sqrt((double)n)), TW = (int)std::ceil((double)n / TH);  // tile_images
+    dims[0] = TH * rDR;
+    dims[1] = TW * rDC;
+    dims[2] = rDR;
+    dims[3] = rDC;
+    if (!out) return GP_OK;
+    TaxiRender p{d.st, b_rdesc.as<uint8_t>(), b_rlocs.as<int32_t>(), rDR, rDC, rC, d.nlocs, rpseudo, n, TW,
+                 dims[0], dims[1], hansen != 0};
+    const int npix = dims[0] * dims[1];
+    hipLaunchKernelGGL(taxi_render_kernel, dim3((npix + TPB - 1) / TPB), dim3(TPB), 0, s, p, out);
+    GP_HIP_CHECK(hipGetLastError());
+    return GP_OK;
+  }
 };
 
 int TaxiBackend::build(const gp_taxi_config* cfg) {
@@ -648,6 +745,22 @@ int TaxiBackend::build(const gp_taxi_config* cfg) {
   obs_dtype = one_hot ? GP_DTYPE_U8 : GP_DTYPE_I32;
   obs_width = one_hot ? d.n_obs : 1;
 
+  {  // render tables: the bordered map and each location's bordered (row, col)
+    std::vector<uint8_t> rd((size_t)DR * DC);
+    for (int r = 0; r < DR; ++r)
+      for (int c = 0; c < DC; ++c) rd[(size_t)r * DC + c] = (uint8_t)desc(r, c);
+    std::vector<int32_t> rl(2 * L);
+    for (int i = 0; i < L; ++i) {
+      rl[2 * i] = cc_r(loc_r[i]);
+      rl[2 * i + 1] = cc_c(loc_c[i]);
+    }
+    if (int e = b_rdesc.upload(rd)) return e;
+    if (int e = b_rlocs.upload(rl)) return e;
+    rDR = DR;
+    rDC = DC;
+    rC = C;
+    rpseudo = pseudo ? 1 : 0;
+  }
   if (int e = b_st.alloc((size_t)B * 4 + 16)) return e;
   d.st = b_st.as<uint32_t>();
   // persistent grid: as many blocks as are co-resident, capped by the number of tiles
@@ -696,4 +809,56 @@ std::unique_ptr<EnvBackend> make_taxi_backend(const gp_taxi_config* cfg, int64_t
     return nullptr;
   }
   return be;
+}
+
+// ------------------------------------------------------------------ C ABI: resize ----
+// OpenCV resizeGeneric_ coefficient setup for INTER_AREA outside decimation (resize.cpp: sx = floor(dx*scale),
+// fx = (float)((dx+1) - (sx+1)*inv_scale), fx = fx <= 0 ? 0 : fx - floor(fx); alpha = saturate_cast<short>
+// (c * 2048)); `clamp`: the horizontal setup pins the last source column.
+static void area_coeffs(int ssize, int dsize, bool clamp, std::vector<int32_t>& ofs, std::vector<int16_t>& a) {
+#pragma clang fp contract(off)
+  const double inv_scale = (double)dsize / ssize, scale = 1. / inv_scale;
+  ofs.resize(dsize);
+  a.resize(2 * (size_t)dsize);
+  for (int dx = 0; dx < dsize; ++dx) {
+    int sx = (int)std::floor(dx * scale);
+    float fx = (float)((dx + 1) - (sx + 1) * inv_scale);
+    fx = fx <= 0 ? 0.f : fx - (float)std::floor(fx);
+    if (clamp && sx >= ssize - 1) {
+      fx = 0.f;
+      sx = ssize - 1;
+    }
+    ofs[dx] = sx;
+    a[2 * dx] = (int16_t)std::lrint((1.f - fx) * 2048.f);
+    a[2 * dx + 1] = (int16_t)std::lrint(fx * 2048.f);
+  }
+}
+
+extern "C" int gp_resize_area_u8(const uint8_t* src, int sh, int sw, int ch, uint8_t* dst, int dh, int dw,
+                                 int dst_pitch, void* stream) {
+  if (!src || !dst || sh < 1 || sw < 1 || ch < 1 || ch > 4 || dh < 1 || dw < 1 || dst_pitch < dw * ch) {
+    gp_set_error("gp_resize_area_u8: bad arguments");
+    return GP_E_INVALID;
+  }
+  if (dh <= sh && dw <= sw && !(dh == sh && dw == sw)) {
+    gp_set_error("gp_resize_area_u8: INTER_AREA decimation (both axes shrink) is not implemented");
+    return GP_E_UNSUPPORTED;
+  }
+  std::vector<int32_t> xo, yo;
+  std::vector<int16_t> xa, yb;
+  area_coeffs(sw, dw, true, xo, xa);
+  area_coeffs(sh, dh, false, yo, yb);
+  DevBuf bx, bxa, by, byb;
+  if (int e = bx.upload(xo)) return e;
+  if (int e = bxa.upload(xa)) return e;
+  if (int e = by.upload(yo)) return e;
+  if (int e = byb.upload(yb)) return e;
+  const hipStream_t s = (hipStream_t)stream;
+  ResizeArea p{src, bx.as<int32_t>(), bxa.as<int16_t>(), by.as<int32_t>(), byb.as<int16_t>(), sh, sw, ch, dh, dw,
+               dst_pitch};
+  const int n = dh * dw * ch;
+  hipLaunchKernelGGL(resize_area_kernel, dim3((n + TPB - 1) / TPB), dim3(TPB), 0, s, p, dst);
+  GP_HIP_CHECK(hipGetLastError());
+  GP_HIP_CHECK(hipStreamSynchronize(s));  // the coefficient buffers are freed on return
+  return GP_OK;
 }

@@ -86,6 +86,9 @@ SIGNATURES = {
     "gp_check": (ctypes.c_int, [_vp]),
     "gp_query": (ctypes.c_int, [_vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)]),
     "gp_taxi_reset_distribution": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
+    "gp_taxi_render": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _vp, ctypes.POINTER(ctypes.c_int32), _vp]),
+    "gp_resize_area_u8": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, ctypes.c_int,
+                                         ctypes.c_int, ctypes.c_int, _vp]),
     "gp_set_profiling": (ctypes.c_int, [_vp, ctypes.c_int]),
     "gp_profile_read": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]),
     "gp_profile_read_resolver": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double),

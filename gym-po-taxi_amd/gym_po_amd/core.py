@@ -288,4 +288,6 @@ class NativeVecEnv:
         return ms.value, n.value
 
     def render(self):
-        raise NotImplementedError("rendering is out of scope (SURVEY.md §2)")
+        """The reference renders none of the grid / continuous envs (msrooms.py:430-432 raises, RoomsEnv and
+        CRoomsEnv inherit gymnasium's NotImplementedError); TaxiVecEnv overrides this."""
+        raise NotImplementedError("render() is not implemented for this env (nor in the reference)")

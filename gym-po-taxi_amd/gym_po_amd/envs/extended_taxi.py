@@ -178,6 +178,33 @@ class TaxiVecEnv(NativeVecEnv):
     def n_dropoffs_completed(self):
         return self.get_state()[2].to(_torch().float64)
 
+    def render(self, idx=None):
+        """rgb_array of envs idx = arange(n) (default: env 0), rendered on the device (extended_taxi.py:289-331):
+        the bordered char map coloured with the shared palette (+64 on the taxi's neighbours for Hansen
+        envs), frames tiled by tile_images, resized like cv2.resize(img, (h*16, w*16), INTER_AREA) with (h, w)
+        the bordered map's shape, and a 20-column black text band. Returns a uint8 [w*16, h*16 + 20, 3] device
+        tensor. The reference indexes its frame stack with the env ids, so only idx = arange(n) is meaningful
+        there; other idx raise ValueError. Not drawn: the last-action caption (cv2.putText). The resize
+        restates OpenCV's INTER_AREA (cv2 is absent: parity unpinned; the tiled frame is pinned)."""
+        torch = _torch()
+        n = 1 if idx is None else len(idx)
+        if idx is not None and not np.array_equal(np.asarray(idx), np.arange(n)):
+            raise ValueError("render(idx): the reference's frame indexing only works for idx = arange(n)")
+        dims = (ctypes.c_int32 * 4)()
+        check(lib().gp_taxi_render(self._handle, n, int(self.hansen), None, dims, None), "gp_taxi_render")
+        rows, cols, fr, fc = dims
+        tiled = torch.empty((rows, cols, 3), dtype=torch.uint8, device=self.device)
+        stream = self._stream()
+        check(lib().gp_taxi_render(self._handle, n, int(self.hansen), ctypes.c_void_p(tiled.data_ptr()), dims,
+                                   stream), "gp_taxi_render")
+        dh, dw = fc * 16, fr * 16   # cv2 dsize = (width, height) = (frame_rows*16, frame_cols*16)
+        out = torch.zeros((dh, dw + 20, 3), dtype=torch.uint8, device=self.device)
+        check(lib().gp_resize_area_u8(ctypes.c_void_p(tiled.data_ptr()), rows, cols, 3,
+                                      ctypes.c_void_p(out.data_ptr()), dh, dw, (dw + 20) * 3, stream),
+              "gp_resize_area_u8")
+        self._last_tiled = tiled
+        return out
+
     def set_replay(self, reset_states=None, pd=None):
         """rng_mode='replay': per-env start states (int32 [B]) and passenger*nlocs+destination pairs
         (int32 [B]) used by the next reset/step wherever an env resets / completes a task."""

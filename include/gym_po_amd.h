@@ -229,6 +229,18 @@ int gp_normal_tail_counts(uint64_t key, int64_t n, const double* thr, int nthr, 
 /* Device-side start-state law of TAXI resets (host copy): P(state index k) over valid states. */
 int gp_taxi_reset_distribution(const gp_env* env, double* out, int cap);
 
+/* rgb_array frames of TAXI envs 0..n-1 (replaces TaxiVecEnv.render(idx=arange(n)), extended_taxi.py:289-309,
+ * up to and including str_map_to_img's colouring and Hansen highlight :126-142 and tile_images
+ * render_utils.py:63-88): uint8 RGB, frames tiled ceil(sqrt(n)) x ceil(n / ceil(sqrt(n))), zero padding.
+ * dims (host, out) = {rows, cols, frame_rows, frame_cols}; out (device, rows*cols*3) may be NULL to query dims.
+ * Other env kinds: GP_E_UNSUPPORTED (the reference renders none of them). Asynchronous on `stream`. */
+int gp_taxi_render(gp_env* env, int n, int hansen_highlight, uint8_t* out, int32_t dims[4], void* stream);
+/* cv2.resize(src, (dw, dh), interpolation=cv2.INTER_AREA) for uint8 sh x sw x ch device images when at least
+ * one axis is enlarged (the resize of str_map_to_img, extended_taxi.py:144-146): OpenCV's generic resize path
+ * restated (cv2 is absent here: parity unpinned). dst rows are dst_pitch bytes apart. Synchronises `stream`. */
+int gp_resize_area_u8(const uint8_t* src, int sh, int sw, int ch, uint8_t* dst, int dh, int dw, int dst_pitch,
+                      void* stream);
+
 /* Kernel timing: when enabled, hipEvents bracket every launch of the env's step kernel on its
  * stream; gp_profile_read syncs and returns the summed kernel time (ms) and launch count since
  * the last read (then clears). Used by bench.py for the live roofline measurement. */

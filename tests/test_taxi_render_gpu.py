@@ -1,0 +1,74 @@
+"""GPU Taxi rgb_array rendering (gp_taxi_render + gp_resize_area_u8) against the reference's own tiled frames
+(tests/golden/taxi_render.npz, pre-resize) and against the numpy restatement (oracle/render.py) end to end.
+The resize is a restatement of OpenCV's INTER_AREA (cv2 absent here): parity with cv2 itself is unpinned."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "gym-po-taxi_amd"))
+from oracle import render  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+GOLD = np.load(os.path.join(ROOT, "tests", "golden", "taxi_render.npz"))
+CASES = {"taxi_n1": ("TAXI_MAP", False), "taxi_n5_hansen": ("TAXI_MAP", True), "taxi_n9": ("TAXI_MAP", False),
+         "ext_n3_hansen": ("EXTENDED_TAXI_MAP", True), "ext_n10": ("EXTENDED_TAXI_MAP", False)}
+
+
+def _env(mp, hansen, n, states):
+    import torch
+    import gym_po_amd
+    from gym_po_amd import maps
+    env = gym_po_amd.TaxiVecEnv(max(n, 16), map=getattr(maps, mp), hansen_obs=hansen, device=torch.device("cuda", 0))
+    env.reset(seed=0)
+    s = env.get_state()[0].cpu().numpy()
+    s[:n] = states
+    env.set_state(s=s)
+    return env
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_render_matches_reference_frames_and_restatement(name):
+    mp, hansen = CASES[name]
+    states = GOLD[name + "_states"]
+    n = len(states)
+    env = _env(mp, hansen, n, states)
+    img = env.render(idx=np.arange(n)).cpu().numpy()
+    tiled = env._last_tiled.cpu().numpy()
+    gold = GOLD[name + "_img"]
+    np.testing.assert_array_equal(tiled, gold[:, :-render.TEXT_SPACE])   # the reference's own pixels
+    want = render.render_rgb(env.desc, env.cc, env.np_locs, env.nlocs, env.cols, states, hansen)
+    assert img.shape == (env.desc.shape[1] * 16, env.desc.shape[0] * 16 + 20, 3)
+    np.testing.assert_array_equal(img, want)
+    env.close()
+
+
+@pytest.mark.parametrize("shape", [(7, 11, 176, 112), (21, 33, 176, 112), (112, 176, 176, 112), (5, 3, 64, 9),
+                                   (13, 13, 13, 13), (9, 40, 30, 20)])
+def test_resize_area_kernel_matches_restatement(shape):
+    import ctypes
+    import torch
+    from gym_po_amd import _lib
+    sh, sw, dh, dw = shape
+    rng = np.random.default_rng(sum(shape))
+    src = rng.integers(0, 256, (sh, sw, 3), dtype=np.uint8)
+    s = torch.from_numpy(src).cuda()
+    d = torch.full((dh, dw + 5, 3), 7, dtype=torch.uint8, device="cuda")
+    rc = _lib.lib().gp_resize_area_u8(ctypes.c_void_p(s.data_ptr()), sh, sw, 3, ctypes.c_void_p(d.data_ptr()), dh, dw,
+                                      (dw + 5) * 3, None)
+    assert rc == 0, _lib.lib().gp_last_error()
+    got = d.cpu().numpy()
+    np.testing.assert_array_equal(got[:, :dw], render.resize_area_u8(src, dh, dw))
+    assert (got[:, dw:] == 7).all()  # the pitch padding is left alone
+
+
+def test_grid_envs_do_not_render_like_the_reference():
+    import torch
+    import gym_po_amd
+    env = gym_po_amd.MultistoryFourRoomsEnv(8, grid_z=1, obs_type="hansen", device=torch.device("cuda", 0))
+    with pytest.raises(NotImplementedError):
+        env.render()
+    env.close()
