@@ -47,6 +47,7 @@ CASES = {
     "rooms_4_hansen8": (RO, dict(layout="4", obs_type="hansen8", time_limit=100), 128, 300, 1, 12, True),
     "rooms_4_grid3": (RO, dict(layout="4", obs_type="grid", time_limit=100), 128, 300, 2, 13, True),
     "rooms_8b_grid5": (RO, dict(layout="8b", obs_type="grid", obs_n=5, time_limit=100), 64, 300, 3, 14, True),
+    "rooms_8_hansen": (RO, dict(layout="8", obs_type="hansen", time_limit=100), 64, 300, 24, 25, True),
     "rooms_10b_hansen": (RO, dict(layout="10b", obs_type="hansen", time_limit=120), 64, 300, 21, 22, True),
     "rooms_16b_vhansen_randgoal": (RO, dict(layout="16b", obs_type="vector_hansen", goal_xy=None, time_limit=150),
                                    64, 300, 23, 24, True),
