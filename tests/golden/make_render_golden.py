@@ -23,6 +23,8 @@ CASES = {
     "taxi_n9": ("TAXI_MAP", False, 9, 3),
     "ext_n3_hansen": ("EXTENDED_TAXI_MAP", True, 3, 4),
     "ext_n10": ("EXTENDED_TAXI_MAP", False, 10, 5),
+    "taxi_n16_hansen": ("TAXI_MAP", True, 16, 6),
+    "ext_n25_hansen": ("EXTENDED_TAXI_MAP", True, 25, 7),
 }
 
 

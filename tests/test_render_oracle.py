@@ -16,7 +16,8 @@ from gym_po_amd.envs.extended_taxi import convert_str_map_to_walled_np_str, get_
 
 GOLD = np.load(os.path.join(ROOT, "tests", "golden", "taxi_render.npz"))
 CASES = {"taxi_n1": (TAXI_MAP, False), "taxi_n5_hansen": (TAXI_MAP, True), "taxi_n9": (TAXI_MAP, False),
-         "ext_n3_hansen": (EXTENDED_TAXI_MAP, True), "ext_n10": (EXTENDED_TAXI_MAP, False)}
+         "ext_n3_hansen": (EXTENDED_TAXI_MAP, True), "ext_n10": (EXTENDED_TAXI_MAP, False),
+         "taxi_n16_hansen": (TAXI_MAP, True), "ext_n25_hansen": (EXTENDED_TAXI_MAP, True)}
 
 
 def map_parts(mp):
