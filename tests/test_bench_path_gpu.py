@@ -69,7 +69,8 @@ def _check_chunks(env, ora, chunks, action_seed, n_act):
     np.testing.assert_array_equal(e, ora.elapsed)
 
 
-@pytest.mark.parametrize("chunks,time_limit", [((20, 128), 500), ((128, 7), 500), ((20, 20), 20)])
+# (1, 4, 20): bench.py's driver sequence (two warmup launches of 1 and W - 1 = 4 steps, then the timed 20)
+@pytest.mark.parametrize("chunks,time_limit", [((20, 128), 500), ((128, 7), 500), ((20, 20), 20), ((1, 4, 20), 500)])
 def test_bench_kernel_staged_k_step_launches_bit_exact(chunks, time_limit, gpu_device):
     from gym_po_amd import MultistoryFourRoomsEnv
     env = MultistoryFourRoomsEnv(B_BENCH, grid_z=1, obs_type="hansen", time_limit=time_limit, device=gpu_device)
