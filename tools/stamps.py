@@ -82,13 +82,16 @@ pd, dd = a[:, :, 8], a[:, :, 9]
 print(f"poll done - last publish                 median {np.median(pd - pub.max(0)[None, :]):.0f} ns")
 print(f"block0 gather done - last publish        median {np.median(a[0, :, 10] - pub.max(0)):.0f} ns")
 print(f"draw cells (8->9)                        median {np.median(dd - pd):.0f} ns")
+if (a[:, :, 14] > 0).all():
+    print(f"  poll done -> lists ready (8->14)       median {np.median(a[:, :, 14] - pd):.0f} ns")
+    print(f"  cell draw proper (14->9)               median {np.median(dd - a[:, :, 14]):.0f} ns")
 print(f"publish_next etc (9->7)                  median {np.median(done - dd):.0f} ns")
 e11, e12, e13 = a[:, :, 11], a[:, :, 12], a[:, :, 13]
 rep("env: B1 -> resetters listed (2->11)", e11 - a[:, :, 2])
 rep("env: staging written (11->12)", e12 - e11)
 rep("env: J_B applied (12->13)", e13 - e12)
 rep("env: B2 wait (13->4)", a[:, :, 4] - e13)
-if (a[:, :, 14] > 0).all():
+if (a[:, :, 15] > 0).all():
     rep("env: early counts (0->14)", a[:, :, 14] - a[:, :, 0])
     rep("env: early flags+ballots (0->15)", a[:, :, 15] - a[:, :, 0])
     rep("env: early resolve (15->14)", a[:, :, 14] - a[:, :, 15])
