@@ -47,7 +47,9 @@ constexpr uint32_t TAG_DRAW = 0x6d733121u;
 #ifndef GP_CR_WAVES
 #define GP_CR_WAVES 2
 #endif
-constexpr double MAX_VELOCITY = 5.0;        // crooms.py:170
+constexpr double MAX_VELOCITY = 5.0;
+// Largest batch of the exact (numpy-stream) mode, which runs in one workgroup.
+#define GP_CR_NUMPY_MAX_ENVS (1 << 20)        // crooms.py:170
 
 struct alignas(32) CrSlot {
   double return_sum;
@@ -158,6 +160,8 @@ __device__ __forceinline__ double zlog1p_neg(double u) {  // log1p(-u) = log(v),
 #endif
 }
 
+// numpy's ki / wi / fi tables (ziggurat_tables.h), one array: ki at 0, wi at 256, fi at 512.
+__device__ const uint64_t d_zig[768] = {GP_ZIG_KI_LIST, GP_ZIG_WI_LIST, GP_ZIG_FI_LIST};
 struct ZigTabs {
   const uint64_t* ki;
   const double* wi;
@@ -380,7 +384,7 @@ __device__ __forceinline__ void reset_env(const CrDev& p, const uint8_t* lds, co
 
 struct StepOut {
   float rew;
-  uint8_t term, trunc;
+  uint8_t term, trunc, oob;
 };
 
 // One env-step of CRoomsEnv.step (crooms.py:276-331).
@@ -440,6 +444,7 @@ __device__ __forceinline__ StepOut crooms_env_step(const CrDev& p, const uint8_t
   px = fmin(fmax(px, 0.0), p.hi_x);
   const int pc = cell_of(p, py, px);
   const bool oob = pc < 0 || tab<uint8_t>(lds, p.off_wall)[pc] != 0;
+  o.oob = oob ? 1 : 0;
   if (!oob) {
     ay = py;
     ax = px;
@@ -663,6 +668,429 @@ __global__ void crooms_set_state(CrDev p, const double* agent, const int32_t* go
   if (el) p.el[env] = min(max(el[env], 0), 0x7FFFFFFF);
 }
 
+// ---- exact (numpy-stream) mode: GP_RNG_NUMPY ----
+// The reference's draws, word for word, from its one PCG64 stream (crooms.py:175-198, :300-331,
+// :217-244): per step rng.random(B) (discrete actions), rng.normal(scale=action_std, size=(B, 2)),
+// rng.normal(scale=0.5, size=(n_oob, 2)) for the envs that hit a wall, then choice() of the reset envs'
+// goals and agents. numpy's normal consumes a data-dependent number of words (ziggurat fast path 1 word,
+// wedge 2, tail 1 + 2k) and choice() draws buffered 32-bit halves with Lemire rejection, so the word ->
+// draw assignment is resolved in windows of XW words: every thread makes one word (a table jump from the
+// window base), classifies it on the fast path, one thread walks the few (~1.2%) slow positions in order
+// (marking the extra words they consume), and a ballot prefix over the surviving positions gives each
+// draw its index. One workgroup runs the whole batch (meant for seed-identical runs at small B); the step
+// itself is crooms_env_step<true> (the replay step, fixture-pinned) on the per-env draws, evaluated dry to
+// learn the wall hits and the resets that decide the later draw counts.
+constexpr int XT = 1024;           // threads of the exact-mode workgroup
+constexpr int XW = XT;             // words per window, one per thread
+constexpr int XWAVES = XT / 64;
+
+struct CrRng {
+  uint64_t s_hi, s_lo, i_hi, i_lo;
+  uint32_t has_u32, uinteger, err, pad;
+};
+
+struct CrExact {
+  CrRng* rng;
+  const PcgJump* wj;               // wj[j]: j LCG steps, j = 0..XW
+  double* noise;                   // [B, 2] action noise, per env
+  double* wall;                    // [B, 2] wall noise, per env
+  double* dense;                   // [2B] draws in stream order
+  uint64_t* u;                     // [B] action-failure k53
+  int32_t* gi;                     // [B] goal / agent indices into valid_states, per env
+  int32_t* ai;
+  int32_t* rank;                   // [B] scratch: rank of an env among the flagged ones, or -1
+  uint32_t lemire_thr;             // (2^32 - n_valid) % n_valid
+};
+
+struct XShared {
+  uint64_t w[XW];
+  double sval[XW];
+  uint64_t zt[768];
+  uint64_t slow[XWAVES];
+  uint32_t wtot[XWAVES], wtot2[XWAVES];
+  uint8_t dead[XW], sacc[XW], sused[XW];
+  uint64_t st_hi, st_lo;
+  uint32_t has_u32, uinteger, err;
+  int wend, endpos, total;
+};
+
+__device__ __forceinline__ u128 x_state(const XShared& sh) { return mk128(sh.st_hi, sh.st_lo); }
+__device__ __forceinline__ void x_advance(XShared& sh, const PcgJump* wj, int n) {
+  const u128 s = apply_jump(wj[n], x_state(sh));
+  sh.st_hi = hi64(s);
+  sh.st_lo = lo64(s);
+}
+
+// Exclusive rank of `f` among the XT threads (ballot per wave, wave totals in LDS); returns the total.
+__device__ __forceinline__ int x_rank(XShared& sh, uint32_t f, int& rank) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t b = __ballot(f != 0);
+  if (lane == 0) sh.wtot[wv] = (uint32_t)__popcll(b);
+  __syncthreads();
+  int base = 0, tot = 0;
+  for (int i = 0; i < XWAVES; ++i) {
+    base += i < wv ? (int)sh.wtot[i] : 0;
+    tot += (int)sh.wtot[i];
+  }
+  rank = base + __popcll(b & ((1ull << lane) - 1ull));
+  __syncthreads();
+  return tot;
+}
+
+// One attempt of numpy's ziggurat starting at window position q whose first word missed the fast path:
+// 1 = a normal (value v), 0 = a rejected wedge (the next attempt starts at q + used), -1 = it would read
+// past the window (the window ends at q).
+__device__ int zig_attempt(const ZigTabs& t, const uint64_t* w, int q, int& used, double& v) {
+  uint64_t r = w[q];
+  int pos = q + 1;
+  const int idx = (int)(r & 0xff);
+  r >>= 8;
+  const uint64_t sign = r & 1u, rabs = (r >> 1) & 0x000fffffffffffffull;
+  double x = (double)rabs * t.wi[idx];
+  if (sign) x = -x;
+  if (rabs < t.ki[idx]) { used = 1; v = x; return 1; }
+  if (idx == 0) {
+    for (;;) {
+      if (pos + 1 >= XW) return -1;
+      const double xx = -GP_ZIG_INV_R * zlog1p_neg(u53_of(w[pos]));
+      const double yy = -zlog1p_neg(u53_of(w[pos + 1]));
+      pos += 2;
+      if (yy + yy > xx * xx) {
+        used = pos - q;
+        v = ((rabs >> 8) & 1u) ? -(GP_ZIG_R + xx) : GP_ZIG_R + xx;
+        return 1;
+      }
+    }
+  }
+  if (pos >= XW) return -1;
+  used = 2;
+  v = x;
+  return ((t.fi[idx - 1] - t.fi[idx]) * u53_of(w[pos]) + t.fi[idx] < zexp(-0.5 * x * x)) ? 1 : 0;
+}
+
+// n draws of rng.normal(scale=scale) (numpy: loc + scale * standard_normal, loc = 0) into dst[0..n).
+__device__ void x_normals(XShared& sh, const CrExact& x, int64_t n, double scale, double* __restrict__ dst) {
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  ZigTabs zt;
+  zt.ki = sh.zt;
+  zt.wi = reinterpret_cast<const double*>(sh.zt + 256);
+  zt.fi = reinterpret_cast<const double*>(sh.zt + 512);
+  int64_t made = 0;
+  while (made < n) {
+    const uint64_t w = pcg_output(apply_jump(x.wj[t + 1], x_state(sh)));
+    sh.w[t] = w;
+    sh.dead[t] = 0;
+    double z;
+    const bool fast = zig_fast(zt, w, z);
+    const uint64_t sm = __ballot(!fast);
+    if (lane == 0) sh.slow[wv] = sm;
+    __syncthreads();
+    if (t == 0) {
+      int cur = 0, wend = XW;
+      for (int i = 0; i < XWAVES && wend == XW; ++i) {
+        uint64_t m = sh.slow[i];
+        while (m) {
+          const int q = i * 64 + __builtin_ctzll(m);
+          m &= m - 1;
+          if (q < cur) continue;  // an extra word of an earlier attempt
+          int used = 1;
+          double v = 0.0;
+          const int a = zig_attempt(zt, sh.w, q, used, v);
+          if (a < 0) { wend = q; break; }
+          sh.sval[q] = v;
+          sh.sacc[q] = (uint8_t)a;
+          sh.sused[q] = (uint8_t)used;
+          for (int j = q + 1; j < q + used; ++j) sh.dead[j] = 1;
+          cur = q + used;
+        }
+      }
+      if (wend == 0) sh.err = 1u;  // a tail attempt longer than a window (never in practice): drain
+      sh.wend = wend;
+      sh.endpos = -1;
+    }
+    __syncthreads();
+    if (sh.err) return;
+    const int wend = sh.wend;
+    const bool prod = t < wend && !sh.dead[t] && (fast || sh.sacc[t]);
+    const double v = fast ? z : sh.sval[t];
+    const int used = fast ? 1 : (int)sh.sused[t];
+    int rank;
+    const int tot = x_rank(sh, prod, rank);
+    if (prod && made + rank < n) dst[made + rank] = 0.0 + scale * v;
+    if (prod && made + rank == n - 1) sh.endpos = t + used;
+    __syncthreads();
+    const int consumed = (made + tot >= n) ? sh.endpos : wend;
+    made += (made + tot >= n) ? (n - made) : tot;
+    if (t == 0) x_advance(sh, x.wj, consumed);
+    __syncthreads();
+  }
+}
+
+// n draws of rng.random() into k53 form (next_double = (w >> 11) * 2^-53; the integer is kept).
+__device__ void x_uniforms(XShared& sh, const CrExact& x, int64_t n, uint64_t* __restrict__ dst) {
+  const int t = threadIdx.x;
+  for (int64_t made = 0; made < n; made += XW) {
+    const uint64_t w = pcg_output(apply_jump(x.wj[t + 1], x_state(sh)));
+    if (made + t < n) dst[made + t] = w >> 11;
+    __syncthreads();
+    if (t == 0) x_advance(sh, x.wj, (int)min((int64_t)XW, n - made));
+    __syncthreads();
+  }
+}
+
+// n draws of rng.choice(valid_states) as indices: integers(0, n_valid) -> 32-bit Lemire on next_uint32,
+// whose high halves are buffered in the bit generator (has_uint32 / uinteger) across calls.
+__device__ void x_choices(XShared& sh, const CrExact& x, int64_t n, uint32_t nv, int32_t* __restrict__ dst) {
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  int64_t made = 0;
+  while (made < n) {
+    const uint32_t h = sh.has_u32;
+    const uint64_t w = pcg_output(apply_jump(x.wj[t + 1], x_state(sh)));
+    const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
+    const bool ab = t == 0 && h && !lemire_rejected(sh.uinteger, nv, x.lemire_thr);
+    const bool alo = !lemire_rejected(lo, nv, x.lemire_thr), ahi = !lemire_rejected(hi, nv, x.lemire_thr);
+    const uint32_t c = (ab ? 1u : 0u) + (alo ? 1u : 0u) + (ahi ? 1u : 0u);  // 0..3
+    const uint64_t b0 = __ballot(c & 1u), b1 = __ballot(c & 2u);
+    const uint64_t lt = (1ull << lane) - 1ull;
+    if (lane == 0) { sh.wtot[wv] = (uint32_t)__popcll(b0); sh.wtot2[wv] = (uint32_t)__popcll(b1); }
+    if (t == 0) sh.endpos = -1;
+    __syncthreads();
+    int base = 0, tot = 0;
+    for (int i = 0; i < XWAVES; ++i) {
+      const int wc = (int)sh.wtot[i] + 2 * (int)sh.wtot2[i];
+      base += i < wv ? wc : 0;
+      tot += wc;
+    }
+    int r = base + __popcll(b0 & lt) + 2 * __popcll(b1 & lt);
+    // candidates in stream order: the buffered half (thread 0), then lo, hi of each word; endpos codes the
+    // last candidate consumed: 0 = the buffered half, 2t + 1 = lo of word t, 2t + 2 = hi of word t
+    if (ab) {
+      if (made + r < n) dst[made + r] = (int32_t)lemire_value(sh.uinteger, nv);
+      if (made + r == n - 1) sh.endpos = 0;
+      ++r;
+    }
+    if (alo) {
+      if (made + r < n) dst[made + r] = (int32_t)lemire_value(lo, nv);
+      if (made + r == n - 1) sh.endpos = 2 * t + 1;
+      ++r;
+    }
+    if (ahi) {
+      if (made + r < n) dst[made + r] = (int32_t)lemire_value(hi, nv);
+      if (made + r == n - 1) sh.endpos = 2 * t + 2;
+    }
+    __syncthreads();
+    const int e = (made + tot >= n) ? sh.endpos : 2 * XW;
+    const int words = (e + 1) / 2;                  // lo of word t -> t + 1 words, hi -> t + 1 words
+    // numpy's next_uint32 stores the high half of every word it draws (uinteger) and keeps it after
+    // handing it out; has_uint32 says whether it is still unused (the last word's lo was the last draw)
+    if (words > 0 && t == words - 1) sh.uinteger = hi;
+    __syncthreads();
+    if (t == 0) {
+      sh.has_u32 = (e & 1) ? 1u : 0u;
+      x_advance(sh, x.wj, words);
+    }
+    made += (made + tot >= n) ? (n - made) : tot;
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ void x_load_action(const CrDev& p, const void* act, size_t off, int env, double& a0,
+                                              double& a1, int& ad) {
+  a0 = a1 = 0.0;
+  ad = 0;
+  if (p.action_kind == 0) {
+    if (p.action_f64) {
+      const double* A = (const double*)act + 2 * (off + env);
+      a0 = A[0];
+      a1 = A[1];
+    } else {
+      const float* A = (const float*)act + 2 * (off + env);
+      a0 = A[0];
+      a1 = A[1];
+    }
+  } else {
+    ad = ((const int32_t*)act)[off + env];
+  }
+}
+
+__device__ __forceinline__ uint32_t x_goal(const CrDev& p, int env) {
+  return p.goal_fixed ? ((uint32_t)(p.goal_y & 0xFFFF) | ((uint32_t)(p.goal_x & 0xFFFF) << 16)) : p.goal[env];
+}
+
+// Scatter dense[2 rank + j] -> per[2 env + j] (W = 2) or dense[rank] -> per[env] (W = 1) for flagged envs.
+template <int W, class T>
+__device__ __forceinline__ void x_scatter(const CrDev& p, const CrExact& x, const T* dense, T* per) {
+  for (int env = threadIdx.x; env < p.B; env += XT) {
+    const int r = x.rank[env];
+    if (r >= 0)
+      for (int j = 0; j < W; ++j) per[(size_t)W * env + j] = dense[(size_t)W * r + j];
+  }
+}
+
+// Ranks of the flagged envs (x.rank, -1 when unflagged) over all B envs; returns the count.
+template <class F>
+__device__ int x_rank_envs(XShared& sh, const CrDev& p, const CrExact& x, F&& flag) {
+  int base = 0;
+  for (int e0 = 0; e0 < p.B; e0 += XT) {
+    const int env = e0 + threadIdx.x;
+    const bool f = env < p.B && flag(env);
+    int r;
+    const int tot = x_rank(sh, f, r);
+    if (env < p.B) x.rank[env] = f ? base + r : -1;
+    base += tot;
+  }
+  __syncthreads();
+  return base;
+}
+
+// K steps (or, with K = 0 and do_reset, reset()) of the whole batch in one workgroup.
+template <int OK>
+__global__ __launch_bounds__(XT) void crooms_numpy_rollout(CrDev p, CrExact x, int K, int do_reset,
+                                                           const void* __restrict__ act, void* __restrict__ obs,
+                                                           float* __restrict__ rew, uint8_t* __restrict__ term,
+                                                           uint8_t* __restrict__ trunc) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  __shared__ XShared sh;
+  const int t = threadIdx.x;
+  for (int i = t; i < p.tab_bytes / 16; i += XT) ((uint4*)lds)[i] = ((const uint4*)p.tabs)[i];
+  for (int i = t; i < 768; i += XT) sh.zt[i] = d_zig[i];
+  if (t == 0) {
+    sh.st_hi = x.rng->s_hi;
+    sh.st_lo = x.rng->s_lo;
+    sh.has_u32 = x.rng->has_u32;
+    sh.uinteger = x.rng->uinteger;
+    sh.err = x.rng->err;
+  }
+  __syncthreads();
+  const size_t osz = (size_t)p.obs_width * (OK == GP_OBS_F32 ? (p.obs_f64 ? 8 : 4)
+                                                             : (OK == GP_OBS_HANSEN || OK == GP_OBS_TABLE ? 4 : 1));
+  if (do_reset && !sh.err) {  // crooms.py:251-266: goal then agent for every env
+    if (!p.goal_fixed) x_choices(sh, x, p.B, (uint32_t)p.n_valid, x.gi);
+    if (!p.agent_fixed && !sh.err) x_choices(sh, x, p.B, (uint32_t)p.n_valid, x.ai);
+    for (int env = t; env < p.B; env += XT) {
+      Draws d;
+      d.k53 = 0;
+      d.gi = p.goal_fixed ? 0u : (uint32_t)x.gi[env];
+      d.ai = p.agent_fixed ? 0u : (uint32_t)x.ai[env];
+      double ay, ax, vy, vx;
+      uint32_t g = x_goal(p, 0);
+      reset_env(p, lds, d, ay, ax, vy, vx, g);
+      p.ay[env] = ay;
+      p.ax[env] = ax;
+      if (p.use_velocity) { p.vy[env] = 0.0; p.vx[env] = 0.0; }
+      if (!p.goal_fixed) p.goal[env] = g;
+      p.el[env] = 0;
+      write_obs<OK>(p, lds, env, ay, ax, g, obs);
+    }
+  }
+  CrDev dd = p;
+  dd.rp_u = x.u;
+  dd.rp_goal = x.gi;
+  dd.rp_agent = x.ai;
+  dd.rp_noise = x.noise;
+  dd.rp_wall = x.wall;
+  float rsum = 0.f;
+  uint32_t eps = 0, lens = 0, nst = 0;
+  for (int k = 0; k < K && !sh.err; ++k) {
+    const size_t off = (size_t)k * p.B;
+    // _sample_action's draws (crooms.py:175-198)
+    if (p.action_kind != 0) x_uniforms(sh, x, p.B, x.u);
+    if (p.action_kind == 0 || p.action_std != 0.0) x_normals(sh, x, 2 * (int64_t)p.B, p.action_std, x.noise);
+    __syncthreads();
+    // the dry step on copies: which envs hit a wall (draw count of the wall noise, crooms.py:321-325)
+    auto dry = [&](int env, StepOut& o) {
+      double a0, a1;
+      int ad;
+      x_load_action(p, act, off, env, a0, a1, ad);
+      double ay = p.ay[env], ax = p.ax[env];
+      double vy = p.use_velocity ? p.vy[env] : 0.0, vx = p.use_velocity ? p.vx[env] : 0.0;
+      uint32_t g = x_goal(p, env);
+      int32_t el = p.el[env];
+      float rs = 0.f;
+      uint32_t ep = 0, ln = 0;
+      o = crooms_env_step<true>(dd, lds, env, true, 0, a0, a1, ad, ay, ax, vy, vx, g, el, rs, ep, ln);
+    };
+    const int n_oob = x_rank_envs(sh, p, x, [&](int env) { StepOut o; dry(env, o); return o.oob != 0; });
+    if (n_oob) {
+      x_normals(sh, x, 2 * (int64_t)n_oob, 0.5, x.dense);
+      __syncthreads();
+      x_scatter<2>(p, x, x.dense, x.wall);
+      __syncthreads();
+    }
+    // with the wall noise in place: which envs reset (crooms.py:289-297), then their goals and agents
+    const int n_rs = x_rank_envs(sh, p, x, [&](int env) { StepOut o; dry(env, o); return (o.term | o.trunc) != 0; });
+    if (n_rs) {
+      int32_t* di = (int32_t*)x.dense;
+      if (!p.goal_fixed) {
+        x_choices(sh, x, n_rs, (uint32_t)p.n_valid, di);
+        __syncthreads();
+        x_scatter<1>(p, x, di, x.gi);
+        __syncthreads();
+      }
+      if (!p.agent_fixed) {
+        x_choices(sh, x, n_rs, (uint32_t)p.n_valid, di);
+        __syncthreads();
+        x_scatter<1>(p, x, di, x.ai);
+        __syncthreads();
+      }
+    }
+    if (sh.err) break;
+    // the step itself, on the state, with every draw in place
+    uint8_t* ob = (uint8_t*)obs + (size_t)k * p.B * osz;
+    for (int env = t; env < p.B; env += XT) {
+      double a0, a1;
+      int ad;
+      x_load_action(p, act, off, env, a0, a1, ad);
+      double ay = p.ay[env], ax = p.ax[env];
+      double vy = p.use_velocity ? p.vy[env] : 0.0, vx = p.use_velocity ? p.vx[env] : 0.0;
+      uint32_t g = x_goal(p, env);
+      int32_t el = p.el[env];
+      const StepOut o = crooms_env_step<true>(dd, lds, env, true, 0, a0, a1, ad, ay, ax, vy, vx, g, el, rsum, eps, lens);
+      ++nst;
+      rew[off + env] = o.rew;
+      term[off + env] = o.term;
+      trunc[off + env] = o.trunc;
+      write_obs<OK>(p, lds, env, ay, ax, g, ob);
+      p.ay[env] = ay;
+      p.ax[env] = ax;
+      if (p.use_velocity) { p.vy[env] = vy; p.vx[env] = vx; }
+      if (!p.goal_fixed) p.goal[env] = g;
+      p.el[env] = el;
+    }
+    __syncthreads();
+  }
+  // metrics into slot 0
+  __shared__ float m_r;
+  __shared__ unsigned long long m_e, m_l, m_n;
+  if (t == 0) { m_r = 0.f; m_e = m_l = m_n = 0; }
+  __syncthreads();
+  for (int d = 32; d >= 1; d >>= 1) {
+    rsum += __shfl_xor(rsum, d, 64);
+    eps += __shfl_xor(eps, d, 64);
+    lens += __shfl_xor(lens, d, 64);
+    nst += __shfl_xor(nst, d, 64);
+  }
+  if ((t & 63) == 0) {
+    atomicAdd(&m_r, rsum);
+    atomicAdd(&m_e, (unsigned long long)eps);
+    atomicAdd(&m_l, (unsigned long long)lens);
+    atomicAdd(&m_n, (unsigned long long)nst);
+  }
+  __syncthreads();
+  if (t == 0) {
+    CrSlot& m = p.mslot[0];
+    m.return_sum += (double)m_r;
+    m.episodes += m_e;
+    m.length_sum += m_l;
+    m.env_steps += m_n;
+    x.rng->s_hi = sh.st_hi;
+    x.rng->s_lo = sh.st_lo;
+    x.rng->has_u32 = sh.has_u32;
+    x.rng->uinteger = sh.uinteger;
+    x.rng->err = sh.err;
+  }
+}
+
 // ------------------------------------------------------------------ host backend ----
 template <class F>
 static int dispatch_obs(int ok, F&& f) {
@@ -683,6 +1111,11 @@ struct CRoomsBackend : EnvBackend {
   uint64_t philox_step = 0;
   std::vector<int32_t> valid_h;
   DevBuf b_tabs, b_ay, b_ax, b_vy, b_vx, b_goal, b_el, b_slot;
+  // exact (numpy-stream) mode
+  DevBuf x_rng, x_wj, x_noise, x_wall, x_dense, x_u, x_gi, x_ai, x_rank;
+  CrExact xd{};
+  int x_alloc();
+  int x_upload_rng(const RngHost& r);
   const uint64_t* rp_u = nullptr;
   const int32_t* rp_goal = nullptr;
   const int32_t* rp_agent = nullptr;
@@ -698,15 +1131,53 @@ struct CRoomsBackend : EnvBackend {
     d.key0 = key[0];
     d.key1 = key[1];
     philox_step = 0;
+    return rng_mode == GP_RNG_NUMPY ? x_upload_rng(r) : GP_OK;
+  }
+  int set_rng_state(const RngHost& r) override {
+    if (rng_mode != GP_RNG_NUMPY) {
+      gp_set_error("crooms: the PCG64 stream is used on the device only in numpy mode");
+      return GP_E_UNSUPPORTED;
+    }
+    rng = r;
+    return x_upload_rng(r);
+  }
+  int get_rng_state(RngHost* r) override {
+    if (rng_mode != GP_RNG_NUMPY) {
+      gp_set_error("crooms: the PCG64 stream is used on the device only in numpy mode");
+      return GP_E_UNSUPPORTED;
+    }
+    GP_HIP_CHECK(hipDeviceSynchronize());
+    CrRng h;
+    GP_HIP_CHECK(hipMemcpy(&h, x_rng.p, sizeof(CrRng), hipMemcpyDeviceToHost));
+    if (h.err) {
+      gp_set_error("crooms numpy mode: a ziggurat tail attempt outran its word window; the stream is invalid");
+      return GP_E_DEVICE;
+    }
+    r->state = mk128(h.s_hi, h.s_lo);
+    r->inc = mk128(h.i_hi, h.i_lo);
+    r->has_u32 = h.has_u32;
+    r->uinteger = h.uinteger;
+    rng = *r;
     return GP_OK;
   }
-  int set_rng_state(const RngHost&) override {
-    gp_set_error("crooms: the PCG64 stream is not used on the device (philox / replay modes)");
-    return GP_E_UNSUPPORTED;
+  int check() override {
+    if (rng_mode != GP_RNG_NUMPY) return GP_OK;
+    RngHost r;
+    return get_rng_state(&r);
   }
-  int get_rng_state(RngHost*) override {
-    gp_set_error("crooms: the PCG64 stream is not used on the device (philox / replay modes)");
-    return GP_E_UNSUPPORTED;
+  int x_launch(int K, int do_reset, const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc,
+               hipStream_t s) {
+    const CrDev dd = dev_for_launch();
+    const CrExact xx = xd;
+    int e = dispatch_obs(d.obs_kind, [&](auto okc) -> int {
+      constexpr int OK = decltype(okc)::value;
+      hipLaunchKernelGGL((crooms_numpy_rollout<OK>), dim3(1), dim3(XT), d.tab_bytes, s, dd, xx, K, do_reset, act,
+                         obs, rew, term, trunc);
+      return GP_OK;
+    });
+    if (e) return e;
+    GP_HIP_CHECK(hipGetLastError());
+    return GP_OK;
   }
   CrDev dev_for_launch() const {
     CrDev dd = d;
@@ -722,6 +1193,12 @@ struct CRoomsBackend : EnvBackend {
     if (rng_mode == GP_RNG_REPLAY && ((!d.goal_fixed && !rp_goal) || (!d.agent_fixed && !rp_agent))) {
       gp_set_error("crooms replay reset needs goal/agent index draws (gp_set_replay i0/i1)");
       return GP_E_STATE;
+    }
+    if (rng_mode == GP_RNG_NUMPY) {
+      int e = x_launch(0, 1, nullptr, obs, nullptr, nullptr, nullptr, s);
+      if (e) return e;
+      has_reset = true;
+      return GP_OK;
     }
     const CrDev dd = dev_for_launch();
     const bool rep = rng_mode == GP_RNG_REPLAY;
@@ -763,6 +1240,12 @@ struct CRoomsBackend : EnvBackend {
     if (!al(act, d.action_kind == 0 ? (d.action_f64 ? 16 : 8) : 4) || !al(obs, 16) || !al(rew, 4)) {
       gp_set_error("crooms: misaligned action / obs / reward buffer");
       return GP_E_INVALID;
+    }
+    if (rng_mode == GP_RNG_NUMPY) {
+      timer.begin(s);
+      int e = x_launch(K, 0, act, obs, rew, term, trunc, s);
+      timer.end(s);
+      return e;
     }
     const CrDev dd = dev_for_launch();
     const uint64_t st = philox_step;
@@ -1069,6 +1552,43 @@ int CRoomsBackend::build(const gp_crooms_config* cfg) {
   grid = std::max(1, std::min(d.ntiles, prop.multiProcessorCount * occ));
   if ((e = b_slot.alloc(sizeof(CrSlot) * grid))) return e;
   d.mslot = b_slot.as<CrSlot>();
+  if (rng_mode == GP_RNG_NUMPY && (e = x_alloc())) return e;
+  return GP_OK;
+}
+
+int CRoomsBackend::x_alloc() {
+  int e;
+  const size_t b = (size_t)B;
+  if ((e = x_rng.alloc(sizeof(CrRng))) || (e = x_wj.alloc(sizeof(PcgJump) * (XW + 1))) ||
+      (e = x_noise.alloc(16 * b)) || (e = x_wall.alloc(16 * b)) || (e = x_dense.alloc(16 * b)) ||
+      (e = x_u.alloc(8 * b)) || (e = x_gi.alloc(4 * b)) || (e = x_ai.alloc(4 * b)) || (e = x_rank.alloc(4 * b)))
+    return e;
+  xd.rng = x_rng.as<CrRng>();
+  xd.wj = x_wj.as<PcgJump>();
+  xd.noise = x_noise.as<double>();
+  xd.wall = x_wall.as<double>();
+  xd.dense = x_dense.as<double>();
+  xd.u = x_u.as<uint64_t>();
+  xd.gi = x_gi.as<int32_t>();
+  xd.ai = x_ai.as<int32_t>();
+  xd.rank = x_rank.as<int32_t>();
+  xd.lemire_thr = lemire_threshold((uint32_t)d.n_valid);
+  return x_upload_rng(rng);
+}
+
+// The device stream state and the window jump table wj[j] = j LCG steps (j = 0..XW) for its increment.
+int CRoomsBackend::x_upload_rng(const RngHost& r) {
+  std::vector<PcgJump> wj(XW + 1);
+  u128 a = 1, c = 0;
+  for (int j = 0; j <= XW; ++j) {
+    wj[j] = PcgJump{hi64(a), lo64(a), hi64(c), lo64(c)};
+    a = pcg_mult() * a;
+    c = pcg_mult() * c + r.inc;
+  }
+  GP_HIP_CHECK(hipDeviceSynchronize());
+  GP_HIP_CHECK(hipMemcpy(x_wj.p, wj.data(), sizeof(PcgJump) * wj.size(), hipMemcpyHostToDevice));
+  CrRng h{hi64(r.state), lo64(r.state), hi64(r.inc), lo64(r.inc), r.has_u32, r.uinteger, 0u, 0u};
+  GP_HIP_CHECK(hipMemcpy(x_rng.p, &h, sizeof(CrRng), hipMemcpyHostToDevice));
   return GP_OK;
 }
 
@@ -1076,7 +1596,6 @@ int CRoomsBackend::build(const gp_crooms_config* cfg) {
 
 // ---- diagnostics of the normal sampler (C ABI below) ----
 namespace {
-__device__ const uint64_t d_zig[768] = {GP_ZIG_KI_LIST, GP_ZIG_WI_LIST, GP_ZIG_FI_LIST};
 
 // numpy's standard_normal over a caller word stream, one lane, in order (numpy consumes the words
 // sequentially and a normal may take several).
@@ -1187,10 +1706,10 @@ extern "C" int gp_normal_tail_counts(uint64_t key, int64_t n, const double* thr,
 
 std::unique_ptr<EnvBackend> make_crooms_backend(const gp_crooms_config* cfg, int64_t B, int device, int rng_mode,
                                                 int* err) {
-  if (rng_mode == GP_RNG_NUMPY) {
-    gp_set_error("crooms: rng_mode numpy is not available on the device (numpy's ziggurat normals consume a "
-                 "data-dependent number of words from one stream); use philox (same laws) or replay");
-    *err = GP_E_UNSUPPORTED;
+  if (rng_mode == GP_RNG_NUMPY && B > GP_CR_NUMPY_MAX_ENVS) {
+    gp_set_error("crooms: rng_mode numpy (the reference's own stream, one workgroup) takes at most %d envs; "
+                 "use philox (same laws) for larger batches", GP_CR_NUMPY_MAX_ENVS);
+    *err = GP_E_INVALID;
     return nullptr;
   }
   if (B < 1 || B > (int64_t)1 << 30) {

@@ -5,9 +5,11 @@ wall bounce with in-cell resampling, goal test, resets, observation functions) r
 kernels of libgympo_amd.so (csrc/crooms.hip) in float64, operation for operation as the reference,
 with float32 (default) or float64 I/O.
 
-RNG: the reference's numpy ziggurat normals consume a data-dependent number of words from one
-stream, so `rng_mode="numpy"` is not offered. `"philox"` (default) draws the same laws from a
-counter-based generator; `"replay"` takes the reference stream's values (bit-exact parity tests).
+RNG: `"philox"` (default) draws the reference's laws from a counter-based generator (every env-step
+independent, full-chip kernels); `"numpy"` draws the reference's own PCG64 stream word for word (numpy's
+ziggurat normals and buffered Lemire choices, seed-identical with the reference; one workgroup resolves
+the data-dependent word counts, so it is meant for small batches, at most 2^20 envs); `"replay"` takes
+the reference stream's values per env (bit-exact parity tests).
 
 Extra keyword arguments beyond the reference: `device`, `rng_mode`, `dtype` (torch.float32 (default)
 or torch.float64 for the continuous actions and observations).
@@ -139,9 +141,6 @@ class CRoomsEnv(NativeVecEnv):
         cfg.time_limit = int(time_limit)
         cfg.step_reward, cfg.wall_reward, cfg.goal_reward = float(step_reward), float(wall_reward), float(goal_reward)
         cfg.goal_threshold = float(goal_threshold)
-        if rng_mode == "numpy":
-            raise _lib.GymPoError("CRoomsEnv: rng_mode='numpy' is not available on the device (numpy's ziggurat "
-                                  "stream is sequential); use 'philox' (same laws) or 'replay'")
         self._obs_window = n if kind == _lib.GP_OBS_WINDOW else None
         self._create(_lib.GP_KIND_CROOMS, cfg, num_envs, device, rng_mode)
 
