@@ -167,8 +167,9 @@ class NativeVecEnv:
         """K steps in one call: actions [K, B(,2)] -> obs [K, B, ...], rew/term/trunc [K, B].
 
         Philox mode, and numpy mode on the grid envs (persistent kernel with a per-step grid
-        exchange), run the K steps in ONE fused launch with the env state in registers; replay
-        mode issues K step launches on the stream. `out` may supply preallocated buffers
+        exchange), run the K steps in ONE fused launch with the env state in registers; C-ROOMS
+        numpy mode runs them in one single-workgroup launch (the stream walk); replay mode issues
+        K step launches on the stream. `out` may supply preallocated buffers
         (obs, rew, term(uint8), trunc(uint8)) shaped like `_alloc_outputs(K)`: they are checked
         for shape, dtype, device and contiguity (ValueError otherwise)."""
         torch = _torch()

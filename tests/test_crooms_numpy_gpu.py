@@ -77,6 +77,8 @@ ORACLE_CASES = [
     ({"obs_type": "hansen8", "action_type": "ordinal", "layout": "16", "goal_xy": None, "time_limit": 20}, 1500, 45, 1),
     ({"obs_type": "grid", "action_type": "cardinal", "action_std": 0.0, "time_limit": 15}, 999, 40, 40),
     ({"obs_type": "goal_room", "layout": "8b", "goal_xy": None, "time_limit": 12}, 4099, 30, 5),
+    # many windows per draw call (2^17 normals per step): slow attempts at window ends, ~10^3 tail draws
+    ({"obs_type": "vector_mdp", "action_std": 0.5, "time_limit": 6}, 65536, 12, 6),
 ]
 
 

@@ -1,0 +1,34 @@
+"""Throughput of C-ROOMS exact mode (rng_mode='numpy', one workgroup) beside philox mode, same config.
+
+Usage (GPU box): python tools/crooms_numpy_rate.py  -> one JSON line per (mode, B).
+"""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gym-po-taxi_amd"))
+import torch  # noqa: E402
+
+from gym_po_amd import CRoomsEnv  # noqa: E402
+
+
+def rate(mode, B, K=50, reps=3):
+    env = CRoomsEnv(B, obs_type="vector_mdp", rng_mode=mode)
+    env.reset(seed=0)
+    a = torch.rand((K, B, 2), device=env.device) * 2 - 1
+    env.rollout(a)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        env.rollout(a)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return {"mode": mode, "num_envs": B, "steps": K * reps, "us_per_step": dt / (K * reps) * 1e6,
+            "env_steps_per_s": B * K * reps / dt}
+
+
+if __name__ == "__main__":
+    for B in (1024, 4096, 65536):
+        for mode in ("numpy", "philox"):
+            print(json.dumps(rate(mode, B)), flush=True)
