@@ -708,7 +708,8 @@ struct XShared {
   uint64_t zt[768];
   uint64_t slow[XWAVES];
   uint32_t wtot[XWAVES], wtot2[XWAVES];
-  uint8_t dead[XW], sacc[XW], sused[XW];
+  uint8_t dead[XW], sacc[XW];
+  uint16_t sused[XW];
   uint64_t st_hi, st_lo;
   uint32_t has_u32, uinteger, err;
   int wend, endpos, total;
@@ -769,7 +770,8 @@ __device__ int zig_attempt(const ZigTabs& t, const uint64_t* w, int q, int& used
 }
 
 // n draws of rng.normal(scale=scale) (numpy: loc + scale * standard_normal, loc = 0) into dst[0..n).
-__device__ void x_normals(XShared& sh, const CrExact& x, int64_t n, double scale, double* __restrict__ dst) {
+__device__ void x_normals(XShared& sh, const CrExact& x, const PcgJump& myj, int64_t n, double scale,
+                          double* __restrict__ dst) {
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   ZigTabs zt;
   zt.ki = sh.zt;
@@ -777,7 +779,7 @@ __device__ void x_normals(XShared& sh, const CrExact& x, int64_t n, double scale
   zt.fi = reinterpret_cast<const double*>(sh.zt + 512);
   int64_t made = 0;
   while (made < n) {
-    const uint64_t w = pcg_output(apply_jump(x.wj[t + 1], x_state(sh)));
+    const uint64_t w = pcg_output(apply_jump(myj, x_state(sh)));
     sh.w[t] = w;
     sh.dead[t] = 0;
     double z;
@@ -785,7 +787,16 @@ __device__ void x_normals(XShared& sh, const CrExact& x, int64_t n, double scale
     const uint64_t sm = __ballot(!fast);
     if (lane == 0) sh.slow[wv] = sm;
     __syncthreads();
-    if (t == 0) {
+    if (!fast) {  // the attempt this word would start (speculative: it may be an extra word of another)
+      int used = 1;
+      double v = 0.0;
+      const int a = zig_attempt(zt, sh.w, t, used, v);
+      sh.sval[t] = v;
+      sh.sacc[t] = (uint8_t)(a < 0 ? 2 : a);
+      sh.sused[t] = (uint16_t)used;
+    }
+    __syncthreads();
+    if (t == 0) {  // the chain over the slow positions, in order
       int cur = 0, wend = XW;
       for (int i = 0; i < XWAVES && wend == XW; ++i) {
         uint64_t m = sh.slow[i];
@@ -793,13 +804,8 @@ __device__ void x_normals(XShared& sh, const CrExact& x, int64_t n, double scale
           const int q = i * 64 + __builtin_ctzll(m);
           m &= m - 1;
           if (q < cur) continue;  // an extra word of an earlier attempt
-          int used = 1;
-          double v = 0.0;
-          const int a = zig_attempt(zt, sh.w, q, used, v);
-          if (a < 0) { wend = q; break; }
-          sh.sval[q] = v;
-          sh.sacc[q] = (uint8_t)a;
-          sh.sused[q] = (uint8_t)used;
+          if (sh.sacc[q] == 2) { wend = q; break; }
+          const int used = sh.sused[q];
           for (int j = q + 1; j < q + used; ++j) sh.dead[j] = 1;
           cur = q + used;
         }
@@ -827,10 +833,10 @@ __device__ void x_normals(XShared& sh, const CrExact& x, int64_t n, double scale
 }
 
 // n draws of rng.random() into k53 form (next_double = (w >> 11) * 2^-53; the integer is kept).
-__device__ void x_uniforms(XShared& sh, const CrExact& x, int64_t n, uint64_t* __restrict__ dst) {
+__device__ void x_uniforms(XShared& sh, const CrExact& x, const PcgJump& myj, int64_t n, uint64_t* __restrict__ dst) {
   const int t = threadIdx.x;
   for (int64_t made = 0; made < n; made += XW) {
-    const uint64_t w = pcg_output(apply_jump(x.wj[t + 1], x_state(sh)));
+    const uint64_t w = pcg_output(apply_jump(myj, x_state(sh)));
     if (made + t < n) dst[made + t] = w >> 11;
     __syncthreads();
     if (t == 0) x_advance(sh, x.wj, (int)min((int64_t)XW, n - made));
@@ -840,12 +846,13 @@ __device__ void x_uniforms(XShared& sh, const CrExact& x, int64_t n, uint64_t* _
 
 // n draws of rng.choice(valid_states) as indices: integers(0, n_valid) -> 32-bit Lemire on next_uint32,
 // whose high halves are buffered in the bit generator (has_uint32 / uinteger) across calls.
-__device__ void x_choices(XShared& sh, const CrExact& x, int64_t n, uint32_t nv, int32_t* __restrict__ dst) {
+__device__ void x_choices(XShared& sh, const CrExact& x, const PcgJump& myj, int64_t n, uint32_t nv,
+                          int32_t* __restrict__ dst) {
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   int64_t made = 0;
   while (made < n) {
     const uint32_t h = sh.has_u32;
-    const uint64_t w = pcg_output(apply_jump(x.wj[t + 1], x_state(sh)));
+    const uint64_t w = pcg_output(apply_jump(myj, x_state(sh)));
     const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
     const bool ab = t == 0 && h && !lemire_rejected(sh.uinteger, nv, x.lemire_thr);
     const bool alo = !lemire_rejected(lo, nv, x.lemire_thr), ahi = !lemire_rejected(hi, nv, x.lemire_thr);
@@ -952,6 +959,7 @@ __global__ __launch_bounds__(XT) void crooms_numpy_rollout(CrDev p, CrExact x, i
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   __shared__ XShared sh;
   const int t = threadIdx.x;
+  const PcgJump myj = x.wj[t + 1];  // every window: word t is t + 1 LCG steps past the window base
   for (int i = t; i < p.tab_bytes / 16; i += XT) ((uint4*)lds)[i] = ((const uint4*)p.tabs)[i];
   for (int i = t; i < 768; i += XT) sh.zt[i] = d_zig[i];
   if (t == 0) {
@@ -965,8 +973,8 @@ __global__ __launch_bounds__(XT) void crooms_numpy_rollout(CrDev p, CrExact x, i
   const size_t osz = (size_t)p.obs_width * (OK == GP_OBS_F32 ? (p.obs_f64 ? 8 : 4)
                                                              : (OK == GP_OBS_HANSEN || OK == GP_OBS_TABLE ? 4 : 1));
   if (do_reset && !sh.err) {  // crooms.py:251-266: goal then agent for every env
-    if (!p.goal_fixed) x_choices(sh, x, p.B, (uint32_t)p.n_valid, x.gi);
-    if (!p.agent_fixed && !sh.err) x_choices(sh, x, p.B, (uint32_t)p.n_valid, x.ai);
+    if (!p.goal_fixed) x_choices(sh, x, myj, p.B, (uint32_t)p.n_valid, x.gi);
+    if (!p.agent_fixed && !sh.err) x_choices(sh, x, myj, p.B, (uint32_t)p.n_valid, x.ai);
     for (int env = t; env < p.B; env += XT) {
       Draws d;
       d.k53 = 0;
@@ -994,8 +1002,8 @@ __global__ __launch_bounds__(XT) void crooms_numpy_rollout(CrDev p, CrExact x, i
   for (int k = 0; k < K && !sh.err; ++k) {
     const size_t off = (size_t)k * p.B;
     // _sample_action's draws (crooms.py:175-198)
-    if (p.action_kind != 0) x_uniforms(sh, x, p.B, x.u);
-    if (p.action_kind == 0 || p.action_std != 0.0) x_normals(sh, x, 2 * (int64_t)p.B, p.action_std, x.noise);
+    if (p.action_kind != 0) x_uniforms(sh, x, myj, p.B, x.u);
+    if (p.action_kind == 0 || p.action_std != 0.0) x_normals(sh, x, myj, 2 * (int64_t)p.B, p.action_std, x.noise);
     __syncthreads();
     // the dry step on copies: which envs hit a wall (draw count of the wall noise, crooms.py:321-325)
     auto dry = [&](int env, StepOut& o) {
@@ -1012,7 +1020,7 @@ __global__ __launch_bounds__(XT) void crooms_numpy_rollout(CrDev p, CrExact x, i
     };
     const int n_oob = x_rank_envs(sh, p, x, [&](int env) { StepOut o; dry(env, o); return o.oob != 0; });
     if (n_oob) {
-      x_normals(sh, x, 2 * (int64_t)n_oob, 0.5, x.dense);
+      x_normals(sh, x, myj, 2 * (int64_t)n_oob, 0.5, x.dense);
       __syncthreads();
       x_scatter<2>(p, x, x.dense, x.wall);
       __syncthreads();
@@ -1022,13 +1030,13 @@ __global__ __launch_bounds__(XT) void crooms_numpy_rollout(CrDev p, CrExact x, i
     if (n_rs) {
       int32_t* di = (int32_t*)x.dense;
       if (!p.goal_fixed) {
-        x_choices(sh, x, n_rs, (uint32_t)p.n_valid, di);
+        x_choices(sh, x, myj, n_rs, (uint32_t)p.n_valid, di);
         __syncthreads();
         x_scatter<1>(p, x, di, x.gi);
         __syncthreads();
       }
       if (!p.agent_fixed) {
-        x_choices(sh, x, n_rs, (uint32_t)p.n_valid, di);
+        x_choices(sh, x, myj, n_rs, (uint32_t)p.n_valid, di);
         __syncthreads();
         x_scatter<1>(p, x, di, x.ai);
         __syncthreads();
