@@ -991,12 +991,7 @@ __global__ __launch_bounds__(XT) void crooms_numpy_rollout(CrDev p, CrExact x, i
       write_obs<OK>(p, lds, env, ay, ax, g, obs);
     }
   }
-  CrDev dd = p;
-  dd.rp_u = x.u;
-  dd.rp_goal = x.gi;
-  dd.rp_agent = x.ai;
-  dd.rp_noise = x.noise;
-  dd.rp_wall = x.wall;
+  // p.rp_* point at the per-env draw buffers (x.u / gi / ai / noise / wall), set by the host
   float rsum = 0.f;
   uint32_t eps = 0, lens = 0, nst = 0;
   for (int k = 0; k < K && !sh.err; ++k) {
@@ -1016,7 +1011,7 @@ __global__ __launch_bounds__(XT) void crooms_numpy_rollout(CrDev p, CrExact x, i
       int32_t el = p.el[env];
       float rs = 0.f;
       uint32_t ep = 0, ln = 0;
-      o = crooms_env_step<true>(dd, lds, env, true, 0, a0, a1, ad, ay, ax, vy, vx, g, el, rs, ep, ln);
+      o = crooms_env_step<true>(p, lds, env, true, 0, a0, a1, ad, ay, ax, vy, vx, g, el, rs, ep, ln);
     };
     const int n_oob = x_rank_envs(sh, p, x, [&](int env) { StepOut o; dry(env, o); return o.oob != 0; });
     if (n_oob) {
@@ -1053,7 +1048,7 @@ __global__ __launch_bounds__(XT) void crooms_numpy_rollout(CrDev p, CrExact x, i
       double vy = p.use_velocity ? p.vy[env] : 0.0, vx = p.use_velocity ? p.vx[env] : 0.0;
       uint32_t g = x_goal(p, env);
       int32_t el = p.el[env];
-      const StepOut o = crooms_env_step<true>(dd, lds, env, true, 0, a0, a1, ad, ay, ax, vy, vx, g, el, rsum, eps, lens);
+      const StepOut o = crooms_env_step<true>(p, lds, env, true, 0, a0, a1, ad, ay, ax, vy, vx, g, el, rsum, eps, lens);
       ++nst;
       rew[off + env] = o.rew;
       term[off + env] = o.term;
@@ -1175,7 +1170,12 @@ struct CRoomsBackend : EnvBackend {
   }
   int x_launch(int K, int do_reset, const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc,
                hipStream_t s) {
-    const CrDev dd = dev_for_launch();
+    CrDev dd = dev_for_launch();
+    dd.rp_u = xd.u;          // the exact kernel's per-env draws, consumed by the replay step
+    dd.rp_goal = xd.gi;
+    dd.rp_agent = xd.ai;
+    dd.rp_noise = xd.noise;
+    dd.rp_wall = xd.wall;
     const CrExact xx = xd;
     int e = dispatch_obs(d.obs_kind, [&](auto okc) -> int {
       constexpr int OK = decltype(okc)::value;
