@@ -716,10 +716,14 @@ struct XShared {
 };
 
 __device__ __forceinline__ u128 x_state(const XShared& sh) { return mk128(sh.st_hi, sh.st_lo); }
-__device__ __forceinline__ void x_advance(XShared& sh, const PcgJump* wj, int n) {
-  const u128 s = apply_jump(wj[n], x_state(sh));
-  sh.st_hi = hi64(s);
-  sh.st_lo = lo64(s);
+// The window base moves past the n words consumed: thread n - 1 holds that jump (wj[n]) in registers.
+// Call between barriers, after every thread has read the base.
+__device__ __forceinline__ void x_advance(XShared& sh, const PcgJump& myj, int n) {
+  if (n > 0 && (int)threadIdx.x == n - 1) {
+    const u128 s = apply_jump(myj, x_state(sh));
+    sh.st_hi = hi64(s);
+    sh.st_lo = lo64(s);
+  }
 }
 
 // Exclusive rank of `f` among the XT threads (ballot per wave, wave totals in LDS); returns the total.
@@ -827,7 +831,7 @@ __device__ void x_normals(XShared& sh, const CrExact& x, const PcgJump& myj, int
     __syncthreads();
     const int consumed = (made + tot >= n) ? sh.endpos : wend;
     made += (made + tot >= n) ? (n - made) : tot;
-    if (t == 0) x_advance(sh, x.wj, consumed);
+    x_advance(sh, myj, consumed);
     __syncthreads();
   }
 }
@@ -839,7 +843,7 @@ __device__ void x_uniforms(XShared& sh, const CrExact& x, const PcgJump& myj, in
     const uint64_t w = pcg_output(apply_jump(myj, x_state(sh)));
     if (made + t < n) dst[made + t] = w >> 11;
     __syncthreads();
-    if (t == 0) x_advance(sh, x.wj, (int)min((int64_t)XW, n - made));
+    x_advance(sh, myj, (int)min((int64_t)XW, n - made));
     __syncthreads();
   }
 }
@@ -892,10 +896,8 @@ __device__ void x_choices(XShared& sh, const CrExact& x, const PcgJump& myj, int
     // handing it out; has_uint32 says whether it is still unused (the last word's lo was the last draw)
     if (words > 0 && t == words - 1) sh.uinteger = hi;
     __syncthreads();
-    if (t == 0) {
-      sh.has_u32 = (e & 1) ? 1u : 0u;
-      x_advance(sh, x.wj, words);
-    }
+    if (t == 0) sh.has_u32 = (e & 1) ? 1u : 0u;
+    x_advance(sh, myj, words);
     made += (made + tot >= n) ? (n - made) : tot;
     __syncthreads();
   }
