@@ -387,8 +387,9 @@ struct StepOut {
   uint8_t term, trunc, oob;
 };
 
-// One env-step of CRoomsEnv.step (crooms.py:276-331).
-template <bool REPLAY>
+// One env-step of CRoomsEnv.step (crooms.py:276-331). DEFER: a terminated / truncated env is left for the
+// caller to reset (its reset draws are not known yet; the exact mode's stream walk).
+template <bool REPLAY, bool DEFER = false>
 __device__ __forceinline__ StepOut crooms_env_step(const CrDev& p, const uint8_t* lds, int env, bool live,
                                                    uint64_t step, double a0, double a1, int ad, double& ay,
                                                    double& ax, double& vy, double& vx, uint32_t& g, int32_t& el,
@@ -472,8 +473,10 @@ __device__ __forceinline__ StepOut crooms_env_step(const CrDev& p, const uint8_t
     eps += 1u;
     lens += (uint32_t)el;
     el = 0;
-    if (p.action_kind == 0) draw_ints<REPLAY>(p, env, step, d);
-    reset_env(p, lds, d, ay, ax, vy, vx, g);
+    if constexpr (!DEFER) {
+      if (p.action_kind == 0) draw_ints<REPLAY>(p, env, step, d);
+      reset_env(p, lds, d, ay, ax, vy, vx, g);
+    }
   }
   return o;
 }
@@ -1022,8 +1025,33 @@ __global__ __launch_bounds__(XT) void crooms_numpy_rollout(CrDev p, CrExact x, i
       x_scatter<2>(p, x, x.dense, x.wall);
       __syncthreads();
     }
-    // with the wall noise in place: which envs reset (crooms.py:289-297), then their goals and agents
-    const int n_rs = x_rank_envs(sh, p, x, [&](int env) { StepOut o; dry(env, o); return (o.term | o.trunc) != 0; });
+    // the step itself with the wall noise in place (crooms.py:276-298), resets deferred: which envs reset
+    uint8_t* ob = (uint8_t*)obs + (size_t)k * p.B * osz;
+    const int n_rs = x_rank_envs(sh, p, x, [&](int env) {
+      double a0, a1;
+      int ad;
+      x_load_action(p, act, off, env, a0, a1, ad);
+      double ay = p.ay[env], ax = p.ax[env];
+      double vy = p.use_velocity ? p.vy[env] : 0.0, vx = p.use_velocity ? p.vx[env] : 0.0;
+      uint32_t g = x_goal(p, env);
+      int32_t el = p.el[env];
+      const StepOut o =
+          crooms_env_step<true, true>(p, lds, env, true, 0, a0, a1, ad, ay, ax, vy, vx, g, el, rsum, eps, lens);
+      ++nst;
+      rew[off + env] = o.rew;
+      term[off + env] = o.term;
+      trunc[off + env] = o.trunc;
+      const bool rs = (o.term | o.trunc) != 0;
+      if (!rs) {
+        write_obs<OK>(p, lds, env, ay, ax, g, ob);
+        p.ay[env] = ay;
+        p.ax[env] = ax;
+        if (p.use_velocity) { p.vy[env] = vy; p.vx[env] = vx; }
+      }
+      p.el[env] = el;
+      return rs;
+    });
+    // the resetting envs' goals then agents (crooms.py:217-244, 293-297), in env order
     if (n_rs) {
       int32_t* di = (int32_t*)x.dense;
       if (!p.goal_fixed) {
@@ -1038,30 +1066,23 @@ __global__ __launch_bounds__(XT) void crooms_numpy_rollout(CrDev p, CrExact x, i
         x_scatter<1>(p, x, di, x.ai);
         __syncthreads();
       }
+      for (int env = t; env < p.B; env += XT) {
+        if (x.rank[env] < 0) continue;
+        Draws d;
+        d.k53 = 0;
+        d.gi = p.goal_fixed ? 0u : (uint32_t)x.gi[env];
+        d.ai = p.agent_fixed ? 0u : (uint32_t)x.ai[env];
+        double ay, ax, vy, vx;
+        uint32_t g = x_goal(p, env);
+        reset_env(p, lds, d, ay, ax, vy, vx, g);
+        p.ay[env] = ay;
+        p.ax[env] = ax;
+        if (p.use_velocity) { p.vy[env] = 0.0; p.vx[env] = 0.0; }
+        if (!p.goal_fixed) p.goal[env] = g;
+        write_obs<OK>(p, lds, env, ay, ax, g, ob);
+      }
     }
     if (sh.err) break;
-    // the step itself, on the state, with every draw in place
-    uint8_t* ob = (uint8_t*)obs + (size_t)k * p.B * osz;
-    for (int env = t; env < p.B; env += XT) {
-      double a0, a1;
-      int ad;
-      x_load_action(p, act, off, env, a0, a1, ad);
-      double ay = p.ay[env], ax = p.ax[env];
-      double vy = p.use_velocity ? p.vy[env] : 0.0, vx = p.use_velocity ? p.vx[env] : 0.0;
-      uint32_t g = x_goal(p, env);
-      int32_t el = p.el[env];
-      const StepOut o = crooms_env_step<true>(p, lds, env, true, 0, a0, a1, ad, ay, ax, vy, vx, g, el, rsum, eps, lens);
-      ++nst;
-      rew[off + env] = o.rew;
-      term[off + env] = o.term;
-      trunc[off + env] = o.trunc;
-      write_obs<OK>(p, lds, env, ay, ax, g, ob);
-      p.ay[env] = ay;
-      p.ax[env] = ax;
-      if (p.use_velocity) { p.vy[env] = vy; p.vx[env] = vx; }
-      if (!p.goal_fixed) p.goal[env] = g;
-      p.el[env] = el;
-    }
     __syncthreads();
   }
   // metrics into slot 0
