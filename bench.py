@@ -93,18 +93,18 @@ def lib_hash():
 
 
 # sources that determine each measured kernel's code (PMC traffic is reused only for the same sources)
-KERNEL_SOURCES = {"fourrooms": ("grid.hip", "gp_common.h"), "taxi": ("taxi.hip", "gp_common.h", "gp_device.h"),
-                  "crooms": ("crooms.hip", "gp_common.h", "gp_device.h"),
-                  "anttag": ("anttag.hip", "gp_common.h", "gp_device.h")}
+KERNEL_SOURCES = {"fourrooms": ("grid.hip", "gp_common.h", "gp_internal.h"),
+                  "taxi": ("taxi.hip", "gp_common.h", "gp_internal.h"),
+                  "crooms": ("crooms.hip", "gp_common.h", "gp_internal.h", "ziggurat_tables.h"),
+                  "anttag": ("anttag.hip", "gp_common.h", "gp_internal.h")}
 
 
 def src_hash(workload):
     h = hashlib.sha1()
     for name in KERNEL_SOURCES[workload]:
         p = os.path.join(ROOT, "gym-po-taxi_amd", "csrc", name)
-        if os.path.exists(p):
-            with open(p, "rb") as f:
-                h.update(f.read())
+        with open(p, "rb") as f:  # a missing file is a stale KERNEL_SOURCES entry: fail, never hash less
+            h.update(f.read())
     return h.hexdigest()[:12]
 
 

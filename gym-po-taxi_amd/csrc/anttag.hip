@@ -48,6 +48,7 @@ struct AtDev {
   int32_t off_cnt, off_list, tab_bytes;
   uint32_t* st;            // [B] ant | target << 8 | elapsed << 16
   AtSlot* mslot;
+  uint32_t* derr;            // device error word (GP_DERR_*)
   const int32_t* rp_choose;  // replay: target move choice [B]
   const int32_t* rp_ant;     // replay: reset ant cell index [B]
   const int32_t* rp_tgt;     // replay: reset target index into the ant cell's valid list [B]
@@ -95,7 +96,8 @@ __device__ __forceinline__ StepOut at_env_step(const AtDev& p, const uint8_t* ld
   int ant = (int)(u & 0xFFu), tgt = (int)((u >> 8) & 0xFFu);
   uint32_t el = (u >> 16) + 1u;
   int ay = cdiv(p, ant), ax = ant - ay * N, ty = cdiv(p, tgt), tx = tgt - ty * N;
-  // ant move
+  // ant move (an action outside [-5, 5) is flagged as the reference's discrete envs would raise, then clamped)
+  if (live && action_out_of_range(a, NACT)) flag_bad_action(p.derr);
   if (a < 0) a += NACT;
   a = min(max(a, 0), NACT - 1);
   const int DY[NACT] = {-1, 0, 1, 0, 0}, DX[NACT] = {0, 1, 0, -1, 0};
@@ -297,6 +299,7 @@ struct AntTagBackend : EnvBackend {
   int grid = 1;
   uint64_t philox_step = 0;
   DevBuf b_tabs, b_st, b_slot;
+  DevErr derr;
   const int32_t* rp_choose = nullptr;
   const int32_t* rp_ant = nullptr;
   const int32_t* rp_tgt = nullptr;
@@ -307,8 +310,9 @@ struct AntTagBackend : EnvBackend {
     d.key0 = key[0];
     d.key1 = key[1];
     philox_step = 0;
-    return GP_OK;
+    return derr.clear();
   }
+  int check() override { return derr.check("anttag"); }
   int set_rng_state(const RngHost&) override {
     gp_set_error("anttag: no numpy stream (build-defined env; philox / replay modes)");
     return GP_E_UNSUPPORTED;
@@ -409,7 +413,7 @@ struct AntTagBackend : EnvBackend {
       out[2] += (double)x.length_sum;
       out[3] += (double)x.env_steps;
     }
-    return GP_OK;
+    return check();
   }
 };
 
@@ -476,6 +480,8 @@ int AntTagBackend::build(const gp_anttag_config* cfg) {
   grid = std::max(1, std::min(d.ntiles, prop.multiProcessorCount * occ));
   if ((e = b_slot.alloc(sizeof(AtSlot) * grid))) return e;
   d.mslot = b_slot.as<AtSlot>();
+  if ((e = derr.alloc())) return e;
+  d.derr = derr.ptr();
   return GP_OK;
 }
 

@@ -23,6 +23,41 @@ void gp_set_error(const char* fmt, ...) {
   va_end(ap);
 }
 
+const char* gp_derr_text(uint32_t flags) {
+  static thread_local char buf[512];
+  buf[0] = 0;
+  if (flags & GP_DERR_ACTION)
+    strncat(buf, "an action outside [-n, n) was given (the reference raises IndexError there; the device clamped it); ",
+            sizeof(buf) - strlen(buf) - 1);
+  if (flags & GP_DERR_TIMEOUT)
+    strncat(buf, "a persistent kernel's cross-block wait timed out (blocks not co-resident?); ",
+            sizeof(buf) - strlen(buf) - 1);
+  if (flags & GP_DERR_STREAM)
+    strncat(buf, "a numpy normal needed more words than one stream window holds; ", sizeof(buf) - strlen(buf) - 1);
+  return buf;
+}
+
+static GpDebugKnobs g_dbg;
+const GpDebugKnobs& gp_debug_knobs() { return g_dbg; }
+
+int DevErr::clear() {
+  if (!buf.p) return GP_OK;
+  GP_HIP_CHECK(hipDeviceSynchronize());
+  GP_HIP_CHECK(hipMemset(buf.p, 0, sizeof(uint32_t)));
+  return GP_OK;
+}
+
+int DevErr::check(const char* kind) const {
+  GP_HIP_CHECK(hipDeviceSynchronize());
+  if (!buf.p) return GP_OK;
+  uint32_t f = 0;
+  GP_HIP_CHECK(hipMemcpy(&f, buf.p, sizeof(f), hipMemcpyDeviceToHost));
+  if (!f) return GP_OK;
+  gp_set_error("%s: device error flags 0x%x: %sthe outputs and env state since the last seed are invalid "
+               "(reseed to clear)", kind, f, gp_derr_text(f));
+  return GP_E_DEVICE;
+}
+
 // ------------------------------------------------------------------ SeedSequence ----
 // numpy/random/bit_generator.pyx (SeedSequence.mix_entropy / generate_state), restated.
 namespace {
@@ -161,6 +196,24 @@ KernelTimer::~KernelTimer() {
 extern "C" {
 
 const char* gp_last_error(void) { return g_err; }
+
+int gp_debug_set(const char* key, int64_t value) {
+  if (!key) {
+    gp_set_error("gp_debug_set: null key");
+    return GP_E_INVALID;
+  }
+  if (!strcmp(key, "disable_fused")) g_dbg.disable_fused = value != 0;
+  else if (!strcmp(key, "no_staging")) g_dbg.no_staging = value != 0;
+  else if (!strcmp(key, "xmode")) g_dbg.xmode = (int)value;
+  else if (!strcmp(key, "spin_limit")) g_dbg.spin_limit = value > 0 ? (uint32_t)value : 0u;
+  else if (!strcmp(key, "fault_block")) g_dbg.fault_block = (int)value;
+  else {
+    gp_set_error("gp_debug_set: unknown key '%s'", key);
+    return GP_E_INVALID;
+  }
+  return GP_OK;
+}
+void gp_debug_reset(void) { g_dbg = GpDebugKnobs{}; }
 int gp_abi_version(void) { return GP_ABI_VERSION; }
 
 int gp_create(int kind, const void* config, int64_t num_envs, int device, int rng_mode, gp_env** out) {

@@ -77,6 +77,7 @@ struct CrDev {
   uint32_t* goal;        // gy | gx << 16 (int16 each; a fixed goal may lie off the grid)
   int32_t* el;
   CrSlot* mslot;
+  uint32_t* derr;        // device error word (GP_DERR_*)
   // replay
   const uint64_t* rp_u;
   const int32_t* rp_goal;
@@ -413,6 +414,7 @@ __device__ __forceinline__ StepOut crooms_env_step(const CrDev& p, const uint8_t
   } else {
     if (live) draw_ints<REPLAY>(p, env, step, d);
     int a = ad;
+    if (live && action_out_of_range(a, p.nact)) flag_bad_action(p.derr);  // IndexError in the reference
     if (a < 0) a += p.nact;                 // numpy negative indexing of action_matrix[a]
     a = min(max(a, 0), p.nact - 1);
     const uint64_t* thr = tab<uint64_t>(lds, p.off_thr) + a * p.nact;
@@ -1137,6 +1139,7 @@ struct CRoomsBackend : EnvBackend {
   uint64_t philox_step = 0;
   std::vector<int32_t> valid_h;
   DevBuf b_tabs, b_ay, b_ax, b_vy, b_vx, b_goal, b_el, b_slot;
+  DevErr derr;
   // exact (numpy-stream) mode
   DevBuf x_rng, x_wj, x_noise, x_wall, x_dense, x_u, x_gi, x_ai, x_rank;
   CrExact xd{};
@@ -1157,6 +1160,7 @@ struct CRoomsBackend : EnvBackend {
     d.key0 = key[0];
     d.key1 = key[1];
     philox_step = 0;
+    if (int e = derr.clear()) return e;
     return rng_mode == GP_RNG_NUMPY ? x_upload_rng(r) : GP_OK;
   }
   int set_rng_state(const RngHost& r) override {
@@ -1187,6 +1191,7 @@ struct CRoomsBackend : EnvBackend {
     return GP_OK;
   }
   int check() override {
+    if (int e = derr.check("crooms")) return e;
     if (rng_mode != GP_RNG_NUMPY) return GP_OK;
     RngHost r;
     return get_rng_state(&r);
@@ -1340,7 +1345,7 @@ struct CRoomsBackend : EnvBackend {
       out[2] += (double)x.length_sum;
       out[3] += (double)x.env_steps;
     }
-    return GP_OK;
+    return check();  // device errors (invalid actions; numpy mode: an invalid stream) invalidate the run
   }
 };
 
@@ -1583,6 +1588,8 @@ int CRoomsBackend::build(const gp_crooms_config* cfg) {
   grid = std::max(1, std::min(d.ntiles, prop.multiProcessorCount * occ));
   if ((e = b_slot.alloc(sizeof(CrSlot) * grid))) return e;
   d.mslot = b_slot.as<CrSlot>();
+  if ((e = derr.alloc())) return e;
+  d.derr = derr.ptr();
   if (rng_mode == GP_RNG_NUMPY && (e = x_alloc())) return e;
   return GP_OK;
 }

@@ -104,6 +104,16 @@ GP_HD uint32_t st_rej(uint64_t s) { return (uint32_t)(s >> 61) & 1u; }
 GP_HD uint32_t st_count(uint64_t s) { return (uint32_t)s; }
 
 // ---------------------------------------------------------------- error plumbing ----
+// Per-handle device error word (GridCtl::err, the other kinds' `derr`): kernels OR bits into it,
+// gp_check / gp_metrics turn a nonzero word into GP_E_DEVICE. Sticky until the handle is re-seeded.
+#define GP_DERR_TIMEOUT 1u  // a persistent kernel's cross-block wait gave up (blocks not co-resident)
+#define GP_DERR_ACTION 2u   // an action outside [-n, n): the reference raises IndexError
+                            // (msrooms.py:400 action_matrix[action], extended_taxi.py:248 ACTIONS_YX[actions])
+#define GP_DERR_STREAM 4u   // C-ROOMS exact mode: a numpy normal needed more words than one window holds
+// numpy indexing of an n-row table accepts a in [-n, n) (negatives wrap); anything else raises.
+__device__ __forceinline__ bool action_out_of_range(int a, int n) { return (uint32_t)(a + n) >= (uint32_t)(2 * n); }
+__device__ __forceinline__ void flag_bad_action(uint32_t* derr) { atomicOr(derr, GP_DERR_ACTION); }
+const char* gp_derr_text(uint32_t flags);  // api.hip: human-readable description of the set bits
 void gp_set_error(const char* fmt, ...);
 #define GP_HIP_CHECK(x)                                                                        \
   do {                                                                                         \

@@ -23,6 +23,13 @@ std::vector<double> argmax_multinomial_distribution(int m, int n);
 // Radix-64 jump tables (JT_LEVELS x 64) for increment `inc`.
 std::vector<PcgJump> build_jump_tables(u128 inc);
 
+// Diagnostic knobs (gp_debug_set), read by the backends at gp_create.
+struct GpDebugKnobs {
+  int disable_fused = 0, no_staging = 0, xmode = 1, fault_block = -1;
+  uint32_t spin_limit = 0;  // 0 = the kernel's default
+};
+const GpDebugKnobs& gp_debug_knobs();
+
 // Per-kind backend interface; gp_env owns one.
 // hipEvent pairs around the step-kernel launches (gp_set_profiling / gp_profile_read).
 struct KernelTimer {
@@ -128,3 +135,14 @@ struct DevBuf {
     return (T*)p;
   }
 };
+
+// The per-handle device error word of the kinds without a control block (taxi, ant-tag, C-ROOMS philox /
+// replay): kernels OR GP_DERR_* bits into it; check() syncs, reads it and reports GP_E_DEVICE.
+struct DevErr {
+  DevBuf buf;
+  int alloc() { return buf.alloc(16); }
+  uint32_t* ptr() const { return buf.as<uint32_t>(); }
+  int clear();                       // on seed: a new stream, earlier errors no longer apply
+  int check(const char* kind) const;  // GP_OK or GP_E_DEVICE with gp_last_error() text
+};
+

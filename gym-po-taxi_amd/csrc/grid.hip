@@ -122,9 +122,11 @@ struct GridDev {
 // co-resident) still drains: every wave reaches the end of the kernel, the results are flagged invalid.
 __device__ __forceinline__ bool spin_give_up(const GridDev& p, uint32_t& spins) {
   ++spins;
-  if ((spins & 63u) == 0 && __hip_atomic_load(&p.ctl->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return true;
+  if ((spins & 63u) == 0 &&
+      (__hip_atomic_load(&p.ctl->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & GP_DERR_TIMEOUT))
+    return true;
   if (spins > p.spin_limit) {
-    atomicOr(&p.ctl->err, 1u);
+    atomicOr(&p.ctl->err, GP_DERR_TIMEOUT);
     return true;
   }
   return false;
@@ -575,8 +577,9 @@ __device__ __forceinline__ Trans transition(const GridDev& p, const TB& tb, uint
   Trans t;
   const int agent = (int)(ae & 0xFFFF);
   t.elapsed = (int)(ae >> 16) + 1;
+  if (action_out_of_range(a, p.nact)) flag_bad_action(&p.ctl->err);  // IndexError in the reference: flagged
   if (a < 0) a += p.nact;               // numpy negative indexing of action_matrix[action]
-  a = min(max(a, 0), p.nact - 1);       // (out-of-range actions raise in the reference; clamped here)
+  a = min(max(a, 0), p.nact - 1);       // (clamped after flagging so the launch stays in bounds)
   const uint32_t eff = min(effective_action(thr, p.nact, a, k53), (uint32_t)p.nact - 1);
   const uint16_t m = tb.move(agent * p.nact + (int)eff);
   t.agent = m & 0x7FFF;
@@ -1528,9 +1531,10 @@ __device__ __forceinline__ uint64_t thr_on_u64(uint64_t t) {
   return t >= (1ull << 53) ? ~0ull : ((t << 11) | 0x7FFull);
 }
 // Sanitised action -> byte offset of its threshold row in s_thr (numpy negative indexing; out-of-range
-// actions, which raise in the reference, are clamped).
+// actions, which raise IndexError in the reference, set GP_DERR_ACTION and are clamped).
 template <int NA>
-__device__ __forceinline__ int32_t action_row(int32_t a) {
+__device__ __forceinline__ int32_t action_row(int32_t a, uint32_t* derr) {
+  if (action_out_of_range(a, NA)) flag_bad_action(derr);
   if (a < 0) a += NA;
   return min(max(a, 0), NA - 1) * NA * 8;
 }
@@ -1632,7 +1636,7 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
     load4f<int32_t>(act, env0, B, a_cur[q]);
     if constexpr (TRIMS) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) a_cur[q][i] = action_row<NA>(a_cur[q][i]);
+      for (int i = 0; i < 4; ++i) a_cur[q][i] = action_row<NA>(a_cur[q][i], &p.ctl->err);
     }
     jtile[q] = p.ftj[min(tau, nt - 1)];
     vmask[q] = 0;
@@ -1697,6 +1701,7 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
         } else {
           const uint64_t k53 = pcg_output(s) >> 11;
           int a = a_cur[q][i];
+          if (action_out_of_range(a, NA)) flag_bad_action(&p.ctl->err);
           if (a < 0) a += NA;                 // numpy negative indexing of action_matrix[action]
           a = min(max(a, 0), NA - 1);         // (out-of-range actions raise in the reference; clamped here)
           const uint32_t eff = fused_effective_action<NA>(s_thr, a, k53);
@@ -1861,7 +1866,7 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
 #pragma unroll
         for (int q = 0; q < QPT; ++q)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) a_nxt[q][i] = action_row<NA>(a_nxt[q][i]);
+          for (int i = 0; i < 4; ++i) a_nxt[q][i] = action_row<NA>(a_nxt[q][i], &p.ctl->err);
       }
     }
     STAMP(13);
@@ -2644,8 +2649,8 @@ int GridBackend::get_rng_state(RngHost* r) {
 }
 
 int GridBackend::device_error(uint32_t flags) {
-  gp_set_error("device error flags 0x%x: a persistent kernel's cross-block wait timed out (blocks not co-resident?); "
-               "the outputs and env state since the last seed are invalid (reseed to clear)", flags);
+  gp_set_error("device error flags 0x%x: %sthe outputs and env state since the last seed are invalid (reseed to clear)",
+               flags, gp_derr_text(flags));
   return GP_E_DEVICE;
 }
 
@@ -3037,44 +3042,46 @@ int GridBackend::build(const gp_grid_config* cfg) {
       return GP_E_INVALID;
     }
   }
-  // LDS staging of the lookup tables for the fused kernel (when they fit)
+  // LDS staging of the lookup tables for the fused kernel (when they fit). The fixed-goal obs table (ofix) and
+  // the {agent, obs} pairs (avo) only speed up the staged Hansen path: they are laid out only when the image
+  // still fits the budget with them, so that they never cost a config its fused eligibility.
   {
-    int off = 0;
-    auto put = [&](GridLdsTab& t, size_t bytes) {
-      t.off = off;
-      t.bytes = (int)bytes;
-      off += (int)((bytes + 15) / 16 * 16);
-    };
     const int k = cfg->obs_kind;
-    put(d.lds.move, (size_t)nc * nact * sizeof(uint16_t));
-    put(d.lds.hbase, k == GP_OBS_HANSEN ? (size_t)nc * sizeof(uint32_t) : 0);
-    put(d.lds.hvec, k == GP_OBS_HANSEN_VEC ? hvec.size() : 0);
-    put(d.lds.t1, t1.size() * sizeof(int32_t));
-    put(d.lds.t2, t2.size() * sizeof(int32_t));
-    put(d.lds.coords, (k == GP_OBS_COORDS || k == GP_OBS_WINDOW) ? coords.size() * sizeof(int16_t) : 0);
-    put(d.lds.window, window.size());
-    put(d.lds.gv, goal_valid_h.size() * sizeof(uint16_t));
-    put(d.lds.av, agent_valid_h.size() * sizeof(uint16_t));
-    put(d.lds.doff, doff.size() * sizeof(int32_t));
-    put(d.lds.ofix, ofix.size() * sizeof(int32_t));
-    put(d.lds.avo, avo.size() * sizeof(uint32_t));
-    put(d.lds.jt, sizeof(PcgJump) * JT_LEVELS * JT_RADIX);
-    put(d.lds.jt8, sizeof(PcgJump) * 2 * 256);
+    auto layout = [&](bool fast) {
+      int off = 0;
+      auto put = [&](GridLdsTab& t, size_t bytes) {
+        t.off = off;
+        t.bytes = (int)bytes;
+        off += (int)((bytes + 15) / 16 * 16);
+      };
+      put(d.lds.move, (size_t)nc * nact * sizeof(uint16_t));
+      put(d.lds.hbase, k == GP_OBS_HANSEN ? (size_t)nc * sizeof(uint32_t) : 0);
+      put(d.lds.hvec, k == GP_OBS_HANSEN_VEC ? hvec.size() : 0);
+      put(d.lds.t1, t1.size() * sizeof(int32_t));
+      put(d.lds.t2, t2.size() * sizeof(int32_t));
+      put(d.lds.coords, (k == GP_OBS_COORDS || k == GP_OBS_WINDOW) ? coords.size() * sizeof(int16_t) : 0);
+      put(d.lds.window, window.size());
+      put(d.lds.gv, goal_valid_h.size() * sizeof(uint16_t));
+      put(d.lds.av, agent_valid_h.size() * sizeof(uint16_t));
+      put(d.lds.doff, doff.size() * sizeof(int32_t));
+      put(d.lds.ofix, fast ? ofix.size() * sizeof(int32_t) : 0);
+      put(d.lds.avo, fast ? avo.size() * sizeof(uint32_t) : 0);
+      put(d.lds.jt, sizeof(PcgJump) * JT_LEVELS * JT_RADIX);  // jump tables last (the philox kernel omits them)
+      put(d.lds.jt8, sizeof(PcgJump) * 2 * 256);
+      return off;
+    };
+    int off = layout(true);
+    if (off > LDS_TABLE_BUDGET && (!ofix.empty() || !avo.empty())) off = layout(false);
     d.lds.total = off <= LDS_TABLE_BUDGET ? off : 0;
   }
   // fused numpy rollout: one 512-thread block per CU, <= 4 tiles of 2048 envs per block
   d.fnt = (int)((B + FEPB - 1) / FEPB);
-  {
-    const char* xm = getenv("GP_XMODE");  // exchange variant (tuning knob)
-    // bits 0-1: 1 = every block all-gathers the granules (default), 0 = block-0 aggregator; bit 4: plain
-    // (not non-temporal) staged output stores; bits 2-3 (stamps builds only): output-store diagnostics
-    d.xmode = xm ? atoi(xm) : 1;
-    // test knobs: a short spin limit and a block that never publishes force the device-error path
-    const char* sl = getenv("GP_SPIN_LIMIT");
-    d.spin_limit = sl && atol(sl) > 0 ? (uint32_t)atol(sl) : SPIN_LIMIT;
-    const char* fb = getenv("GP_FAULT_BLOCK");
-    d.fault_block = fb ? atoi(fb) : -1;
-  }
+  const GpDebugKnobs& dbg = gp_debug_knobs();  // diagnostic knobs (gp_debug_set); defaults in production
+  // exchange variant: bits 0-1: 1 = every block all-gathers the granules (default), 0 = block-0 aggregator;
+  // bit 4: plain (not non-temporal) staged output stores; bits 2-3 (stamps builds only): output diagnostics
+  d.xmode = dbg.xmode;
+  d.spin_limit = dbg.spin_limit ? dbg.spin_limit : SPIN_LIMIT;
+  d.fault_block = dbg.fault_block;
   {
     hipDeviceProp_t prop;
     GP_HIP_CHECK(hipGetDeviceProperties(&prop, device));
@@ -3083,15 +3090,13 @@ int GridBackend::build(const gp_grid_config* cfg) {
                                                              FTPB, d.lds.total));
     const int G = std::min({prop.multiProcessorCount, FMAXG, d.fnt});
     const int qpt = (d.fnt + G - 1) / G;
-    const char* off = getenv("GP_DISABLE_FUSED");  // testing knob: force the two-kernel numpy path
-    if (occ >= 1 && d.fnt <= FMAXT && qpt <= 4 && d.lds.total > 0 && !(off && off[0] == '1')) {
+    if (occ >= 1 && d.fnt <= FMAXT && qpt <= 4 && d.lds.total > 0 && !dbg.disable_fused) {
       fused_G = G;
       fused_qpt = qpt <= 1 ? 1 : (qpt <= 2 ? 2 : 4);
       const int k = cfg->obs_kind;
-      const char* ns = getenv("GP_NO_STAGING");  // tuning knob: direct output stores from the env waves
       // staged outputs: <= 2 tiles per block, scalar obs, and only complete tiles (every block owns exactly
       // fused_qpt full 2048-env tiles: the staged kernel drops the per-env bounds checks)
-      if (fused_qpt <= 2 && (k == GP_OBS_HANSEN || k == GP_OBS_TABLE) && !(ns && ns[0] == '1') &&
+      if (fused_qpt <= 2 && (k == GP_OBS_HANSEN || k == GP_OBS_TABLE) && !dbg.no_staging &&
           (int64_t)B == (int64_t)fused_qpt * G * FEPB) {
         int occ2 = 0;
         GP_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(

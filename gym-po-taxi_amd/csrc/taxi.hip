@@ -58,6 +58,7 @@ struct TaxiDev {
   int32_t off_trans, off_obs, off_cdf, off_valid, tab_bytes;
   uint32_t* st;                    // [B] s | nd << 12 | elapsed << 16
   TaxiSlot* mslot;                 // [grid]
+  uint32_t* derr;                  // device error word (GP_DERR_*)
   const int32_t* rp_state;         // replay: reset state per env (GP_RNG_REPLAY)
   const int32_t* rp_pd;            // replay: p*L + d per env
 };
@@ -132,7 +133,8 @@ __device__ __forceinline__ StepOut taxi_env_step(const TaxiDev& p, const uint8_t
   uint32_t s = u & 0xFFFu, nd = (u >> 12) & 0xFu, el = (u >> 16) + 1u;  // elapsed += 1 (:245)
   // numpy negative indexing of ACTIONS_YX[actions]: -5..-2 are the moves, -1 moves (0,0) but is not
   // a pickup/dropoff (p_or_d = actions == 4, extended_taxi.py:264) -> table column 5 (a no-op).
-  // Out-of-range actions raise in the reference; they are clamped here.
+  // Out-of-range actions raise IndexError in the reference: flagged (GP_DERR_ACTION), then clamped.
+  if (live && action_out_of_range(a, NACT)) flag_bad_action(p.derr);
   a = a < 0 ? (a == -1 ? NACT : max(a + NACT, 0)) : min(a, NACT - 1);
   const uint32_t t = l_trans(lds, p)[s * TCOL + (uint32_t)a];
   s = t & 0xFFFu;
@@ -445,6 +447,7 @@ struct TaxiBackend : EnvBackend {
   uint64_t philox_step = 0;
   std::vector<double> law;      // P(start state = valid[k])
   DevBuf b_tabs, b_st, b_slot;
+  DevErr derr;
   const int32_t* rp_state = nullptr;
   const int32_t* rp_pd = nullptr;
 
@@ -456,8 +459,9 @@ struct TaxiBackend : EnvBackend {
     d.key0 = key[0];
     d.key1 = key[1];
     philox_step = 0;
-    return GP_OK;
+    return derr.clear();
   }
+  int check() override { return derr.check("taxi"); }
   int set_rng_state(const RngHost& r) override {
     gp_set_error("taxi: the PCG64 stream is not used on the device (philox / replay modes)");
     return GP_E_UNSUPPORTED;
@@ -582,7 +586,7 @@ struct TaxiBackend : EnvBackend {
       out[2] += (double)x.length_sum;
       out[3] += (double)x.env_steps;
     }
-    return GP_OK;
+    return check();
   }
   int reset_distribution(double* out, int cap) const override {
     for (int k = 0; k < (int)law.size() && k < cap; ++k) out[k] = law[k];
@@ -772,6 +776,8 @@ int TaxiBackend::build(const gp_taxi_config* cfg) {
   grid = std::max(1, std::min(d.ntiles, prop.multiProcessorCount * occ));
   if (int e = b_slot.alloc(sizeof(TaxiSlot) * grid)) return e;
   d.mslot = b_slot.as<TaxiSlot>();
+  if (int e = derr.alloc()) return e;
+  d.derr = derr.ptr();
   if (d.tab_bytes > 64 * 1024) {
     gp_set_error("taxi: tables (%d B) exceed the LDS budget", d.tab_bytes);
     return GP_E_INVALID;

@@ -100,6 +100,8 @@ SIGNATURES = {
                                                           ctypes.POINTER(ctypes.c_double)]),
     "gp_standard_normal_words": (ctypes.c_int, [_vp, ctypes.c_int64, _vp, ctypes.c_int64,
                                                 ctypes.POINTER(ctypes.c_int64), _vp]),
+    "gp_debug_set": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int64]),
+    "gp_debug_reset": (None, []),
     "gp_normal_tail_counts": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_int64, ctypes.POINTER(ctypes.c_double),
                                              ctypes.c_int, ctypes.POINTER(ctypes.c_uint64),
                                              ctypes.POINTER(ctypes.c_double), _vp]),
@@ -151,6 +153,23 @@ def check(rc, what=""):
         msg = lib().gp_last_error()
         raise GymPoError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
     return rc
+
+
+class debug_knobs:
+    """Diagnostic knobs of envs created inside the block (gp_debug_set; restored to the defaults on exit):
+    disable_fused, no_staging, xmode, spin_limit, fault_block. Tests and A/B tooling only."""
+
+    def __init__(self, **knobs):
+        self.knobs = knobs
+
+    def __enter__(self):
+        for k, v in self.knobs.items():
+            check(lib().gp_debug_set(k.encode(), int(v)), f"gp_debug_set({k})")
+        return self
+
+    def __exit__(self, *exc):
+        lib().gp_debug_reset()
+        return False
 
 
 def int_to_u32_words(x):

@@ -88,12 +88,29 @@ class NativeVecEnv:
         dt = {"int32": torch.int32, "float32": torch.float32, "float64": torch.float64}[self._action_dtype]
         shape = ((self.num_envs,) if K is None else (K, self.num_envs)) + self._action_tail
         if isinstance(actions, torch.Tensor):
+            if actions.device.type == "cpu":
+                self._check_host_actions(actions.numpy())
             a = actions.to(device=self.device, dtype=dt)
         else:
-            a = torch.as_tensor(np.asarray(actions), device=self.device).to(dt)
+            an = np.asarray(actions)
+            self._check_host_actions(an)
+            a = torch.as_tensor(an, device=self.device).to(dt)
         if tuple(a.shape) != shape:
             a = a.reshape(shape)
         return a.contiguous()
+
+    def _check_host_actions(self, a):
+        """Host-resident discrete actions are range-checked before upload, raising the reference's own error:
+        numpy's IndexError from `action_matrix[action]` (msrooms.py:400, rooms.py:208) / `ACTIONS_YX[actions]`
+        (extended_taxi.py:248); negatives in [-n, 0) wrap as numpy indexing does. Device tensors are checked
+        on the device instead (GP_DERR_ACTION -> GymPoError from check() / metrics()), without a sync."""
+        n = getattr(getattr(self, "single_action_space", None), "n", None)
+        if n is None or self._action_dtype != "int32" or a.size == 0:
+            return
+        lo, hi = a.min(), a.max()
+        if hi >= n or lo < -n:
+            bad = int(hi) if hi >= n else int(lo)
+            raise IndexError(f"index {bad} is out of bounds for axis 0 with size {n}")
 
     def _post_obs(self, obs):
         return obs

@@ -204,7 +204,9 @@ int gp_valid_cells(const gp_env* env, int which, int32_t* out, int cap);
 int gp_metrics(gp_env* env, double out[4]);
 
 /* Syncs the handle's device and returns GP_E_DEVICE if any launch since the last seed failed on the
- * device (numpy-mode GRID: a persistent kernel's cross-block wait timed out), else GP_OK. The
+ * device (numpy-mode GRID: a persistent kernel's cross-block wait timed out; any kind: an action outside
+ * [-n, n) was given, where the reference raises IndexError at msrooms.py:400 / rooms.py:208 /
+ * extended_taxi.py:248 — the device clamps it and flags the handle), else GP_OK. The
  * asynchronous step/rollout calls cannot report such failures themselves; gp_metrics and
  * gp_get_rng_state run the same check. (No reference counterpart: numpy steps are synchronous.) */
 int gp_check(gp_env* env);
@@ -248,6 +250,15 @@ int gp_set_profiling(gp_env* env, int enable);
 int gp_profile_read(gp_env* env, double* total_ms, int64_t* n_launches);
 /* Same for the numpy-mode reset resolver kernel that follows each step kernel. */
 int gp_profile_read_resolver(gp_env* env, double* total_ms, int64_t* n_launches);
+
+/* ---- diagnostics (never needed in production; no reference counterpart) ----
+ * Process-wide test / tuning knobs, read by gp_create (handles created earlier keep their values):
+ *   "disable_fused" (GRID numpy mode: 1 = the two-kernel path only), "no_staging" (1 = the fused kernel's
+ *   env waves store outputs directly), "xmode" (fused exchange variant, default 1), "spin_limit" (polls
+ *   before a cross-block wait gives up, 0 = default), "fault_block" (this block never publishes: forces
+ *   the timeout path; -1 = off). gp_debug_reset restores the defaults. Unknown key: GP_E_INVALID. */
+int gp_debug_set(const char* key, int64_t value);
+void gp_debug_reset(void);
 
 /* ---- host-only helpers (no device needed) ---- */
 /* PCG64 state {state_hi, state_lo, inc_hi, inc_lo, has_uint32, uinteger} that numpy's

@@ -6,8 +6,8 @@ then gives up after GridCtl's spin limit, sets the device error flag, and every 
 as soon as it sees the flag, so the launch still drains. The host reports the flag as GP_E_DEVICE
 (GymPoError) from check(), metrics() and rng_state; reseeding clears it.
 
-The test forces the failure deterministically with two test knobs read at env creation:
-GP_FAULT_BLOCK (that block never publishes) and GP_SPIN_LIMIT (a short wait limit).
+The test forces the failure deterministically with two diagnostic knobs read at env creation
+(gp_debug_set): fault_block (that block never publishes) and spin_limit (a short wait limit).
 """
 import pytest
 
@@ -15,17 +15,15 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("fused", [True, False])
-def test_spin_timeout_raises_instead_of_silent_results(fused, gpu_device, monkeypatch):
+def test_spin_timeout_raises_instead_of_silent_results(fused, gpu_device):
     import torch
     from gym_po_amd import MultistoryFourRoomsEnv
-    from gym_po_amd._lib import GymPoError
+    from gym_po_amd._lib import GymPoError, debug_knobs
     B = 2048 * 8
-    if not fused:
-        monkeypatch.setenv("GP_DISABLE_FUSED", "1")
-    env_ok = MultistoryFourRoomsEnv(B, grid_z=1, obs_type="hansen", device=gpu_device)
-    monkeypatch.setenv("GP_SPIN_LIMIT", "4000")
-    monkeypatch.setenv("GP_FAULT_BLOCK", "1")
-    env = MultistoryFourRoomsEnv(B, grid_z=1, obs_type="hansen", device=gpu_device)
+    with debug_knobs(disable_fused=not fused):
+        env_ok = MultistoryFourRoomsEnv(B, grid_z=1, obs_type="hansen", device=gpu_device)
+    with debug_knobs(disable_fused=not fused, spin_limit=4000, fault_block=1):
+        env = MultistoryFourRoomsEnv(B, grid_z=1, obs_type="hansen", device=gpu_device)
     assert (env.query("fused_blocks") > 0) == fused
     env.reset(seed=3)
     acts = torch.randint(0, 4, (6, B), dtype=torch.int32, device=gpu_device)

@@ -303,11 +303,13 @@ def test_numpy_rollout_equals_stepwise(gpu_device):
 
 @pytest.mark.parametrize("name", ["fr_hansen_tl20", "fr_vgh_z3_randgoal", "rooms_2_goal_mdp_randgoal",
                                   "rooms_4_grid3"])
-def test_two_kernel_numpy_path_bit_exact(name, gpu_device, monkeypatch):
+def test_two_kernel_numpy_path_bit_exact(name, gpu_device):
     """The non-fused numpy path (streaming step kernel + reset resolver), used above 4M envs."""
-    monkeypatch.setenv("GP_DISABLE_FUSED", "1")
+    from gym_po_amd._lib import debug_knobs
     meta, data = load_case(name)
-    env = make_env(meta)
+    with debug_knobs(disable_fused=1):
+        env = make_env(meta)
+    assert env.query("fused_blocks") == 0
     acts = step_actions(meta)
     np.testing.assert_array_equal(np_obs(reset_obs(env, meta["seed"])).astype(np.float64),
                                   data["obs0"].astype(np.float64))
@@ -319,9 +321,10 @@ def test_two_kernel_numpy_path_bit_exact(name, gpu_device, monkeypatch):
     assert rng_tuple(env.rng_state) == [int(x) for x in data["final_rng_state"]]
 
 
-def test_two_kernel_forced_rejection(gpu_device, monkeypatch):
-    monkeypatch.setenv("GP_DISABLE_FUSED", "1")
-    test_forced_rejection_slow_path_step(777, gpu_device)
+def test_two_kernel_forced_rejection(gpu_device):
+    from gym_po_amd._lib import debug_knobs
+    with debug_knobs(disable_fused=1):
+        test_forced_rejection_slow_path_step(777, gpu_device)
 
 
 @pytest.mark.parametrize("B", [4096 * 256 + 5, 2_500_000])
