@@ -102,11 +102,14 @@ __device__ __forceinline__ void stage_tables(const CrDev& p, uint8_t* lds) {
 // ziggurat on 64-bit words. `r` is the normal's first word; `next` yields the words it consumes after that
 // (a rejected layer draw or the tail, ~1% of normals). Operation for operation as numpy (no FMA
 // contraction in this file), so over numpy's word stream it returns numpy's values (checked bit for bit
-// against numpy by gp_standard_normal_words; exp / log1p are the device libm's, so a tail value may differ
-// from glibc's in the last bit).
-// Compact float64 exp and log1p for the ziggurat's slow path (GP_ZIG_OCML=0, default; the device libm's
-// versions with GP_ZIG_OCML=1). Both within ~1 ulp over the ranges used (exp: [-6.7, 0]; log1p(-u): u in
-// [0, 1 - 2^-53]); explicit fma (this file disables contraction).
+// against numpy by gp_standard_normal_words).
+// log1p of the tail: numpy calls the C library's log1p (npy_log1p -> libm; NOT the SIMD np.log1p ufunc, which
+// differs from libm in ~1% of last bits). zlog1p_neg restates glibc 2.35's log1p (sysdeps/ieee754/dbl-64/
+// s_log1p.c: fdlibm's reduction and its Lp1..Lp7 polynomial in the parallel R1 + z2 R2 + z4 R3 + z6 R4 order),
+// IEEE double ops without contraction, so tail values equal numpy's bit for bit; host copy gp_log1p_libm for
+// the CPU test against libm (tests/test_log1p_cpu.py). exp of the wedge test: a compact ~1-ulp version
+// (GP_ZIG_OCML=1: the device libm's) -- a wedge accept / reject can only differ from glibc's when both sides of
+// `(fi[i-1] - fi[i]) u + fi[i] < exp(-x^2 / 2)` agree to within an ulp (probability ~1e-16 per wedge draw).
 #ifndef GP_ZIG_OCML
 #define GP_ZIG_OCML 0
 #endif
@@ -133,32 +136,63 @@ __device__ __forceinline__ double zexp(double y) {
   return ldexp(q, (int)k);
 #endif
 }
-__device__ __forceinline__ double zlog1p_neg(double u) {  // log1p(-u) = log(v), v = 1 - u (exact for u = k 2^-53)
-#if GP_ZIG_OCML
-  return log1p(-u);
-#else
-  const double v = 1.0 - u;
-  int e;
-  double m = frexp(v, &e);                                     // v = m 2^e, m in [0.5, 1)
-  if (m < 0.7071067811865476) {
-    m = m * 2.0;
-    e -= 1;
+GP_HD int32_t zhi(double x) { return (int32_t)(__builtin_bit_cast(uint64_t, x) >> 32); }
+GP_HD double zset_hi(double x, int32_t h) {
+  return __builtin_bit_cast(double, (__builtin_bit_cast(uint64_t, x) & 0xFFFFFFFFull) | ((uint64_t)(uint32_t)h << 32));
+}
+// log1p(-u) for u in [0, 1): glibc's __log1p(x) at x = -u (the branches x >= 0.41422, |x| < 2^-54 and
+// x <= -1 cannot occur here). No fma anywhere: every operation is a separately rounded IEEE double op.
+GP_HD double zlog1p_neg(double u) {
+  const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+  const double Lp1 = 6.666666666666735130e-01, Lp2 = 3.999999999940941908e-01, Lp3 = 2.857142874366239149e-01,
+               Lp4 = 2.222219843214978396e-01, Lp5 = 1.818357216161805012e-01, Lp6 = 1.531383769920937332e-01,
+               Lp7 = 1.479819860511658591e-01;
+  const double x = -u;
+  const int32_t hx = zhi(x), ax = hx & 0x7fffffff;
+  if (ax < 0x3e200000) return x - x * x * 0.5;  // |x| < 2^-29 (u = 0: x - 0 = -0.0, numpy's log1p(-0.0))
+  int32_t k = 1, hu = 0;
+  double f = 0.0, c = 0.0;
+  if (hx > 0 || hx <= (int32_t)0xbfd2bec3) {  // -0.2929 < x < 0.41422 (glibc keeps fdlibm's 0xbfd2bec3)
+    k = 0;
+    f = x;
+    hu = 1;
+  } else {
+    double v = 1.0 + x;
+    hu = zhi(v);
+    k = (hu >> 20) - 1023;
+    c = (k > 0) ? 1.0 - (v - x) : x - (v - 1.0);  // correction term
+    c /= v;
+    hu &= 0x000fffff;
+    if (hu < 0x6a09e) {
+      v = zset_hi(v, hu | 0x3ff00000);  // normalize v
+    } else {
+      k += 1;
+      v = zset_hi(v, hu | 0x3fe00000);  // normalize v / 2
+      hu = (0x00100000 - hu) >> 2;
+    }
+    f = v - 1.0;
   }
-  const double sn = (m - 1.0) / (m + 1.0), s2 = sn * sn;       // log m = 2 atanh(s), |s| <= 0.1716
-  double q = 1.0 / 23.0;
-  q = fma(q, s2, 1.0 / 21.0);
-  q = fma(q, s2, 1.0 / 19.0);
-  q = fma(q, s2, 1.0 / 17.0);
-  q = fma(q, s2, 1.0 / 15.0);
-  q = fma(q, s2, 1.0 / 13.0);
-  q = fma(q, s2, 1.0 / 11.0);
-  q = fma(q, s2, 1.0 / 9.0);
-  q = fma(q, s2, 1.0 / 7.0);
-  q = fma(q, s2, 1.0 / 5.0);
-  q = fma(q, s2, 1.0 / 3.0);
-  const double lm = fma(2.0 * sn * s2, q, 2.0 * sn);
-  return fma((double)e, 0.6931471803691238, fma((double)e, 1.9082149292705877e-10, lm));
-#endif
+  const double hfsq = 0.5 * f * f;
+  const double dk = (double)k;
+  if (hu == 0) {  // |f| < 2^-20
+    if (f == 0.0) {
+      if (k == 0) return 0.0;
+      c += dk * ln2_lo;
+      return dk * ln2_hi + c;
+    }
+    const double R = hfsq * (1.0 - 0.66666666666666666 * f);
+    if (k == 0) return f - R;
+    return dk * ln2_hi - ((R - (dk * ln2_lo + c)) - f);
+  }
+  const double s = f / (2.0 + f);
+  const double z = s * s;
+  const double R1 = z * Lp1, z2 = z * z;
+  const double R2 = Lp2 + z * Lp3, z4 = z2 * z2;
+  const double R3 = Lp4 + z * Lp5, z6 = z4 * z2;
+  const double R4 = Lp6 + z * Lp7;
+  const double R = R1 + z2 * R2 + z4 * R3 + z6 * R4;
+  if (k == 0) return f - (hfsq - s * (hfsq + R));
+  return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + (dk * ln2_lo + c))) - f);
 }
 
 // numpy's ki / wi / fi tables (ziggurat_tables.h), one array: ki at 0, wi at 256, fi at 512.
@@ -1697,6 +1731,17 @@ __global__ __launch_bounds__(256) void zig_tail_kernel(uint32_t k0, uint32_t k1,
   }
 }
 }  // namespace
+
+// Host copy of the device's zlog1p_neg (same source, same IEEE operation order): the CPU suite checks it against
+// the C library's log1p, which numpy's tail draws call.
+extern "C" int gp_zig_log1p_neg(const double* u, double* out, int64_t n) {
+  if (n < 0 || (n && (!u || !out))) {
+    gp_set_error("gp_zig_log1p_neg: bad arguments");
+    return GP_E_INVALID;
+  }
+  for (int64_t i = 0; i < n; ++i) out[i] = zlog1p_neg(u[i]);
+  return GP_OK;
+}
 
 extern "C" int gp_standard_normal_words(const uint64_t* words, int64_t nwords, double* out, int64_t n, int64_t* used,
                                         void* stream) {

@@ -96,7 +96,7 @@ struct GridDev {
   int32_t fnt;              // 2048-env fused tiles
   const PcgJump* ftj;       // [fnt] jump by tau*FEPB + 1
   const PcgJump* flt4;      // [FTPB] jump by 4t
-  const PcgJump* fjB;       // [1] jump by B
+  const PcgJump* fjB;       // [2] jump by B, jump by G * FEPB (a block's tile stride)
   uint64_t* fslot;          // [2][3][G] tagged block granules, then [2][fnt] tile words
   unsigned long long* dbg;  // GP_STAMPS diagnostic builds: [G][64][8] s_memtime stamps
   GridLds lds;
@@ -940,6 +940,13 @@ constexpr uint32_t TAG_MASK = 0x7FFFu;
 #ifndef GP_ALIGNBIT
 #define GP_ALIGNBIT 0
 #endif
+//  GP_PRO2 1: the launch prologue pays ONE global-load latency: the env waves issue their state / action /
+//    tile-jump loads first and copy only the small lookup tables (everything before the PCG jump tables,
+//    ~3.5 KB for FourRooms) into LDS before the block barrier; the store waves, idle until the first step's
+//    B1, copy the jump tables (26 KB) behind it, and the control wave sets up from the global copies.
+#ifndef GP_PRO2
+#define GP_PRO2 1
+#endif
 
 struct FusedShared {
   uint32_t wcnt[FMAXQ][FENVW];   // per-env-wave reset counts of each tile
@@ -1233,6 +1240,35 @@ __device__ __forceinline__ void lds_image_copy(char* dyn, const char* src, int b
     if (a5) d[i0 + 5 * bd] = v5;
     if (a6) d[i0 + 6 * bd] = v6;
     if (a7) d[i0 + 7 * bd] = v7;
+  }
+}
+
+// Copy image bytes [b0, b1) (multiples of 16) to the same LDS offsets with threads t0 .. t0 + nt - 1, every
+// thread's 16-B loads in flight before its first LDS store.
+__device__ __forceinline__ void lds_image_copy_range(char* dyn, const char* src, int b0, int b1, int t, int nthr) {
+  const int c0 = b0 >> 4, n = (b1 - b0) >> 4;
+  const uint4* s = reinterpret_cast<const uint4*>(src) + c0;
+  uint4* d = reinterpret_cast<uint4*>(dyn) + c0;
+  for (int i0 = t; i0 < n; i0 += 8 * nthr) {
+    uint4 v0, v1, v2, v3, v4, v5, v6, v7;
+    const bool a1 = i0 + nthr < n, a2 = i0 + 2 * nthr < n, a3 = i0 + 3 * nthr < n, a4 = i0 + 4 * nthr < n,
+               a5 = i0 + 5 * nthr < n, a6 = i0 + 6 * nthr < n, a7 = i0 + 7 * nthr < n;
+    v0 = s[i0];
+    if (a1) v1 = s[i0 + nthr];
+    if (a2) v2 = s[i0 + 2 * nthr];
+    if (a3) v3 = s[i0 + 3 * nthr];
+    if (a4) v4 = s[i0 + 4 * nthr];
+    if (a5) v5 = s[i0 + 5 * nthr];
+    if (a6) v6 = s[i0 + 6 * nthr];
+    if (a7) v7 = s[i0 + 7 * nthr];
+    d[i0] = v0;
+    if (a1) d[i0 + nthr] = v1;
+    if (a2) d[i0 + 2 * nthr] = v2;
+    if (a3) d[i0 + 3 * nthr] = v3;
+    if (a4) d[i0 + 4 * nthr] = v4;
+    if (a5) d[i0 + 5 * nthr] = v5;
+    if (a6) d[i0 + 6 * nthr] = v6;
+    if (a7) d[i0 + 7 * nthr] = v7;
   }
 }
 
@@ -1634,11 +1670,31 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
       for (int i = 0; i < 4; ++i) gl[q][i] = fixed_goal;
     }
     load4f<int32_t>(act, env0, B, a_cur[q]);
+    jtile[q] = p.ftj[min(tau, nt - 1)];
+  }
+  const PcgJump jstride = p.fjB[1];
+  if constexpr (GP_PRO2) {
+    // keep the state / action / jump loads above ahead of the table copy's (the compiler otherwise sinks them
+    // below it, and their latency lands after the barrier): their latencies overlap
+    asm volatile("" ::: "memory");
+    // the small lookup tables and shared words while the loads above are in flight, then the block barrier
+    char* dyn = const_cast<char*>(tb.dyn);
+    if (tid < NA * NA) const_cast<uint64_t*>(s_thr)[tid] = GP_TRIMS ? thr_on_u64(p.thr[tid]) : p.thr[tid];
+    if (tid < 4) sh.jB[tid] = (&p.fjB->a_hi)[tid];
+    if (tid < 8) sh.dof[tid] = (OK == GP_OBS_HANSEN && p.doff && tid < p.obs_dirs) ? p.doff[tid] : 0x7FFFFFFF;
+    if (tid == 0) sh.rdone = 0;
+    lds_image_copy_range(dyn, p.limg, 0, p.lds.jt.off, tid, FENVW * 64);
+    __syncthreads();
+    LSTAMP(1);
+  }
+#pragma unroll
+  for (int q = 0; q < QPT; ++q) {
+    const int tau = q * G + (int)blockIdx.x;
+    const int env0 = tau * FEPB + tid * EPT;
     if constexpr (TRIMS) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) a_cur[q][i] = action_row<NA>(a_cur[q][i], &p.ctl->err);
     }
-    jtile[q] = p.ftj[min(tau, nt - 1)];
     vmask[q] = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) vmask[q] |= (STG || env0 + i < B) ? 1u << i : 0u;
@@ -1649,6 +1705,7 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
         if ((vmask[q] >> i) & 1u) lens += ae[q][i] >> 16;
     }
   }
+  LSTAMP(4);
 #pragma unroll
   for (int d = 0; d < 8; ++d)
     dof[d] = (OK == GP_OBS_HANSEN && d < p.obs_dirs) ? vgpr_u32(tb.doff(d)) : 0x7FFFFFFF;
@@ -1656,8 +1713,12 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
   // it was spilled to VGPR lanes and re-read by v_readlane + v_mov in every draw).
   const u128 incv = mk128(((uint64_t)vgpr_u32((uint32_t)(hi64(st.inc) >> 32)) << 32) | vgpr_u32((uint32_t)hi64(st.inc)),
                           ((uint64_t)vgpr_u32((uint32_t)(lo64(st.inc) >> 32)) << 32) | vgpr_u32((uint32_t)lo64(st.inc)));
+  // lane draw states jump(s0, e0 + 1): tile 0 by its tile base then this thread's offset (two affine maps, no
+  // composition), the block's further tiles by the tile stride from the previous one
+  S[0] = apply_jump(jl, apply_jump(jtile[0], st.s0));
 #pragma unroll
-  for (int q = 0; q < QPT; ++q) S[q] = apply_jump(compose_jump(jl, jtile[q]), st.s0);
+  for (int q = 1; q < QPT; ++q) S[q] = apply_jump(jstride, S[q - 1]);
+  LSTAMP(5);
   for (int k = 0; k < K; ++k) {
     STAMP(0);
     const uint32_t tag0 = (step_base + (uint32_t)k + 1u) * 4u;
@@ -1952,9 +2013,11 @@ __device__ __forceinline__ void fused_ctrl(const GridDev& p_in, FusedShared& sh,
     const int q = 2 * c + (lane >> 5);
     ctau[c] = q * G + (int)blockIdx.x;
     chk[c] = ncalls && q < QPT && ctau[c] < nt;
-    CS[c] = chk[c] ? pcg_jump(tb.jt(), st.s0, (uint32_t)p.B + (uint32_t)ctau[c] * (RCOV / 2) + (uint32_t)(lane & 31))
+    CS[c] = chk[c] ? pcg_jump(GP_PRO2 ? p.jt : tb.jt(), st.s0,
+                              (uint32_t)p.B + (uint32_t)ctau[c] * (RCOV / 2) + (uint32_t)(lane & 31))
                    : (u128)0;
   }
+  if constexpr (GP_PRO2) __syncthreads();  // the prologue barrier (the env waves staged the small tables)
   uint32_t dummy_u[QPT][4];
   int dummy_i[QPT][4];
   const uint32_t dummy_c[QPT] = {};
@@ -2122,6 +2185,19 @@ __device__ __forceinline__ void fused_ctrl(const GridDev& p_in, FusedShared& sh,
 }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// Cache policy of the staged output stream (16-B stores by the store waves). GP_OUT_WT 1: `sc1` vector stores,
+// written through the XCD's L2 and dropped from it, so a launch ends with no dirty output lines to write back
+// (the kernel-end release pays for every dirty byte: MI355X_MICROARCH.md "boundary"); 0: `nt` (kept in L2).
+#ifndef GP_OUT_WT
+#define GP_OUT_WT 0  // measured: sc1 made K = 128 launches 9% and K = 20 launches 2% slower than nt
+#endif
+__device__ __forceinline__ void out_store16(u32x4* d, u32x4 v) {
+#if GP_OUT_WT
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(d), "v"(v));  // no clobber: never read back
+#else
+  __builtin_nontemporal_store(v, d);
+#endif
+}
 // Copy one staged output plane of tile tau (n32 = 32-bit words per env) to HBM: 16-B chunks of
 // 4 (n32 = 1) or 16 (n32 = 0: byte planes) envs when the destination is 16-B aligned, else 4-B words.
 __device__ __forceinline__ void stage_plane(const char* src, char* dst, int env_base, int B, int esz, int sl,
@@ -2137,14 +2213,14 @@ __device__ __forceinline__ void stage_plane(const char* src, char* dst, int env_
 #pragma unroll
       for (int j = 0; j < (N4 + NL - 1) / NL; ++j) {
         if (N4 % NL != 0 && sl + j * NL >= N4) break;
-        if (nt) __builtin_nontemporal_store(s4[j * NL], d4 + j * NL);
+        if (nt) out_store16(d4 + j * NL, s4[j * NL]);
         else d4[j * NL] = s4[j * NL];
       }
     } else {
 #pragma unroll
       for (int j = 0; j < (N1 + NL - 1) / NL; ++j) {
         if (N1 % NL != 0 && sl + j * NL >= N1) break;
-        if (nt) __builtin_nontemporal_store(s4[j * NL], d4 + j * NL);
+        if (nt) out_store16(d4 + j * NL, s4[j * NL]);
         else d4[j * NL] = s4[j * NL];
       }
     }
@@ -2156,7 +2232,7 @@ __device__ __forceinline__ void stage_plane(const char* src, char* dst, int env_
     const int e = env_base + c * epc;
     if (e + epc <= B) {
       if (a16 && nt)
-        __builtin_nontemporal_store(reinterpret_cast<const u32x4*>(src)[c], reinterpret_cast<u32x4*>(dst + (size_t)e * esz));
+        out_store16(reinterpret_cast<u32x4*>(dst + (size_t)e * esz), reinterpret_cast<const u32x4*>(src)[c]);
       else if (a16)
         *reinterpret_cast<uint4*>(dst + (size_t)e * esz) = reinterpret_cast<const uint4*>(src)[c];
       else
@@ -2187,6 +2263,10 @@ __device__ __forceinline__ void fused_store(const GridDev& p, FusedShared& sh, c
   int32_t dov[QPT][4];
   const uint32_t dc[QPT] = {};
   (void)dov;
+  if constexpr (GP_PRO2) {
+    __syncthreads();  // the prologue barrier; then the PCG jump tables behind the first step's transitions
+    lds_image_copy_range(const_cast<char*>(tb.dyn), p.limg, p.lds.jt.off, p.lds.total, sl, FSTW * 64);
+  }
   for (int k = 0; k < K; ++k) {
     const uint32_t tag0 = (step_base + (uint32_t)k + 1u) * 4u;
     uint64_t* slots = p.fslot + (size_t)((step_base + (uint32_t)k) & 1u) * 3 * G;
@@ -2237,13 +2317,15 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
   // The launch prologue: the lookup-table image into LDS in one copy loop (the fused path is only taken
   // when it fits) and the small shared words, then a block barrier. (Letting each role issue its own first
   // global loads before this copy, to overlap their latency, measured slower: 17.2 vs 16.1 µs at K = 1.)
-  if (tid < NA * NA) s_thr[tid] = GP_TRIMS ? thr_on_u64(p.thr[tid]) : p.thr[tid];
-  lds_image_copy(dyn, p.limg, p.lds.total);
-  if (tid < 4) sh.jB[tid] = (&p.fjB->a_hi)[tid];
-  if (tid == 0) sh.rdone = 0;
-  if (tid < 8) sh.dof[tid] = (OK == GP_OBS_HANSEN && p.doff && tid < p.obs_dirs) ? p.doff[tid] : 0x7FFFFFFF;
-  __syncthreads();
-  LSTAMP(1);
+  if constexpr (!GP_PRO2) {
+    if (tid < NA * NA) s_thr[tid] = GP_TRIMS ? thr_on_u64(p.thr[tid]) : p.thr[tid];
+    lds_image_copy(dyn, p.limg, p.lds.total);
+    if (tid < 4) sh.jB[tid] = (&p.fjB->a_hi)[tid];
+    if (tid == 0) sh.rdone = 0;
+    if (tid < 8) sh.dof[tid] = (OK == GP_OBS_HANSEN && p.doff && tid < p.obs_dirs) ? p.doff[tid] : 0x7FFFFFFF;
+    __syncthreads();
+    LSTAMP(1);
+  }
   float rsum = 0.f;
   uint32_t eps = 0, lens = 0, nst = 0;
   if (wid == FENVW) {
@@ -2608,10 +2690,11 @@ int GridBackend::upload_rng() {
     const PcgJump step_ftile = pcg_jump_params((u128)FEPB, rng.inc);
     ft[0] = pcg_jump_params((u128)1, rng.inc);
     for (int k = 1; k < d.fnt; ++k) ft[k] = compose(step_ftile, ft[k - 1]);
-    const PcgJump jb = pcg_jump_params((u128)B, rng.inc);
+    const PcgJump jb[2] = {pcg_jump_params((u128)B, rng.inc),                   // random(B)
+                           pcg_jump_params((u128)fused_G * FEPB, rng.inc)};  // tile stride of a block (q -> q + 1)
     GP_HIP_CHECK(hipMemcpy(b_flt4.p, fl.data(), fl.size() * sizeof(PcgJump), hipMemcpyHostToDevice));
     GP_HIP_CHECK(hipMemcpy(b_ftj.p, ft.data(), ft.size() * sizeof(PcgJump), hipMemcpyHostToDevice));
-    GP_HIP_CHECK(hipMemcpy(b_fjB.p, &jb, sizeof(PcgJump), hipMemcpyHostToDevice));
+    GP_HIP_CHECK(hipMemcpy(b_fjB.p, jb, sizeof(jb), hipMemcpyHostToDevice));
   }
   return refresh_lds_image();
 }
@@ -3114,7 +3197,7 @@ int GridBackend::build(const gp_grid_config* cfg) {
       (e = b_tlist.alloc(sizeof(uint16_t) * (size_t)d.nblk * EPB)) || (e = b_rflag.alloc(sizeof(uint32_t) * 256)) ||
       (e = b_mslot.alloc(sizeof(MetricSlot) * (size_t)nslots)) ||
       (e = b_ftj.alloc(sizeof(PcgJump) * (size_t)std::max(d.fnt, 1))) || (e = b_flt4.alloc(sizeof(PcgJump) * FTPB)) ||
-      (e = b_fjB.alloc(sizeof(PcgJump))) || (e = b_fslot.alloc(sizeof(uint64_t) * 8 * (size_t)std::max(d.fnt, 1))))
+      (e = b_fjB.alloc(2 * sizeof(PcgJump))) || (e = b_fslot.alloc(sizeof(uint64_t) * 8 * (size_t)std::max(d.fnt, 1))))
     return e;
   d.move = b_move.as<uint16_t>();
   d.thr = b_thr.as<uint64_t>();

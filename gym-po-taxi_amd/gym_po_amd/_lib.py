@@ -100,6 +100,8 @@ SIGNATURES = {
                                                           ctypes.POINTER(ctypes.c_double)]),
     "gp_standard_normal_words": (ctypes.c_int, [_vp, ctypes.c_int64, _vp, ctypes.c_int64,
                                                 ctypes.POINTER(ctypes.c_int64), _vp]),
+    "gp_zig_log1p_neg": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                        ctypes.c_int64]),
     "gp_debug_set": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int64]),
     "gp_debug_reset": (None, []),
     "gp_normal_tail_counts": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_int64, ctypes.POINTER(ctypes.c_double),

@@ -265,6 +265,10 @@ void gp_debug_reset(void);
  * Generator(PCG64(SeedSequence(entropy, spawn_key))) starts from. */
 int gp_pcg64_seed_state(const uint32_t* entropy, int n_entropy, const uint32_t* spawn_key, int n_spawn,
                         uint64_t out[6]);
+/* log1p(-u[i]) for u in [0, 1) exactly as the C library computes it (glibc 2.35 __log1p restated, the version
+ * the C-ROOMS exact mode's ziggurat tail uses on the device: numpy's random_standard_normal calls npy_log1p ->
+ * libm, distributions.c). Host-only check entry for the CPU tests. */
+int gp_zig_log1p_neg(const double* u, double* out, int64_t n);
 /* P(argmax = k), k < m, for Multinomial(n, uniform over m) counts, ties to the first index:
  * the law of TaxiVecEnv._reset_mask (extended_taxi.py:344-352). Returns m. */
 int gp_argmax_multinomial_distribution(int m, int n, double* out);

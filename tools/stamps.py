@@ -46,6 +46,12 @@ print(f"  first entry -> step 0 start: min {s0.min() - t0} max {s0.max() - t0} n
       f"loop done -> kernel end median {np.median(L4[:, 3] - L4[:, 2]):.0f} max {np.max(L4[:, 3] - L4[:, 2])} ns")
 print(f"  first entry -> last kernel end {L4[:, 3].max() - t0} ns = {(L4[:, 3].max() - t0) / K:.0f} ns/step; "
       f"last step start -> last loop done {L4[:, 2].max() - (a[:G, min(K, 64) - 1, 0] * 10).max()} ns")
+L6 = raw[NS:].reshape(256, 8)[:G, 4:6] * 10
+print(f"  env prologue after the barrier: action rows done median {np.median(L6[:, 0] - L4[:, 1]):.0f} ns, lane "
+      f"states ready median {np.median(L6[:, 1] - L4[:, 1]):.0f} ns (max over blocks {np.max(L6[:, 1] - t0)} ns from "
+      f"first entry)")
+st_k = a[:G, :min(K, 64), 0] * 10 - t0
+print("  step k start, max over blocks (ns from first entry), k = 0..7:", [int(x) for x in st_k.max(0)[:8]])
 env.set_profiling(True)
 for _ in range(5):
     env.rollout(acts)
