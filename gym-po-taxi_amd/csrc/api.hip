@@ -207,6 +207,7 @@ int gp_debug_set(const char* key, int64_t value) {
   else if (!strcmp(key, "xmode")) g_dbg.xmode = (int)value;
   else if (!strcmp(key, "spin_limit")) g_dbg.spin_limit = value > 0 ? (uint32_t)value : 0u;
   else if (!strcmp(key, "fault_block")) g_dbg.fault_block = (int)value;
+  else if (!strcmp(key, "fused_tile")) g_dbg.fused_tile = (int)value;
   else {
     gp_set_error("gp_debug_set: unknown key '%s'", key);
     return GP_E_INVALID;
@@ -345,6 +346,38 @@ int gp_rollout(gp_env* env, int K, const void* actions, void* obs, float* rew, u
   if (K == 0) return GP_OK;
   return env->be->rollout(K, actions, obs, rew, term, trunc, (hipStream_t)stream);
 }
+
+struct gp_plan {
+  gp_env* env;
+  int K;
+  const void* act;
+  void* obs;
+  float* rew;
+  uint8_t* term;
+  uint8_t* trunc;
+  hipStream_t stream;
+};
+
+int gp_plan_create(gp_env* env, int K, const void* actions, void* obs, float* rew, uint8_t* term, uint8_t* trunc,
+                   void* stream, gp_plan** out) {
+  GP_REQUIRE_ENV();
+  if (!out || K < 1 || !actions || !obs || !rew || !term || !trunc) {
+    gp_set_error("gp_plan_create: bad arguments");
+    return GP_E_INVALID;
+  }
+  *out = new gp_plan{env, K, actions, obs, rew, term, trunc, (hipStream_t)stream};
+  return GP_OK;
+}
+
+int gp_plan_run(gp_plan* plan) {
+  if (!plan || !plan->env || !plan->env->be) {
+    gp_set_error("gp_plan_run: null plan");
+    return GP_E_INVALID;
+  }
+  return plan->env->be->rollout(plan->K, plan->act, plan->obs, plan->rew, plan->term, plan->trunc, plan->stream);
+}
+
+void gp_plan_destroy(gp_plan* plan) { delete plan; }
 
 int gp_get_state(gp_env* env, void* a, void* b, void* c, void* d, void* stream) {
   GP_REQUIRE_ENV();

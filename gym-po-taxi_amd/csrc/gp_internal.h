@@ -26,6 +26,7 @@ std::vector<PcgJump> build_jump_tables(u128 inc);
 // Diagnostic knobs (gp_debug_set), read by the backends at gp_create.
 struct GpDebugKnobs {
   int disable_fused = 0, no_staging = 0, xmode = 1, fault_block = -1;
+  int fused_tile = 0;       // GRID fused kernel: envs per tile (512 / 1024 / 2048); 0 = chosen by size
   uint32_t spin_limit = 0;  // 0 = the kernel's default
 };
 const GpDebugKnobs& gp_debug_knobs();

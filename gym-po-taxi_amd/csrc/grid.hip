@@ -93,10 +93,12 @@ struct GridDev {
   uint16_t* tlist;   // [nblk*EPB] local offsets of a tile's resetting envs, ascending
   uint32_t* rflag;   // [<=256] K2 per-block rejection flags, tagged with the epoch
   // fused numpy rollout
-  int32_t fnt;              // 2048-env fused tiles
-  const PcgJump* ftj;       // [fnt] jump by tau*FEPB + 1
+  int32_t fnt;              // fused tiles
+  int32_t ftile, faw;       // envs per fused tile (512, 1024 or 2048 = FEPB) and the env waves that own them
+                            // (ftile / 256; the other env waves of the block only join the barriers)
+  const PcgJump* ftj;       // [fnt] jump by tau*ftile + 1
   const PcgJump* flt4;      // [FTPB] jump by 4t
-  const PcgJump* fjB;       // [2] jump by B, jump by G * FEPB (a block's tile stride)
+  const PcgJump* fjB;       // [2] jump by B, jump by G * ftile (a block's tile stride)
   uint64_t* fslot;          // [2][3][G] tagged block granules, then [2][fnt] tile words
   unsigned long long* dbg;  // GP_STAMPS diagnostic builds: [G][64][8] s_memtime stamps
   GridLds lds;
@@ -1603,13 +1605,13 @@ __device__ __forceinline__ uint32_t fused_effective_action(const uint64_t* s_thr
 
 // The obs of the previous step's resetters (their provisional obs were stored with the step's
 // outputs): written during the next step's exchange wait.
-template <int OK, int QPT>
+template <int OK, int QPT, bool SMALL>
 __device__ __forceinline__ void flush_reset_obs(const GridDev& p, const LTabs& tb, void* ob, int tid,
                                                 const uint32_t (&pc)[QPT][4], uint32_t (&pfm)[QPT]) {
 #pragma unroll
   for (int q = 0; q < QPT; ++q) {
     if (!pfm[q]) continue;
-    const int env0 = (q * (int)gridDim.x + (int)blockIdx.x) * FEPB + tid * EPT;
+    const int env0 = (q * (int)gridDim.x + (int)blockIdx.x) * (SMALL ? p.ftile : FEPB) + tid * EPT;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       if ((pfm[q] >> i) & 1u) write_obs<OK>(p, tb, env0 + i, (int)(pc[q][i] >> 16), (int)(pc[q][i] & 0xFFFFu), ob);
@@ -1618,7 +1620,7 @@ __device__ __forceinline__ void flush_reset_obs(const GridDev& p, const LTabs& t
 }
 
 // The env waves of the fused kernel.
-template <int OK, int QPT, int NA, bool STG>
+template <int OK, int QPT, int NA, bool STG, bool SMALL>
 __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, const uint64_t* s_thr,
                                           const LTabs& tb, char* stg, int K, const int32_t* __restrict__ act,
                                           void* __restrict__ obs, float* __restrict__ rew,
@@ -1644,6 +1646,7 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
   const size_t ow = (size_t)p.obs_width * ((OK == GP_OBS_HANSEN_VEC || OK == GP_OBS_WINDOW) ? 1 : 4);
   const PcgJump jB_unused{0, 1, 0, 0};
   constexpr bool TRIMS = GP_TRIMS;
+  const int TILE = SMALL ? p.ftile : FEPB;  // envs per tile (compile-time 2048 unless SMALL)
   uint32_t ae[QPT][4];
   int gl[QPT][4];
   int32_t a_cur[QPT][4];  // TRIMS: threshold-row byte offsets (action_row) instead of raw actions
@@ -1657,7 +1660,7 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
 #pragma unroll
   for (int q = 0; q < QPT; ++q) {
     const int tau = q * G + (int)blockIdx.x;
-    const int env0 = tau * FEPB + tid * EPT;
+    const int env0 = tau * TILE + tid * EPT;
     pfm[q] = 0;
     load4f<uint32_t>(p.ae, env0, B, ae[q]);
     if (rgoal) {
@@ -1690,7 +1693,7 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
 #pragma unroll
   for (int q = 0; q < QPT; ++q) {
     const int tau = q * G + (int)blockIdx.x;
-    const int env0 = tau * FEPB + tid * EPT;
+    const int env0 = tau * TILE + tid * EPT;
     if constexpr (TRIMS) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) a_cur[q][i] = action_row<NA>(a_cur[q][i], &p.ctl->err);
@@ -1728,7 +1731,7 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
 #pragma unroll
       for (int q = 0; q < QPT; ++q)
       {
-        const int e0 = (q * G + (int)blockIdx.x) * FEPB + tid * EPT;
+        const int e0 = (q * G + (int)blockIdx.x) * TILE + tid * EPT;
         if constexpr (STG) {  // complete tiles: one unconditional 16-B load
           const int4 v = *reinterpret_cast<const int4*>(act + (size_t)(k + 1) * B + e0);
           a_nxt[q][0] = v.x; a_nxt[q][1] = v.y; a_nxt[q][2] = v.z; a_nxt[q][3] = v.w;
@@ -1749,7 +1752,7 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
     for (int o = 0; o < QPT * 4; ++o) {
       // GP_ILV: slot-major (q fastest) so that the tiles' dependent draw chains interleave
       const int q = GP_ILV ? o % QPT : o / 4, i = GP_ILV ? o / QPT : o % 4;
-      const int env0 = (q * G + (int)blockIdx.x) * FEPB + tid * EPT;
+      const int env0 = (q * G + (int)blockIdx.x) * TILE + tid * EPT;
       {
         u128& s = sd[q];
         if (i) s = pcg_step(s, incv);
@@ -1896,7 +1899,7 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
 #ifdef GP_STAMPS
         if (p.xmode & 4) break;  // diagnostic: no output stores
 #endif
-        const int env0 = (q * G + (int)blockIdx.x) * FEPB + tid * EPT;
+        const int env0 = (q * G + (int)blockIdx.x) * TILE + tid * EPT;
         uint8_t tm[4], tr[4];
         int ag[4];
         float rw[4];
@@ -1916,7 +1919,7 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
       }
     }
     STAMP(12);
-    if (!STG && k > 0) flush_reset_obs<OK, QPT>(p, tb, (uint8_t*)obs + (off ? off - B : 0) * ow, tid, pc, pfm);
+    if (!STG && k > 0) flush_reset_obs<OK, QPT, SMALL>(p, tb, (uint8_t*)obs + (off ? off - B : 0) * ow, tid, pc, pfm);
     {
       const PcgJump jB{sh.jB[0], sh.jB[1], sh.jB[2], sh.jB[3]};
 #pragma unroll
@@ -1953,7 +1956,7 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
     }
     STAMP(5);
   }
-  if (!STG && K > 0) flush_reset_obs<OK, QPT>(p, tb, (uint8_t*)obs + (size_t)(K - 1) * B * ow, tid, pc, pfm);
+  if (!STG && K > 0) flush_reset_obs<OK, QPT, SMALL>(p, tb, (uint8_t*)obs + (size_t)(K - 1) * B * ow, tid, pc, pfm);
   if constexpr (GP_ACC) {
     uint32_t nv = 0;
 #pragma unroll
@@ -1970,7 +1973,7 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
   }
 #pragma unroll
   for (int q = 0; q < QPT; ++q) {
-    const int env0 = (q * G + (int)blockIdx.x) * FEPB + tid * EPT;
+    const int env0 = (q * G + (int)blockIdx.x) * TILE + tid * EPT;
     store4f<uint32_t>(p.ae, env0, B, ae[q]);
     if (rgoal) {
       uint16_t gg[4];
@@ -1983,7 +1986,7 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
 
 // The control wave of the fused kernel: speculative rejection checks, the granule exchange, the
 // next PCG64 state; publishes the RNG state at the end (block 0).
-template <int OK, int QPT, bool STG>
+template <int OK, int QPT, bool STG, bool SMALL>
 __device__ __forceinline__ void fused_ctrl(const GridDev& p_in, FusedShared& sh, const LTabs& tb, char* stg, int K) {
   constexpr int NC = (QPT + 1) / 2;  // checker states per lane (32 lanes per tile)
   const GridDev& p = p_in;
@@ -2142,7 +2145,7 @@ __device__ __forceinline__ void fused_ctrl(const GridDev& p_in, FusedShared& sh,
     if (lane < QPT) sh.tpre[lane] = mypre;
     wave_lds_sync();
     if (STG && ncalls) {  // the env waves' resetter lists (written right after B1: normally long done)
-      const uint32_t want = (uint32_t)FENVW * (uint32_t)(k + 1);
+      const uint32_t want = (uint32_t)(SMALL ? p.faw : FENVW) * (uint32_t)(k + 1);  // env waves that own envs
       while (__hip_atomic_load(&sh.rdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want)
         __builtin_amdgcn_s_sleep(1);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
@@ -2200,35 +2203,41 @@ __device__ __forceinline__ void out_store16(u32x4* d, u32x4 v) {
 }
 // Copy one staged output plane of tile tau (n32 = 32-bit words per env) to HBM: 16-B chunks of
 // 4 (n32 = 1) or 16 (n32 = 0: byte planes) envs when the destination is 16-B aligned, else 4-B words.
-__device__ __forceinline__ void stage_plane(const char* src, char* dst, int env_base, int B, int esz, int sl,
+template <int TILE>
+__device__ __forceinline__ void stage_plane_whole(const char* src, char* dst, int env_base, int esz, int sl, bool nt) {
+  // whole aligned tile (the common case): straight-line 16-B copies, immediate offsets; lane sl takes chunks
+  // sl, sl + NL, ... of the plane's TILE / 4 (4-byte elements) or TILE / 16 (bytes) chunks
+  constexpr int NL = FSTW * 64, N4 = TILE / 4, N1 = TILE / 16;
+  const u32x4* s4 = reinterpret_cast<const u32x4*>(src) + sl;
+  u32x4* d4 = reinterpret_cast<u32x4*>(dst + (size_t)env_base * esz) + sl;
+  if (esz == 4) {
+#pragma unroll
+    for (int j = 0; j < (N4 + NL - 1) / NL; ++j) {
+      if (N4 % NL != 0 && sl + j * NL >= N4) break;
+      if (nt) out_store16(d4 + j * NL, s4[j * NL]);
+      else d4[j * NL] = s4[j * NL];
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < (N1 + NL - 1) / NL; ++j) {
+      if (N1 % NL != 0 && sl + j * NL >= N1) break;
+      if (nt) out_store16(d4 + j * NL, s4[j * NL]);
+      else d4[j * NL] = s4[j * NL];
+    }
+  }
+}
+__device__ __forceinline__ void stage_plane(const char* src, char* dst, int env_base, int tile, int B, int esz, int sl,
                                             bool nt) {
   constexpr int NL = FSTW * 64;
-  if (env_base + FEPB <= B && (((uintptr_t)dst + (size_t)env_base * esz) & 15) == 0) {
-    // whole aligned tile (the common case): straight-line 16-B copies, immediate offsets
-    const u32x4* s4 = reinterpret_cast<const u32x4*>(src) + sl;
-    u32x4* d4 = reinterpret_cast<u32x4*>(dst + (size_t)env_base * esz) + sl;
-    // chunks of this plane: FEPB / 4 (4-byte elements) or FEPB / 16 (bytes); lane sl takes sl, sl + NL, ...
-    constexpr int N4 = FEPB / 4, N1 = FEPB / 16;
-    if (esz == 4) {
-#pragma unroll
-      for (int j = 0; j < (N4 + NL - 1) / NL; ++j) {
-        if (N4 % NL != 0 && sl + j * NL >= N4) break;
-        if (nt) out_store16(d4 + j * NL, s4[j * NL]);
-        else d4[j * NL] = s4[j * NL];
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < (N1 + NL - 1) / NL; ++j) {
-        if (N1 % NL != 0 && sl + j * NL >= N1) break;
-        if (nt) out_store16(d4 + j * NL, s4[j * NL]);
-        else d4[j * NL] = s4[j * NL];
-      }
-    }
+  if (env_base + tile <= B && (((uintptr_t)dst + (size_t)env_base * esz) & 15) == 0) {
+    if (tile == FEPB) stage_plane_whole<FEPB>(src, dst, env_base, esz, sl, nt);
+    else if (tile == FEPB / 2) stage_plane_whole<FEPB / 2>(src, dst, env_base, esz, sl, nt);
+    else stage_plane_whole<FEPB / 4>(src, dst, env_base, esz, sl, nt);
     return;
   }
   const bool a16 = (((uintptr_t)dst + (size_t)env_base * esz) & 15) == 0;  // wave-uniform
   const int epc = a16 ? 16 / esz : 4 / esz;                                   // envs per chunk
-  for (int c = sl; c < FEPB / epc; c += NL) {
+  for (int c = sl; c < tile / epc; c += NL) {
     const int e = env_base + c * epc;
     if (e + epc <= B) {
       if (a16 && nt)
@@ -2244,11 +2253,40 @@ __device__ __forceinline__ void stage_plane(const char* src, char* dst, int env_
   }
 }
 
+// Env waves beyond p.faw when the tiles are smaller than FEPB (strong-scaling shard sizes: 512 / 1024-env tiles
+// so that every CU gets a tile): they help stage the tables, post zero reset counts once and then only take part
+// in the block barriers (fused_resets role R_PASS), like the store waves minus the copies.
+template <int OK, int QPT>
+__device__ __forceinline__ void fused_idle(const GridDev& p, FusedShared& sh, const LTabs& tb, int K) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int G = (int)gridDim.x;
+  const uint32_t step_base = p.ctl->step;
+  const Stream st{};
+  const PcgJump jB{0, 1, 0, 0};
+  uint32_t du[QPT][4], dp[QPT] = {};
+  int di[QPT][4];
+  const uint32_t dc[QPT] = {};
+  if (lane == 0)
+#pragma unroll
+    for (int q = 0; q < QPT; ++q) sh.wcnt[q][wid] = 0;
+  if constexpr (GP_PRO2) {
+    lds_image_copy_range(const_cast<char*>(tb.dyn), p.limg, 0, p.lds.jt.off, tid, FENVW * 64);
+    __syncthreads();
+  }
+  for (int k = 0; k < K; ++k) {
+    const uint32_t tag0 = (step_base + (uint32_t)k + 1u) * 4u;
+    uint64_t* slots = p.fslot + (size_t)((step_base + (uint32_t)k) & 1u) * 3 * G;
+    lds_barrier();  // B1
+    lds_barrier();  // B2
+    fused_resets<OK, QPT, R_PASS>(p, sh, tb, st, (u128)0, jB, slots, tag0, du, di, dc, dc, du, dp);
+  }
+}
+
 // The store waves of the fused kernel. They take part in every block barrier (fused_resets role
 // R_PASS) and, with STG, move step k's staged outputs from LDS to HBM right after step k's resets,
 // i.e. while the env waves advance and run step k+1's VALU-bound transitions, so that the outputs'
 // HBM write burst does not overlap the next exchange (whose polling loads it would slow down).
-template <int OK, int QPT, bool STG>
+template <int OK, int QPT, bool STG, bool SMALL>
 __device__ __forceinline__ void fused_store(const GridDev& p, FusedShared& sh, const LTabs& tb, const char* stg, int K,
                                             void* __restrict__ obs, float* __restrict__ rew,
                                             uint8_t* __restrict__ term, uint8_t* __restrict__ trunc) {
@@ -2284,16 +2322,18 @@ __device__ __forceinline__ void fused_store(const GridDev& p, FusedShared& sh, c
         const int tau = q * G + (int)blockIdx.x;
         if (tau >= p.fnt) continue;
         const char* t = stg + q * STG_TILE_BYTES;
-        stage_plane(t + FEPB * 4, (char*)(rew + off), tau * FEPB, B, 4, sl, nt);
-        stage_plane(t + FEPB * 8, (char*)(term + off), tau * FEPB, B, 1, sl, nt);
-        stage_plane(t + FEPB * 9, (char*)(trunc + off), tau * FEPB, B, 1, sl, nt);
+        const int tile = SMALL ? p.ftile : FEPB;
+        stage_plane(t + FEPB * 4, (char*)(rew + off), tau * tile, tile, B, 4, sl, nt);
+        stage_plane(t + FEPB * 8, (char*)(term + off), tau * tile, tile, B, 1, sl, nt);
+        stage_plane(t + FEPB * 9, (char*)(trunc + off), tau * tile, tile, B, 1, sl, nt);
       }
       // the obs: the resetters' final obs were written by the control wave before the last barrier
 #pragma unroll
       for (int q = 0; q < QPT; ++q) {
         const int tau = q * G + (int)blockIdx.x;
         if (tau >= p.fnt) continue;
-        stage_plane(stg + q * STG_TILE_BYTES, (char*)obs + off * 4, tau * FEPB, B, 4, sl, nt);
+        const int tile = SMALL ? p.ftile : FEPB;
+        stage_plane(stg + q * STG_TILE_BYTES, (char*)obs + off * 4, tau * tile, tile, B, 4, sl, nt);
       }
     }
   }
@@ -2302,7 +2342,7 @@ __device__ __forceinline__ void fused_store(const GridDev& p, FusedShared& sh, c
 // The parameters come by value. (Passed as a pointer to the device copy GridDev::self instead, the launch
 // read no host-resident kernel arguments, but the step loop re-loaded fields through the scalar cache and ran
 // ≈10% slower per step: measured in one call, 5.90 vs 5.33 µs/step.)
-template <int OK, int QPT, int NA, bool STG>
+template <int OK, int QPT, int NA, bool STG, bool SMALL>
 __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, const int32_t* __restrict__ act,
                                                            void* __restrict__ obs, float* __restrict__ rew,
                                                            uint8_t* __restrict__ term, uint8_t* __restrict__ trunc) {
@@ -2330,14 +2370,16 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
   uint32_t eps = 0, lens = 0, nst = 0;
   if (wid == FENVW) {
     __builtin_amdgcn_s_setprio(3);  // the exchange is on every step's critical path
-    fused_ctrl<OK, QPT, STG>(p, sh, tb, stg, K);
+    fused_ctrl<OK, QPT, STG, SMALL>(p, sh, tb, stg, K);
+  } else if (SMALL && wid < FENVW && wid >= p.faw) {
+    fused_idle<OK, QPT>(p, sh, tb, K);
   } else if (wid > FENVW) {
     // above the env waves: the store waves issue their few copy instructions right after B2 instead of
     // trailing the VALU-bound transitions on their SIMD (+6% measured vs priority 0; 2 was no better)
     __builtin_amdgcn_s_setprio(GP_STORE_PRIO);
-    fused_store<OK, QPT, STG>(p, sh, tb, stg, K, obs, rew, term, trunc);
+    fused_store<OK, QPT, STG, SMALL>(p, sh, tb, stg, K, obs, rew, term, trunc);
   } else {
-    fused_env<OK, QPT, NA, STG>(p, sh, s_thr, tb, stg, K, act, obs, rew, term, trunc, rsum, eps, lens, nst);
+    fused_env<OK, QPT, NA, STG, SMALL>(p, sh, s_thr, tb, stg, K, act, obs, rew, term, trunc, rsum, eps, lens, nst);
   }
   LSTAMP(2);
   // metrics (the control wave contributes zeros)
@@ -2557,7 +2599,7 @@ struct GridBackend : EnvBackend {
     if (!strcmp(key, "fused_blocks")) *v = fused_G;
     else if (!strcmp(key, "fused_tiles_per_block")) *v = fused_qpt;
     else if (!strcmp(key, "fused_staged")) *v = fused_stg ? 1 : 0;
-    else if (!strcmp(key, "fused_tile_envs")) *v = FEPB;
+    else if (!strcmp(key, "fused_tile_envs")) *v = d.ftile;
     else return EnvBackend::query(key, v);
     return GP_OK;
   }
@@ -2604,11 +2646,23 @@ struct GridBackend : EnvBackend {
   template <int OK, int QPT, bool STG>
   void launch_fused_qs(int K, const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc, hipStream_t s) {
     const size_t lds = (size_t)d.lds.total + (STG ? (size_t)QPT * STG_TILE_BYTES : 0);
+    // SMALL: tiles of 512 / 1024 envs (runtime size, idle env waves); only with <= 2 tiles per block
+    if constexpr (QPT <= 2) {
+      if (d.ftile != FEPB) {
+        if (d.nact == 4)
+          hipLaunchKernelGGL((grid_rollout_numpy<OK, QPT, 4, STG, true>), dim3(fused_G), dim3(FTPB), lds, s, d, K,
+                             (const int32_t*)act, obs, rew, term, trunc);
+        else
+          hipLaunchKernelGGL((grid_rollout_numpy<OK, QPT, 8, STG, true>), dim3(fused_G), dim3(FTPB), lds, s, d, K,
+                             (const int32_t*)act, obs, rew, term, trunc);
+        return;
+      }
+    }
     if (d.nact == 4)
-      hipLaunchKernelGGL((grid_rollout_numpy<OK, QPT, 4, STG>), dim3(fused_G), dim3(FTPB), lds, s, d, K,
+      hipLaunchKernelGGL((grid_rollout_numpy<OK, QPT, 4, STG, false>), dim3(fused_G), dim3(FTPB), lds, s, d, K,
                          (const int32_t*)act, obs, rew, term, trunc);
     else
-      hipLaunchKernelGGL((grid_rollout_numpy<OK, QPT, 8, STG>), dim3(fused_G), dim3(FTPB), lds, s, d, K,
+      hipLaunchKernelGGL((grid_rollout_numpy<OK, QPT, 8, STG, false>), dim3(fused_G), dim3(FTPB), lds, s, d, K,
                          (const int32_t*)act, obs, rew, term, trunc);
   }
   template <int OK, int QPT>
@@ -2687,11 +2741,11 @@ int GridBackend::upload_rng() {
   if (fused_G) {
     std::vector<PcgJump> fl(FTPB), ft(d.fnt);
     for (int t = 0; t < FTPB; ++t) fl[t] = pcg_jump_params((u128)(4 * t), rng.inc);
-    const PcgJump step_ftile = pcg_jump_params((u128)FEPB, rng.inc);
+    const PcgJump step_ftile = pcg_jump_params((u128)d.ftile, rng.inc);
     ft[0] = pcg_jump_params((u128)1, rng.inc);
     for (int k = 1; k < d.fnt; ++k) ft[k] = compose(step_ftile, ft[k - 1]);
     const PcgJump jb[2] = {pcg_jump_params((u128)B, rng.inc),                   // random(B)
-                           pcg_jump_params((u128)fused_G * FEPB, rng.inc)};  // tile stride of a block (q -> q + 1)
+                           pcg_jump_params((u128)fused_G * d.ftile, rng.inc)};  // tile stride of a block (q -> q + 1)
     GP_HIP_CHECK(hipMemcpy(b_flt4.p, fl.data(), fl.size() * sizeof(PcgJump), hipMemcpyHostToDevice));
     GP_HIP_CHECK(hipMemcpy(b_ftj.p, ft.data(), ft.size() * sizeof(PcgJump), hipMemcpyHostToDevice));
     GP_HIP_CHECK(hipMemcpy(b_fjB.p, jb, sizeof(jb), hipMemcpyHostToDevice));
@@ -3158,8 +3212,23 @@ int GridBackend::build(const gp_grid_config* cfg) {
     d.lds.total = off <= LDS_TABLE_BUDGET ? off : 0;
   }
   // fused numpy rollout: one 512-thread block per CU, <= 4 tiles of 2048 envs per block
-  d.fnt = (int)((B + FEPB - 1) / FEPB);
   const GpDebugKnobs& dbg = gp_debug_knobs();  // diagnostic knobs (gp_debug_set); defaults in production
+  {
+    // fused tile size: 2048 envs (8 env waves) unless that leaves CUs without a tile (strong-scaling shard sizes:
+    // 2^17 envs are 64 tiles of 2048 but 256 of 512), halved down to 512 (2 env waves) until every CU has one
+    hipDeviceProp_t prop;
+    GP_HIP_CHECK(hipGetDeviceProperties(&prop, device));
+    const int cus = std::min(prop.multiProcessorCount, FMAXG);
+    int tile = FEPB;
+    if (dbg.fused_tile == 512 || dbg.fused_tile == 1024 || dbg.fused_tile == 2048) {
+      tile = dbg.fused_tile;
+    } else {
+      while (tile > 512 && (B + tile - 1) / tile < cus) tile /= 2;
+    }
+    d.ftile = tile;
+    d.faw = tile / (64 * EPT);
+  }
+  d.fnt = (int)((B + d.ftile - 1) / d.ftile);
   // exchange variant: bits 0-1: 1 = every block all-gathers the granules (default), 0 = block-0 aggregator;
   // bit 4: plain (not non-temporal) staged output stores; bits 2-3 (stamps builds only): output diagnostics
   d.xmode = dbg.xmode;
@@ -3169,21 +3238,22 @@ int GridBackend::build(const gp_grid_config* cfg) {
     hipDeviceProp_t prop;
     GP_HIP_CHECK(hipGetDeviceProperties(&prop, device));
     int occ = 0;
-    GP_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, grid_rollout_numpy<GP_OBS_WINDOW, 4, 8, false>,
+    GP_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, grid_rollout_numpy<GP_OBS_WINDOW, 4, 8, false, false>,
                                                              FTPB, d.lds.total));
     const int G = std::min({prop.multiProcessorCount, FMAXG, d.fnt});
     const int qpt = (d.fnt + G - 1) / G;
-    if (occ >= 1 && d.fnt <= FMAXT && qpt <= 4 && d.lds.total > 0 && !dbg.disable_fused) {
+    // (tiles smaller than FEPB only come with <= 2 tiles per block: the kernels for them exist for QPT <= 2)
+    if (occ >= 1 && d.fnt <= FMAXT && qpt <= (d.ftile == FEPB ? 4 : 2) && d.lds.total > 0 && !dbg.disable_fused) {
       fused_G = G;
       fused_qpt = qpt <= 1 ? 1 : (qpt <= 2 ? 2 : 4);
       const int k = cfg->obs_kind;
       // staged outputs: <= 2 tiles per block, scalar obs, and only complete tiles (every block owns exactly
-      // fused_qpt full 2048-env tiles: the staged kernel drops the per-env bounds checks)
+      // fused_qpt full tiles: the staged kernel drops the per-env bounds checks)
       if (fused_qpt <= 2 && (k == GP_OBS_HANSEN || k == GP_OBS_TABLE) && !dbg.no_staging &&
-          (int64_t)B == (int64_t)fused_qpt * G * FEPB) {
+          (int64_t)B == (int64_t)fused_qpt * G * d.ftile) {
         int occ2 = 0;
         GP_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &occ2, grid_rollout_numpy<GP_OBS_HANSEN, 2, 8, true>, FTPB, d.lds.total + 2 * STG_TILE_BYTES));
+            &occ2, grid_rollout_numpy<GP_OBS_HANSEN, 2, 8, true, false>, FTPB, d.lds.total + 2 * STG_TILE_BYTES));
         fused_stg = occ2 >= 1;
       }
     }

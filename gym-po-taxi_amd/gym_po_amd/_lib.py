@@ -78,6 +78,9 @@ SIGNATURES = {
     "gp_reset": (ctypes.c_int, [_vp, _vp, _vp]),
     "gp_step": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gp_rollout": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "gp_plan_create": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.POINTER(_vp)]),
+    "gp_plan_run": (ctypes.c_int, [_vp]),
+    "gp_plan_destroy": (None, [_vp]),
     "gp_get_state": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
     "gp_set_state": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
     "gp_set_replay": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),

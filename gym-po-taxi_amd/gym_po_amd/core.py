@@ -21,6 +21,20 @@ def _torch():
     return torch
 
 
+class _PlanKeep:
+    """Owns a gp_plan (freed with the run closure) and keeps its buffers alive."""
+
+    def __init__(self, plan, bufs):
+        self.plan, self.bufs = plan, bufs
+
+    def __del__(self):
+        try:
+            if self.plan is not None:
+                lib().gp_plan_destroy(self.plan)
+        except Exception:  # noqa: BLE001
+            pass
+
+
 class NativeVecEnv:
     """Base class: one C-ABI handle, one device, one stream (the torch current stream)."""
     is_vector_env = True
@@ -229,16 +243,25 @@ class NativeVecEnv:
             out = self._alloc_outputs(K)
         else:
             self._check_out(out, K)
-        fn, h = lib().gp_rollout, self._handle
+        L, h = lib(), self._handle
         args = [ctypes.c_void_p(x.data_ptr()) for x in (a,) + tuple(out)]
         stream0 = torch.cuda.current_stream(self.device).cuda_stream
-        keep = (a, out)
+        fn = L.gp_rollout
+        if hasattr(L, "gp_plan_create"):
+            plan = ctypes.c_void_p()
+            check(L.gp_plan_create(h, K, *args, stream0, ctypes.byref(plan)), "gp_plan_create")
+            keep = _PlanKeep(plan, (a, out))
+            fn_plan = L.gp_plan_run
+        else:  # an older library chosen through GYM_PO_AMD_LIB (in-call A/B tooling)
+            keep = _PlanKeep(None, (a, out))
+            fn_plan = lambda _p: fn(h, K, *args, stream0)  # noqa: E731
 
         def run(stream=None):
-            rc = fn(h, K, *args, stream0 if stream is None else stream)
+            # the bound plan: one pointer across ctypes (another stream: the plain call with its arguments)
+            rc = fn_plan(keep.plan) if stream is None else fn(h, K, *args, stream)
             if rc:
                 check(rc, "gp_rollout")
-            return keep
+            return keep.bufs
         return run, (out[0], out[1], out[2].view(torch.bool), out[3].view(torch.bool))
 
     def check(self):

@@ -181,6 +181,14 @@ int gp_step(gp_env* env, const void* actions, void* obs, float* rew, uint8_t* te
  * steps in one launch with the state in registers; other cases issue K step launches. */
 int gp_rollout(gp_env* env, int K, const void* actions, void* obs, float* rew, uint8_t* term, uint8_t* trunc,
                void* stream);
+/* A prepared gp_rollout (the agent loop's allocation-free hot path, bench.py's timed call): the arguments are
+ * validated and bound once; gp_plan_run(plan) enqueues the K steps with nothing to marshal per call (one
+ * pointer across the FFI instead of eight). The buffers must outlive the plan; gp_plan_destroy frees it. */
+typedef struct gp_plan gp_plan;
+int gp_plan_create(gp_env* env, int K, const void* actions, void* obs, float* rew, uint8_t* term, uint8_t* trunc,
+                   void* stream, gp_plan** out);
+int gp_plan_run(gp_plan* plan);
+void gp_plan_destroy(gp_plan* plan);
 
 /* Canonical state (device pointers, int32 unless noted). GRID: agent cell, goal cell, elapsed
  * [B] each. TAXI: s, elapsed, n_dropoffs. CROOMS: agent yx f64[B,2], goal cell yx i32[B,2],
@@ -256,7 +264,8 @@ int gp_profile_read_resolver(gp_env* env, double* total_ms, int64_t* n_launches)
  *   "disable_fused" (GRID numpy mode: 1 = the two-kernel path only), "no_staging" (1 = the fused kernel's
  *   env waves store outputs directly), "xmode" (fused exchange variant, default 1), "spin_limit" (polls
  *   before a cross-block wait gives up, 0 = default), "fault_block" (this block never publishes: forces
- *   the timeout path; -1 = off). gp_debug_reset restores the defaults. Unknown key: GP_E_INVALID. */
+ *   the timeout path; -1 = off), "fused_tile" (GRID fused kernel envs per tile: 512, 1024 or 2048; 0 = by
+ *   size). gp_debug_reset restores the defaults. Unknown key: GP_E_INVALID. */
 int gp_debug_set(const char* key, int64_t value);
 void gp_debug_reset(void);
 

@@ -99,14 +99,21 @@ def test_bench_kernel_random_goal_staged_k_steps(gpu_device):
     _check_chunks(env, ora, (24, 40), action_seed=5, n_act=8)
 
 
-@pytest.mark.parametrize("B", [1 << 17, 1 << 18])
-def test_strong_scaling_shard_sizes_staged_bit_exact(B, gpu_device):
-    """The per-GPU shard of a strong-scaling run (1M envs over 8 / 4 GPUs): 2^17 / 2^18 envs take the same
-    staged kernel with one 2048-env tile per block (64 / 128 blocks), K = 20 then 128 steps per launch."""
+@pytest.mark.parametrize("B,force_tile", [(1 << 17, 0), (1 << 18, 0), (1 << 17, 2048), (1 << 18, 512),
+                                          (3 << 17, 0)])
+def test_strong_scaling_shard_sizes_staged_bit_exact(B, force_tile, gpu_device):
+    """The per-GPU shard of a strong-scaling run (1M envs over 8 / 4 GPUs): 2^17 / 2^18 envs get tiles of 512 /
+    1024 envs (2 / 4 env waves per block) so that every CU has one; also forced to 2048-env tiles (64 blocks of
+    8 env waves) and 512-env tiles (two tiles per block), and 3 * 2^17 (1024-env tiles, 1.5 per CU). K = 20
+    then 128 steps per launch, bit-exact."""
     from gym_po_amd import MultistoryFourRoomsEnv
-    env = MultistoryFourRoomsEnv(B, grid_z=1, obs_type="hansen", device=gpu_device)
+    from gym_po_amd._lib import debug_knobs
+    with debug_knobs(fused_tile=force_tile):
+        env = MultistoryFourRoomsEnv(B, grid_z=1, obs_type="hansen", device=gpu_device)
     G, q, stg, tile = _staged_geometry(env)
-    assert G * q * tile == B and stg, (G, q, stg, tile)
+    assert G * (q - 1) * tile < B <= G * q * tile, (G, q, stg, tile)
+    assert tile == (force_tile or {1 << 17: 512, 1 << 18: 1024, 3 << 17: 1024}[B])
+    assert bool(stg) == (B == G * q * tile), (G, q, stg, tile)  # staged iff the tiles are complete
     ora = gridworld.FourRoomsOracle(B, 1, obs_type="hansen")
     o_g = _reset_obs(env, 31)
     np.testing.assert_array_equal(o_g.astype(np.int64), np.asarray(ora.reset_seed(31)).astype(np.int64))

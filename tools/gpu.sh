@@ -48,7 +48,7 @@ case "$task" in
       i=$((i+1))
       run 300 $O/p$i.log rocprofv3 --pmc $C --output-format csv -d $O/p$i -o p -- python3 bench.py --no-cpu-baseline "$@"
     done
-    python3 tools/pmc_to_json.py $O ${PMC_KERNEL:-grid_rollout_numpy} ${PMC_CFG:-fourrooms_hansen4_B1048576_numpy} $O/pmc.json ${PMC_WORKLOAD:-fourrooms}
+    python3 tools/pmc_to_json.py $O ${PMC_KERNEL:-grid_rollout_numpy} ${PMC_CFG:-fourrooms_hansen4_B1048576_numpy} $O/pmc.json ${PMC_WORKLOAD:-fourrooms} ${PMC_K:-20}
     cat $O/pmc.json ;;
   sq)
     i=0
