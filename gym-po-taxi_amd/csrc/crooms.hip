@@ -49,7 +49,6 @@ constexpr uint32_t TAG_DRAW = 0x6d733121u;
 #endif
 constexpr double MAX_VELOCITY = 5.0;
 // Largest batch of the exact (numpy-stream) mode, which runs in one workgroup.
-#define GP_CR_NUMPY_MAX_ENVS (1 << 20)        // crooms.py:170
 
 struct alignas(32) CrSlot {
   double return_sum;
@@ -423,12 +422,13 @@ struct StepOut {
 };
 
 // One env-step of CRoomsEnv.step (crooms.py:276-331). DEFER: a terminated / truncated env is left for the
-// caller to reset (its reset draws are not known yet; the exact mode's stream walk).
+// caller to reset (its reset draws are not known yet; the exact mode's stream walk). wix (replay): the pair of
+// the wall-noise buffer this env reads when it hits a wall (default: its own, env).
 template <bool REPLAY, bool DEFER = false>
 __device__ __forceinline__ StepOut crooms_env_step(const CrDev& p, const uint8_t* lds, int env, bool live,
                                                    uint64_t step, double a0, double a1, int ad, double& ay,
                                                    double& ax, double& vy, double& vx, uint32_t& g, int32_t& el,
-                                                   float& rsum, uint32_t& eps, uint32_t& lens) {
+                                                   float& rsum, uint32_t& eps, uint32_t& lens, int wix = -1) {
   StepOut o;
   el += 1;
   Draws d;
@@ -490,7 +490,7 @@ __device__ __forceinline__ StepOut crooms_env_step(const CrDev& p, const uint8_t
     const double cy = floor(per_cell(p, ay)) * p.cell + p.half_cell;
     const double cx = floor(per_cell(p, ax)) * p.cell + p.half_cell;
     double wy = 0.0, wx = 0.0;
-    if (live) draw_normals<REPLAY>(p, env, step, 1, 0.5, wy, wx, nblk, nhave);
+    if (live) draw_normals<REPLAY>(p, REPLAY && wix >= 0 ? wix : env, step, 1, 0.5, wy, wx, nblk, nhave);
     ay = fmin(fmax(cy + wy, cy - p.half_cell), (cy + p.half_cell) - 1e-8);
     ax = fmin(fmax(cx + wx, cx - p.half_cell), (cx + p.half_cell) - 1e-8);
     vy = 0.0;
@@ -1153,6 +1153,654 @@ __global__ __launch_bounds__(XT) void crooms_numpy_rollout(CrDev p, CrExact x, i
   }
 }
 
+// ---- exact (numpy-stream) mode, multi-workgroup (B > XG_MIN_ENVS) ----
+// The same stream, call for call, resolved over ALL positions of a draw call at once instead of window by window:
+// each draw call is a short sequence of grid-wide kernels on the stream (no workgroup walks the stream), with
+// the call's stream state in one of two slots (read slot rd, written slot wr = the state after the call).
+//   normal(n): position q holds word q (= output of jump(S, q + 1)). A position is "slow" when its word misses
+//     the ziggurat fast path (~1.2%); the attempt it would start uses span(q) words (wedge 2, tail 1 + 2k) and
+//     may be rejected (a wedge: the chain continues at q + 2). The chain of attempts from position 0 visits
+//     every position except the extra words of the on-chain slow attempts, so a position's fate only depends
+//     on the slow attempts just before it: each block evaluates the attempts of its positions and of a halo of
+//     XG_LOOK positions before them in LDS, walks every slow position back to the start of its cluster (the
+//     first slow attempt not spanned by an earlier one; clusters are almost always that one attempt) and
+//     forward through it (list ranking by clusters, no serial walk over the call), and counts its produced
+//     positions (on-chain and accepted). The next kernel gives every normal its index from those counts (a
+//     reduce-then-scan over the call: no block waits on another), and the n-th normal's end is the words used.
+//   choice(n): candidates are the buffered half (if any), then lo / hi of each word; a candidate is drawn
+//     unless Lemire rejects it (~n / 2^32): counted per block, then indexed the same way; the last draw fixes
+//     has_uint32 / uinteger.
+//   env phases (dry step -> wall hits, real step -> resets, applying the resets) are per-env kernels that
+//     publish a bitmap of their flagged envs and per-block counts; a later phase finds a flagged env's rank
+//     (its index into the draws of the call that serves it: the wall noise, the reset choices) from them.
+// Counts: every producer block stores its count, and adds (1 << 40 | count) to its group's (64 blocks)
+// accumulator; the group's last arriver writes the group sum and clears the accumulator for the next launch.
+// A consumer's prefix for block b is the sum of the group sums before b's group and of the counts of the blocks
+// before b in it (at most 256 + 63 loads per block, all independent).
+constexpr int XGT = 256;          // threads (positions / envs) per block of the grid kernels
+constexpr int XGW = XGT / 64;     // waves (bitmap words) per block
+constexpr int XG_LOOK = 64;       // the halo of a normal call's block view (one wave)
+constexpr int XG_SPAN = 32;       // longest slow attempt (a 15-pair tail; else GP_DERR_STREAM)
+constexpr int XG_MIN_ENVS = 4096; // at or below: the one-workgroup kernel (fewer launches per step)
+
+struct XgCounts {                 // per-block counts of one producer launch
+  uint32_t* bc;                   // [blocks] block counts
+  unsigned long long* acc;        // [groups] arrivals << 40 | count sum (zero between launches)
+  uint32_t* gs;                   // [groups] group sums (64 blocks per group)
+};
+
+struct XgFlags {                  // the flagged envs of one env phase
+  uint64_t* bits;                 // [blocks * XGW] bitmap (nullptr: every env, ranked by env index)
+  XgCounts c;
+};
+
+struct XgCall {                   // one draw call over stream positions
+  const PcgJump* jt;              // radix-64 jump tables (JT_LEVELS x 64)
+  const PcgJump* wj;              // wj[j]: j LCG steps (j <= XGT)
+  CrRng* st;                      // stream-state slots [2]
+  int rd, wr;
+  XgCounts nsrc;                  // n = nmul * (flagged envs of a phase) when nsrc.gs is set, else n_host
+  int nsrc_blocks;
+  int nmul;
+  int64_t n_host;
+  int P;                          // capacity in positions
+  uint64_t* bits;                 // normal: slow-position bitmap [P / 64]
+  uint64_t* pbits;                // normal: produced-position bitmap [P / 64]
+  uint64_t* bstate;               // [P / XGT][2] the call's state jumped to each block's first position
+  uint16_t* span;                 // per slow position: words of its attempt
+  double* val;                    // per slow position: the attempt's normal
+  XgCounts pc;                    // per-block counts of produced normals / drawn choices
+  double scale;                   // normal: dst[r] = loc 0 + scale * z (r: the normal's index in the call)
+  double* dst;
+  int32_t* idst;                  // choice: idst[r]
+  uint32_t nv, lthr;              // choice: values, Lemire threshold
+  uint32_t* err;                  // device error word (GP_DERR_STREAM)
+};
+
+// Block-wide sum (every thread gets it). Uses its own LDS; safe to call repeatedly.
+__device__ __forceinline__ uint32_t xg_block_sum(uint32_t x) {
+  __shared__ uint32_t ws[XGW];
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = x;
+  __syncthreads();
+  uint32_t s = 0;
+#pragma unroll
+  for (int i = 0; i < XGW; ++i) s += ws[i];
+  __syncthreads();
+  return s;
+}
+// Block-wide exclusive scan of small per-thread counts: this thread's offset, the block total in tot.
+__device__ __forceinline__ uint32_t xg_block_scan(uint32_t c, uint32_t& tot) {
+  __shared__ uint32_t ws[XGW];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t x = c;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) ws[wv] = x;
+  __syncthreads();
+  uint32_t base = 0;
+  tot = 0;
+#pragma unroll
+  for (int i = 0; i < XGW; ++i) {
+    base += i < wv ? ws[i] : 0u;
+    tot += ws[i];
+  }
+  __syncthreads();
+  return base + x - c;
+}
+// Producer side (thread 0 of block bid of nblocks): the block's count, its group's sum when it arrives last.
+__device__ __forceinline__ void xg_publish(const XgCounts& c, int bid, int nblocks, uint32_t cnt) {
+  c.bc[bid] = cnt;
+  const int g = bid >> 6;
+  const unsigned long long old = atomicAdd(&c.acc[g], (1ull << 40) | (unsigned long long)cnt);
+  if ((int)(old >> 40) == min(64, nblocks - 64 * g) - 1) {
+    c.gs[g] = (uint32_t)(old & ((1ull << 40) - 1ull)) + cnt;
+    __hip_atomic_store(&c.acc[g], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+// Consumer side (block-cooperative): the counts of blocks [0, bid) of a finished producer launch.
+__device__ __forceinline__ uint32_t xg_prefix(const XgCounts& c, int bid) {
+  const int g = bid >> 6, t = threadIdx.x;
+  uint32_t x = 0;
+  for (int j = t; j < g; j += XGT) x += c.gs[j];
+  if (t < bid - 64 * g) x += c.bc[64 * g + t];
+  return xg_block_sum(x);
+}
+// Consumer side (block-cooperative): the total of a finished producer launch of nblocks blocks.
+__device__ __forceinline__ uint32_t xg_total(const XgCounts& c, int nblocks) {
+  uint32_t x = 0;
+  for (int j = threadIdx.x; j < (nblocks + 63) / 64; j += XGT) x += c.gs[j];
+  return xg_block_sum(x);
+}
+// This thread's bit in a block's XGW bitmap words and the set bits before it in the block.
+__device__ __forceinline__ bool xg_block_bit(const uint64_t* w, uint32_t& before) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint64_t mine = 0;
+  before = 0;
+#pragma unroll
+  for (int j = 0; j < XGW; ++j) {
+    const uint64_t x = w[j];
+    if (j < wv) before += (uint32_t)__builtin_popcountll(x);
+    if (j == wv) mine = x;
+  }
+  before += (uint32_t)__builtin_popcountll(mine & ((1ull << lane) - 1ull));
+  return (mine >> lane) & 1ull;
+}
+// Stores the block's flag ballots (every wave of the block reaches this) and publishes the block's count.
+__device__ __forceinline__ void xg_flag_block(const XgFlags& f, int bid, int nblocks, bool flag) {
+  const uint64_t m = __ballot(flag);
+  if ((threadIdx.x & 63) == 0) f.bits[bid * XGW + (threadIdx.x >> 6)] = m;
+  const uint32_t cnt = xg_block_sum((threadIdx.x & 63) == 0 ? (uint32_t)__builtin_popcountll(m) : 0u);
+  if (threadIdx.x == 0) xg_publish(f.c, bid, nblocks, cnt);
+}
+
+// n of a call (block-cooperative).
+__device__ __forceinline__ int64_t xg_n(const XgCall& a) {
+  return a.nsrc.gs ? (int64_t)a.nmul * (int64_t)xg_total(a.nsrc, a.nsrc_blocks) : a.n_host;
+}
+__device__ __forceinline__ u128 xg_inc(const CrRng& s) { return mk128(s.i_hi, s.i_lo); }
+// positions a normal call of n draws may need (words per normal: 1.012 on average; capped by the buffers)
+__device__ __forceinline__ int xg_norm_need(const XgCall& a, int64_t n) {
+  return (int)min((int64_t)a.P, n + n / 16 + 4096);
+}
+// words a choice call of n draws may need (two candidates per word; Lemire rejections ~n / 2^32)
+__device__ __forceinline__ int xg_cho_need(const XgCall& a, int64_t n) {
+  return (int)min((int64_t)a.P, n / 2 + n / 1024 + 256);
+}
+__device__ __forceinline__ void xg_put_state(CrRng* st, int wr, const CrRng& old, u128 s, uint32_t has, uint32_t u) {
+  CrRng n = old;
+  n.s_hi = hi64(s);
+  n.s_lo = lo64(s);
+  n.has_u32 = has;
+  n.uinteger = u;
+  st[wr] = n;
+}
+// The block's base state jump(S, q0) (thread 0, into LDS bb and, when bstate is set, into bstate[bid]).
+__device__ __forceinline__ u128 xg_base_state(const XgCall& a, const CrRng& s0, int q0, uint64_t* bstate) {
+  __shared__ uint64_t bb[2];
+  if (threadIdx.x == 0) {
+    const u128 b = pcg_jump(a.jt, mk128(s0.s_hi, s0.s_lo), (uint32_t)q0);
+    bb[0] = hi64(b);
+    bb[1] = lo64(b);
+    if (bstate) {
+      bstate[2 * blockIdx.x] = bb[0];
+      bstate[2 * blockIdx.x + 1] = bb[1];
+    }
+  }
+  __syncthreads();
+  return mk128(bb[0], bb[1]);
+}
+
+// One attempt of numpy's ziggurat starting at position q whose LCG state (before its word) is s:
+// 1 = a normal v in `used` words, 0 = a rejected wedge (2 words), -1 = longer than XG_SPAN words.
+__device__ int xg_attempt(const ZigTabs& t, u128 s, u128 inc, int& used, double& v) {
+  uint64_t r = pcg_output(s);
+  int pos = 1;
+  auto next = [&]() -> uint64_t {
+    s = pcg_step(s, inc);
+    ++pos;
+    return pcg_output(s);
+  };
+  const int idx = (int)(r & 0xff);
+  r >>= 8;
+  const uint64_t sign = r & 1u, rabs = (r >> 1) & 0x000fffffffffffffull;
+  double x = (double)rabs * t.wi[idx];
+  if (sign) x = -x;
+  if (rabs < t.ki[idx]) { used = 1; v = x; return 1; }
+  if (idx == 0) {
+    for (;;) {
+      if (pos + 2 > XG_SPAN) { used = pos; return -1; }
+      const double xx = -GP_ZIG_INV_R * zlog1p_neg(u53_of(next()));
+      const double yy = -zlog1p_neg(u53_of(next()));
+      if (yy + yy > xx * xx) {
+        used = pos;
+        v = ((rabs >> 8) & 1u) ? -(GP_ZIG_R + xx) : GP_ZIG_R + xx;
+        return 1;
+      }
+    }
+  }
+  used = 2;
+  v = x;
+  return ((t.fi[idx - 1] - t.fi[idx]) * u53_of(next()) + t.fi[idx] < zexp(-0.5 * x * x)) ? 1 : 0;
+}
+
+__device__ __forceinline__ ZigTabs xg_zig() {
+  return ZigTabs{d_zig, reinterpret_cast<const double*>(d_zig + 256), reinterpret_cast<const double*>(d_zig + 512)};
+}
+
+// A block's view of positions [q0 - XG_LOOK, q0 + XGT) (the halo: the slow attempts that can reach into the
+// block): slow bits, spans, flags (bit 0 on-chain, bit 1 accepted) in LDS. Index i = position - (q0 - XG_LOOK).
+constexpr int XGH = XG_LOOK + XGT;
+struct XgView {
+  uint64_t bits[XGH / 64];
+  uint16_t span[XGH];
+  uint8_t flag[XGH];
+};
+__device__ __forceinline__ bool xv_slow(const XgView& v, int i) { return (v.bits[i >> 6] >> (i & 63)) & 1ull; }
+// The slow positions of view indices [lo, hi) (hi - lo <= 128) as up to three bit words from (lo & ~63).
+__device__ __forceinline__ void xv_window(const XgView& v, int lo, int hi, uint64_t (&m)[3], int& base) {
+  base = lo & ~63;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const int b0 = base + 64 * k;
+    uint64_t w = (b0 < hi && b0 < XGH) ? v.bits[b0 >> 6] : 0ull;
+    if (b0 < lo) w &= ~0ull << (lo - b0);
+    if (b0 + 64 > hi) w &= (hi - b0) <= 0 ? 0ull : ((hi - b0) >= 64 ? ~0ull : ((1ull << (hi - b0)) - 1ull));
+    m[k] = w;
+  }
+}
+// Whether the slow attempt at view index i is on the chain: back to its cluster's start, then forward. -1: the
+// cluster may reach before the view (never when the view starts before position 0), for xg_on_chain_abs.
+__device__ __forceinline__ int xv_on_chain(const XgView& v, int i, bool at0) {
+  int c = i;
+  for (int hop = 0; hop < XGH; ++hop) {
+    if (c - XG_SPAN < 0 && !at0) return -1;
+    uint64_t m[3];
+    int base;
+    xv_window(v, max(0, c - XG_SPAN), c, m, base);
+    int best = -1;
+#pragma unroll
+    for (int k = 0; k < 3 && best < 0; ++k) {
+      uint64_t w = m[k];
+      while (w) {
+        const int p = base + 64 * k + __builtin_ctzll(w);
+        w &= w - 1;
+        if (p + (int)v.span[p] > c) { best = p; break; }
+      }
+    }
+    if (best < 0) break;
+    c = best;
+  }
+  int cur = c;
+  for (int p0 = c; p0 <= i; p0 += 128) {
+    uint64_t m[3];
+    int base;
+    xv_window(v, p0, min(i + 1, p0 + 128), m, base);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      uint64_t w = m[k];
+      while (w) {
+        const int p = base + 64 * k + __builtin_ctzll(w);
+        w &= w - 1;
+        if (p == i) return p >= cur ? 1 : 0;
+        if (p >= cur) cur = p + (int)v.span[p];
+      }
+    }
+  }
+  return 1;  // not reached: i is slow
+}
+// The same walk in stream positions for a cluster that reaches before the block's view (a chain of overlapping
+// slow attempts longer than the halo's spare XG_LOOK - XG_SPAN words: rare): positions outside the view are
+// evaluated on the spot (their own jump), inside it read from the view.
+__device__ __noinline__ int xg_on_chain_abs(const XgCall& a, const XgView& v, int q0, const CrRng& s0, int qi) {
+  const ZigTabs zt = xg_zig();
+  const u128 S = mk128(s0.s_hi, s0.s_lo), inc = xg_inc(s0);
+  auto slow_at = [&](int p, int& span) -> bool {
+    const int i = p - (q0 - XG_LOOK);
+    if (i >= 0 && i < XGH) {
+      if (!xv_slow(v, i)) return false;
+      span = v.span[i];
+      return true;
+    }
+    const u128 X = pcg_jump(a.jt, S, (uint32_t)p + 1u);
+    double z;
+    if (zig_fast(zt, pcg_output(X), z)) return false;
+    double vv;
+    if (xg_attempt(zt, X, inc, span, vv) < 0) atomicOr(a.err, GP_DERR_STREAM);
+    return true;
+  };
+  int c = qi;
+  for (;;) {
+    int best = -1;
+    for (int p = max(0, c - XG_SPAN); p < c && best < 0; ++p) {
+      int sp = 1;
+      if (slow_at(p, sp) && p + sp > c) best = p;
+    }
+    if (best < 0) break;
+    c = best;
+  }
+  int cur = c;
+  for (int p = c; p < qi; ++p) {
+    int sp = 1;
+    if (p >= cur && slow_at(p, sp)) cur = p + sp;
+  }
+  return qi >= cur ? 1 : 0;
+}
+
+// N1: words of the block's positions and of its halo, their slow bits and the slow attempts (span, acceptance,
+// value), every slow position's place on the chain (for the halo's last XG_LOOK - XG_SPAN positions too), then
+// which of the block's positions produce a normal: a slow one when on-chain and accepted, a fast one unless an
+// on-chain slow attempt in the XG_SPAN positions before it spans it. Writes the slow and produced bitmaps, span /
+// value of the block's slow positions, the block's base state and its count.
+__global__ __launch_bounds__(XGT) void xg_norm_classify(XgCall a) {
+  const int64_t n = xg_n(a);
+  const int need = xg_norm_need(a, n);
+  const int q0 = blockIdx.x * XGT;
+  if (n == 0 || q0 >= need) return;
+  __shared__ XgView v;
+  __shared__ uint64_t hb[2];
+  const CrRng s0 = a.st[a.rd];
+  const int t = threadIdx.x, lane = t & 63;
+  if (t == 64) {  // the halo's base state (wave 1) beside the block's (thread 0, in xg_base_state)
+    const u128 h = q0 >= XG_LOOK ? pcg_jump(a.jt, mk128(s0.s_hi, s0.s_lo), (uint32_t)(q0 - XG_LOOK)) : (u128)0;
+    hb[0] = hi64(h);
+    hb[1] = lo64(h);
+  }
+  const u128 sb = xg_base_state(a, s0, q0, a.bstate);
+  const ZigTabs zt = xg_zig();
+  const u128 inc = xg_inc(s0);
+  // own position (view index XG_LOOK + t) and, for t < XG_LOOK, the halo position (view index t)
+  double val = 0.0;
+#pragma unroll
+  for (int part = 0; part < 2; ++part) {
+    if (part == 1 && t >= XG_LOOK) break;  // wave-uniform (XG_LOOK = one wave)
+    const int i = part == 0 ? XG_LOOK + t : t;
+    const int q = q0 - XG_LOOK + i;
+    const bool live = q >= 0 && q < need;
+    const u128 X = apply_jump(a.wj[t + 1], part == 0 ? sb : mk128(hb[0], hb[1]));
+    double z;
+    const bool slow = live && !zig_fast(zt, pcg_output(X), z);
+    const uint64_t m = __ballot(slow);
+    if (lane == 0) v.bits[i >> 6] = m;
+    if (slow) {
+      int u = 1;
+      double vv = 0.0;
+      const int r = xg_attempt(zt, X, inc, u, vv);
+      if (r < 0) atomicOr(a.err, GP_DERR_STREAM);
+      v.span[i] = (uint16_t)u;
+      v.flag[i] = (uint8_t)(r > 0 ? 2u : 0u);
+      if (part == 0) val = vv;
+    }
+  }
+  __syncthreads();
+  // on-chain bits of the slow positions at view indices [XG_SPAN, XGH): own (t) and the halo's tail (t < 32)
+  const int i = XG_LOOK + t, q = q0 + t;
+  const bool slow = xv_slow(v, i);
+  int on = 0;
+  if (slow && (on = xv_on_chain(v, i, q0 == 0)) < 0) on = xg_on_chain_abs(a, v, q0, s0, q);
+  const int ih = XG_SPAN + t;
+  int onh = 0;
+  const bool slowh = t < XG_LOOK - XG_SPAN && xv_slow(v, ih);
+  if (slowh && (onh = xv_on_chain(v, ih, q0 == 0)) < 0) onh = xg_on_chain_abs(a, v, q0, s0, q0 - XG_LOOK + ih);
+  __syncthreads();  // every walk has read the view's spans; now the flags get their on-chain bit
+  if (slow && on) v.flag[i] |= 1u;
+  if (slowh && onh) v.flag[ih] |= 1u;
+  __syncthreads();
+  bool prod;
+  if (q >= need) {
+    prod = false;
+  } else if (slow) {
+    prod = (v.flag[i] & 3u) == 3u;
+    a.span[q] = v.span[i];
+    a.val[q] = val;
+  } else {
+    prod = true;
+    uint64_t m[3];
+    int base;
+    xv_window(v, i - XG_SPAN, i, m, base);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      uint64_t w = m[k];
+      while (w) {
+        const int p = base + 64 * k + __builtin_ctzll(w);
+        w &= w - 1;
+        if ((v.flag[p] & 1u) && p + (int)v.span[p] > i) prod = false;
+      }
+    }
+  }
+  const uint64_t pm = __ballot(prod);
+  if (lane == 0) {
+    a.bits[q >> 6] = v.bits[i >> 6];
+    a.pbits[q >> 6] = pm;
+  }
+  const uint32_t cnt = xg_block_sum(lane == 0 ? (uint32_t)__builtin_popcountll(pm) : 0u);
+  if (t == 0) xg_publish(a.pc, blockIdx.x, (need + XGT - 1) / XGT, cnt);
+}
+
+// N2: every produced normal's index r (prefix of the block counts + its rank in the block) -> dst[r]; the n-th
+// one ends the call. No block waits on another.
+__global__ __launch_bounds__(XGT) void xg_norm_write(XgCall a) {
+  const int64_t n = xg_n(a);
+  const int need = xg_norm_need(a, n);
+  const int bid = blockIdx.x, q0 = bid * XGT;
+  const CrRng s0 = a.st[a.rd];
+  if (n == 0) {  // nothing drawn: the state carries over
+    if (bid == 0 && threadIdx.x == 0) a.st[a.wr] = s0;
+    return;
+  }
+  if (q0 >= need) return;
+  const int64_t pre = xg_prefix(a.pc, bid);
+  const int nb = (need + XGT - 1) / XGT;
+  if (bid == nb - 1 && threadIdx.x == 0 && pre + a.pc.bc[bid] < n) atomicOr(a.err, GP_DERR_STREAM);
+  if (pre >= n) return;  // block-uniform
+  uint32_t before;
+  const bool prod = xg_block_bit(a.pbits + (size_t)bid * XGW, before);
+  const int64_t r = pre + before;
+  if (!prod || r >= n) return;
+  const int q = q0 + threadIdx.x;
+  const bool fq = !((a.bits[q >> 6] >> (threadIdx.x & 63)) & 1ull);
+  double val;
+  if (fq) {
+    const u128 sb = mk128(a.bstate[2 * bid], a.bstate[2 * bid + 1]);
+    zig_fast(xg_zig(), pcg_output(apply_jump(a.wj[threadIdx.x + 1], sb)), val);
+  } else {
+    val = a.val[q];
+  }
+  a.dst[r] = 0.0 + a.scale * val;  // numpy: loc + scale * standard_normal
+  if (r == n - 1) {
+    const uint32_t endpos = (uint32_t)q + (fq ? 1u : (uint32_t)a.span[q]);
+    xg_put_state(a.st, a.wr, s0, pcg_jump(a.jt, mk128(s0.s_hi, s0.s_lo), endpos), s0.has_u32, s0.uinteger);
+  }
+}
+
+// choice(n), per word q: the Lemire acceptances of (lo, hi) (+ the buffered half at q = 0) as 3 flag bits.
+__device__ __forceinline__ uint32_t xg_cho_flags(const XgCall& a, const CrRng& s0, int q, int need, uint64_t w) {
+  uint32_t f = 0;
+  if (q < need) {
+    if (q == 0 && s0.has_u32 && !lemire_rejected(s0.uinteger, a.nv, a.lthr)) f |= 1u;
+    if (!lemire_rejected((uint32_t)w, a.nv, a.lthr)) f |= 2u;
+    if (!lemire_rejected((uint32_t)(w >> 32), a.nv, a.lthr)) f |= 4u;
+  }
+  return f;
+}
+// C1: per block, the drawn candidates (and the block's base state).
+__global__ __launch_bounds__(XGT) void xg_cho_count(XgCall a) {
+  const int64_t n = xg_n(a);
+  const int need = xg_cho_need(a, n);
+  const int q0 = blockIdx.x * XGT;
+  if (n == 0 || q0 >= need) return;
+  const CrRng s0 = a.st[a.rd];
+  const u128 sb = xg_base_state(a, s0, q0, a.bstate);
+  const uint64_t w = pcg_output(apply_jump(a.wj[threadIdx.x + 1], sb));
+  const uint32_t cnt = xg_block_sum((uint32_t)__builtin_popcount(xg_cho_flags(a, s0, q0 + threadIdx.x, need, w)));
+  if (threadIdx.x == 0) xg_publish(a.pc, blockIdx.x, (need + XGT - 1) / XGT, cnt);
+}
+// C2: the draws to idst[r]; the n-th one fixes the next state, has_uint32 and uinteger.
+__global__ __launch_bounds__(XGT) void xg_cho_write(XgCall a) {
+  const int64_t n = xg_n(a);
+  const int need = xg_cho_need(a, n);
+  const int bid = blockIdx.x, q0 = bid * XGT;
+  const CrRng s0 = a.st[a.rd];
+  if (n == 0) {
+    if (bid == 0 && threadIdx.x == 0) a.st[a.wr] = s0;
+    return;
+  }
+  if (q0 >= need) return;
+  const int64_t pre = xg_prefix(a.pc, bid);
+  const int nb = (need + XGT - 1) / XGT;
+  if (bid == nb - 1 && threadIdx.x == 0 && pre + a.pc.bc[bid] < n) atomicOr(a.err, GP_DERR_STREAM);
+  if (pre >= n) return;  // block-uniform
+  const int q = q0 + threadIdx.x;
+  const uint64_t w = pcg_output(apply_jump(a.wj[threadIdx.x + 1], mk128(a.bstate[2 * bid], a.bstate[2 * bid + 1])));
+  const uint32_t f = xg_cho_flags(a, s0, q, need, w);
+  uint32_t tot;
+  int64_t r = pre + xg_block_scan((uint32_t)__builtin_popcount(f), tot);
+  // candidates in stream order: buffered half (code 0), lo of word q (2q + 1), hi (2q + 2)
+  const uint32_t cand[3] = {s0.uinteger, (uint32_t)w, (uint32_t)(w >> 32)};
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    if (!((f >> c) & 1u)) continue;
+    if (r < n) a.idst[r] = (int32_t)lemire_value(cand[c], a.nv);
+    if (r == n - 1) {
+      const uint32_t e = c == 0 ? 0u : 2u * (uint32_t)q + (uint32_t)c;  // the last candidate consumed
+      const uint32_t words = (e + 1u) / 2u;
+      // numpy's next_uint32 buffers the high half of every word it draws and keeps it after handing it out
+      xg_put_state(a.st, a.wr, s0, pcg_jump(a.jt, mk128(s0.s_hi, s0.s_lo), words), (e & 1u),
+                   e ? (uint32_t)(w >> 32) : s0.uinteger);
+    }
+    ++r;
+  }
+}
+
+// random(n): n uniforms k53 = w >> 11 (numpy next_double), word e for draw e.
+__global__ __launch_bounds__(XGT) void xg_uniforms(XgCall a, uint64_t* __restrict__ dst) {
+  const int64_t n = a.n_host;
+  const int q0 = blockIdx.x * XGT;
+  const CrRng s0 = a.st[a.rd];
+  const u128 S = mk128(s0.s_hi, s0.s_lo);
+  if (blockIdx.x == 0 && threadIdx.x == 0) xg_put_state(a.st, a.wr, s0, pcg_jump(a.jt, S, (uint32_t)n), s0.has_u32,
+                                                         s0.uinteger);
+  if (q0 >= n) return;
+  const u128 sb = xg_base_state(a, s0, q0, nullptr);
+  const int q = q0 + threadIdx.x;
+  if (q < n) dst[q] = pcg_output(apply_jump(a.wj[threadIdx.x + 1], sb)) >> 11;
+}
+
+// Dry step on copies: which envs hit a wall (the wall-noise draw count, crooms.py:321-325) -> fd.
+template <int OK>
+__global__ __launch_bounds__(XGT) void xg_dry(CrDev p, XgFlags fd, const void* __restrict__ act, size_t off) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  for (int i = threadIdx.x; i < p.tab_bytes / 16; i += XGT) ((uint4*)lds)[i] = ((const uint4*)p.tabs)[i];
+  __syncthreads();
+  const int env = blockIdx.x * XGT + threadIdx.x;
+  bool f = false;
+  if (env < p.B) {
+    double a0, a1;
+    int ad;
+    x_load_action(p, act, off, env, a0, a1, ad);
+    double ay = p.ay[env], ax = p.ax[env];
+    double vy = p.use_velocity ? p.vy[env] : 0.0, vx = p.use_velocity ? p.vx[env] : 0.0;
+    uint32_t g = x_goal(p, env);
+    int32_t el = p.el[env];
+    float rs = 0.f;
+    uint32_t ep = 0, ln = 0;
+    const StepOut o = crooms_env_step<true>(p, lds, env, true, 0, a0, a1, ad, ay, ax, vy, vx, g, el, rs, ep, ln);
+    f = o.oob != 0;
+  }
+  xg_flag_block(fd, blockIdx.x, gridDim.x, f);
+}
+
+// The step with the wall noise in place (crooms.py:276-298; an env that hits a wall reads pair r of the wall
+// noise, r = its rank among fd's envs), resets deferred -> fs.
+template <int OK>
+__global__ __launch_bounds__(XGT) void xg_step(CrDev p, XgFlags fd, XgFlags fs, const void* __restrict__ act,
+                                               size_t off, void* __restrict__ obs, float* __restrict__ rew,
+                                               uint8_t* __restrict__ term, uint8_t* __restrict__ trunc) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  for (int i = threadIdx.x; i < p.tab_bytes / 16; i += XGT) ((uint4*)lds)[i] = ((const uint4*)p.tabs)[i];
+  const int bid = blockIdx.x;
+  const uint32_t wpre = xg_prefix(fd.c, bid);  // (its block sum syncs the table copy too)
+  uint32_t wbefore;
+  xg_block_bit(fd.bits + (size_t)bid * XGW, wbefore);
+  const int env = bid * XGT + threadIdx.x;
+  bool f = false;
+  float rsum = 0.f;
+  uint32_t eps = 0, lens = 0, nst = 0;
+  if (env < p.B) {
+    double a0, a1;
+    int ad;
+    x_load_action(p, act, off, env, a0, a1, ad);
+    double ay = p.ay[env], ax = p.ax[env];
+    double vy = p.use_velocity ? p.vy[env] : 0.0, vx = p.use_velocity ? p.vx[env] : 0.0;
+    uint32_t g = x_goal(p, env);
+    int32_t el = p.el[env];
+    const StepOut o = crooms_env_step<true, true>(p, lds, env, true, 0, a0, a1, ad, ay, ax, vy, vx, g, el, rsum, eps,
+                                                  lens, (int)(wpre + wbefore));
+    nst = 1;
+    rew[off + env] = o.rew;
+    term[off + env] = o.term;
+    trunc[off + env] = o.trunc;
+    f = (o.term | o.trunc) != 0;
+    if (!f) {
+      write_obs<OK>(p, lds, env, ay, ax, g, obs);
+      p.ay[env] = ay;
+      p.ax[env] = ax;
+      if (p.use_velocity) { p.vy[env] = vy; p.vx[env] = vx; }
+    }
+    p.el[env] = el;
+  }
+  xg_flag_block(fs, bid, gridDim.x, f);
+  // episode statistics: block reduction, one set of atomics per block into slot 0
+  __shared__ float m_r[XGW];
+  __shared__ uint32_t m_e[XGW], m_l[XGW], m_n[XGW];
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    rsum += __shfl_xor(rsum, d, 64);
+    eps += __shfl_xor(eps, d, 64);
+    lens += __shfl_xor(lens, d, 64);
+    nst += __shfl_xor(nst, d, 64);
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) { m_r[wv] = rsum; m_e[wv] = eps; m_l[wv] = lens; m_n[wv] = nst; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float r = 0.f;
+    uint32_t ee = 0, l = 0, nn = 0;
+    for (int i = 0; i < XGW; ++i) { r += m_r[i]; ee += m_e[i]; l += m_l[i]; nn += m_n[i]; }
+    CrSlot& m = p.mslot[0];
+    atomicAdd(&m.return_sum, (double)r);
+    atomicAdd(&m.episodes, (unsigned long long)ee);
+    atomicAdd(&m.length_sum, (unsigned long long)l);
+    atomicAdd(&m.env_steps, (unsigned long long)nn);
+  }
+}
+
+// The resets (crooms.py:217-244 goal then agent; :251-266 for reset()): fs's envs, the env of rank r taking
+// gi[r] / ai[r]; or every env (fs.bits == nullptr: reset(), by env index; elapsed and velocity cleared too).
+template <int OK>
+__global__ __launch_bounds__(XGT) void xg_apply_resets(CrDev p, XgFlags fs, const int32_t* __restrict__ gi,
+                                                       const int32_t* __restrict__ ai, void* __restrict__ obs) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int bid = blockIdx.x, env = bid * XGT + threadIdx.x;
+  int r = env;
+  bool f = env < p.B;
+  if (fs.bits) {
+    const uint64_t* w = fs.bits + (size_t)bid * XGW;
+    uint64_t any = 0;
+#pragma unroll
+    for (int j = 0; j < XGW; ++j) any |= w[j];
+    if (!any) return;  // block-uniform: nothing resets here
+    const uint32_t pre = xg_prefix(fs.c, bid);
+    uint32_t before;
+    f = xg_block_bit(w, before);
+    r = (int)(pre + before);
+  }
+  for (int i = threadIdx.x; i < p.tab_bytes / 16; i += XGT) ((uint4*)lds)[i] = ((const uint4*)p.tabs)[i];
+  __syncthreads();
+  if (!f) return;
+  Draws d;
+  d.k53 = 0;
+  d.gi = p.goal_fixed ? 0u : (uint32_t)gi[r];
+  d.ai = p.agent_fixed ? 0u : (uint32_t)ai[r];
+  double ay, ax, vy, vx;
+  uint32_t g = x_goal(p, env);
+  reset_env(p, lds, d, ay, ax, vy, vx, g);
+  p.ay[env] = ay;
+  p.ax[env] = ax;
+  if (p.use_velocity) { p.vy[env] = 0.0; p.vx[env] = 0.0; }
+  if (!p.goal_fixed) p.goal[env] = g;
+  if (!fs.bits) p.el[env] = 0;
+  write_obs<OK>(p, lds, env, ay, ax, g, obs);
+}
+
+__global__ void xg_copy_state(CrRng* st, int from, int to) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) st[to] = st[from];
+}
+
 // ------------------------------------------------------------------ host backend ----
 template <class F>
 static int dispatch_obs(int ok, F&& f) {
@@ -1179,6 +1827,88 @@ struct CRoomsBackend : EnvBackend {
   CrExact xd{};
   int x_alloc();
   int x_upload_rng(const RngHost& r);
+  // multi-workgroup exact mode (B > XG_MIN_ENVS): position buffers, block counts, the env phases' flags
+  DevBuf xg_jt, xg_bits, xg_pbits, xg_bstate, xg_span, xg_val, xg_cnt, xg_ebits;
+  int xg_P = 0;                  // positions of a draw call (>= what normal(2B) needs)
+  int xg_nbe = 0;                // env blocks
+  int xg_slot = 0;               // the stream-state slot holding the current state (0 between API calls)
+  bool xg_on() const { return rng_mode == GP_RNG_NUMPY && B > XG_MIN_ENVS; }
+  // count sets in xg_cnt: 0 = the draw calls' positions, 1 = dry-step wall hits, 2 = resetting envs
+  XgCounts xg_counts(int k) {
+    const size_t nbp = (size_t)xg_P / XGT, cap = std::max(nbp, (size_t)xg_nbe), ng = cap / 64 + 1;
+    uint8_t* base = xg_cnt.as<uint8_t>() + (size_t)k * (8 * ng + 4 * ng + 4 * cap);
+    XgCounts c{};
+    c.acc = reinterpret_cast<unsigned long long*>(base);
+    c.gs = reinterpret_cast<uint32_t*>(base + 8 * ng);
+    c.bc = reinterpret_cast<uint32_t*>(base + 12 * ng);
+    return c;
+  }
+  size_t xg_cnt_bytes() const {
+    const size_t nbp = (size_t)xg_P / XGT, cap = std::max(nbp, (size_t)xg_nbe), ng = cap / 64 + 1;
+    return 3 * (8 * ng + 4 * ng + 4 * cap);
+  }
+  XgFlags xg_flags(int k) {  // k = 1 wall hits, 2 resets
+    XgFlags f{};
+    f.bits = xg_ebits.as<uint64_t>() + (size_t)(k - 1) * xg_nbe * XGW;
+    f.c = xg_counts(k);
+    return f;
+  }
+  XgCall xg_call(int64_t n_host, int nsrc, int nmul) {  // nsrc: n = nmul * (flagged envs of count set nsrc)
+    XgCall a{};
+    a.jt = xg_jt.as<PcgJump>();
+    a.wj = x_wj.as<PcgJump>();
+    a.st = x_rng.as<CrRng>();
+    a.rd = xg_slot;
+    a.wr = xg_slot ^ 1;
+    if (nsrc) {
+      a.nsrc = xg_counts(nsrc);
+      a.nsrc_blocks = xg_nbe;
+    }
+    a.nmul = nmul;
+    a.n_host = n_host;
+    a.P = xg_P;
+    a.bits = xg_bits.as<uint64_t>();
+    a.pbits = xg_pbits.as<uint64_t>();
+    a.bstate = xg_bstate.as<uint64_t>();
+    a.span = xg_span.as<uint16_t>();
+    a.val = xg_val.as<double>();
+    a.pc = xg_counts(0);
+    a.nv = (uint32_t)d.n_valid;
+    a.lthr = xd.lemire_thr;
+    a.err = derr.ptr();
+    return a;
+  }
+  int xg_normals(int64_t n_host, int nsrc, int nmul, double scale, double* dst, hipStream_t s) {
+    XgCall a = xg_call(n_host, nsrc, nmul);
+    a.scale = scale;
+    a.dst = dst;
+    const unsigned nbp = (unsigned)(xg_P / XGT);
+    hipLaunchKernelGGL(xg_norm_classify, dim3(nbp), dim3(XGT), 0, s, a);
+    hipLaunchKernelGGL(xg_norm_write, dim3(nbp), dim3(XGT), 0, s, a);
+    xg_slot ^= 1;
+    GP_HIP_CHECK(hipGetLastError());
+    return GP_OK;
+  }
+  int xg_choices(int64_t n_host, int nsrc, int32_t* dst, hipStream_t s) {
+    XgCall a = xg_call(n_host, nsrc, 1);
+    a.idst = dst;
+    const unsigned nbc = (unsigned)((B / 2 + B / 1024 + 256 + XGT - 1) / XGT);
+    hipLaunchKernelGGL(xg_cho_count, dim3(nbc), dim3(XGT), 0, s, a);
+    hipLaunchKernelGGL(xg_cho_write, dim3(nbc), dim3(XGT), 0, s, a);
+    xg_slot ^= 1;
+    GP_HIP_CHECK(hipGetLastError());
+    return GP_OK;
+  }
+  int xg_finish(hipStream_t s) {  // the current state back into slot 0 (what get_rng_state / the next call read)
+    if (xg_slot) {
+      hipLaunchKernelGGL(xg_copy_state, dim3(1), dim3(64), 0, s, x_rng.as<CrRng>(), 1, 0);
+      xg_slot = 0;
+    }
+    GP_HIP_CHECK(hipGetLastError());
+    return GP_OK;
+  }
+  int xg_reset(void* obs, hipStream_t s);
+  int xg_rollout(int K, const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc, hipStream_t s);
   const uint64_t* rp_u = nullptr;
   const int32_t* rp_goal = nullptr;
   const int32_t* rp_agent = nullptr;
@@ -1265,7 +1995,7 @@ struct CRoomsBackend : EnvBackend {
       return GP_E_STATE;
     }
     if (rng_mode == GP_RNG_NUMPY) {
-      int e = x_launch(0, 1, nullptr, obs, nullptr, nullptr, nullptr, s);
+      int e = xg_on() ? xg_reset(obs, s) : x_launch(0, 1, nullptr, obs, nullptr, nullptr, nullptr, s);
       if (e) return e;
       has_reset = true;
       return GP_OK;
@@ -1313,7 +2043,7 @@ struct CRoomsBackend : EnvBackend {
     }
     if (rng_mode == GP_RNG_NUMPY) {
       timer.begin(s);
-      int e = x_launch(K, 0, act, obs, rew, term, trunc, s);
+      int e = xg_on() ? xg_rollout(K, act, obs, rew, term, trunc, s) : x_launch(K, 0, act, obs, rew, term, trunc, s);
       timer.end(s);
       return e;
     }
@@ -1631,7 +2361,7 @@ int CRoomsBackend::build(const gp_crooms_config* cfg) {
 int CRoomsBackend::x_alloc() {
   int e;
   const size_t b = (size_t)B;
-  if ((e = x_rng.alloc(sizeof(CrRng))) || (e = x_wj.alloc(sizeof(PcgJump) * (XW + 1))) ||
+  if ((e = x_rng.alloc(2 * sizeof(CrRng))) || (e = x_wj.alloc(sizeof(PcgJump) * (XW + 1))) ||
       (e = x_noise.alloc(16 * b)) || (e = x_wall.alloc(16 * b)) || (e = x_dense.alloc(16 * b)) ||
       (e = x_u.alloc(8 * b)) || (e = x_gi.alloc(4 * b)) || (e = x_ai.alloc(4 * b)) || (e = x_rank.alloc(4 * b)))
     return e;
@@ -1645,7 +2375,96 @@ int CRoomsBackend::x_alloc() {
   xd.ai = x_ai.as<int32_t>();
   xd.rank = x_rank.as<int32_t>();
   xd.lemire_thr = lemire_threshold((uint32_t)d.n_valid);
+  if (B > XG_MIN_ENVS) {
+    // positions of a draw call: normal(2B) needs 2B + 2B / 16 + 4096 at most (xg_norm_need), rounded to blocks
+    const int64_t P = ((2 * b + 2 * b / 16 + 4096 + 64 * XGT - 1) / (64 * XGT)) * (64 * XGT);
+    if (P > (int64_t)1 << 30) {
+      gp_set_error("crooms numpy mode: num_envs too large");
+      return GP_E_INVALID;
+    }
+    xg_P = (int)P;
+    xg_nbe = (int)((b + XGT - 1) / XGT);
+    const size_t nbp = (size_t)P / XGT + 1;
+    if ((e = xg_jt.alloc(sizeof(PcgJump) * JT_LEVELS * JT_RADIX)) || (e = xg_bits.alloc((size_t)P / 8)) ||
+        (e = xg_pbits.alloc((size_t)P / 8)) || (e = xg_bstate.alloc(16 * nbp)) || (e = xg_span.alloc(2 * (size_t)P)) ||
+        (e = xg_val.alloc(8 * (size_t)P)) || (e = xg_cnt.alloc(xg_cnt_bytes())) ||
+        (e = xg_ebits.alloc(2 * 8 * (size_t)xg_nbe * XGW)))
+      return e;
+    GP_HIP_CHECK(hipMemset(xg_cnt.p, 0, xg_cnt_bytes()));  // the group accumulators start (and stay) cleared
+  }
   return x_upload_rng(rng);
+}
+
+int CRoomsBackend::xg_reset(void* obs, hipStream_t s) {  // crooms.py:251-266: goal then agent for every env
+  xg_slot = 0;
+  int e;
+  if (!d.goal_fixed && (e = xg_choices(B, 0, xd.gi, s))) return e;
+  if (!d.agent_fixed && (e = xg_choices(B, 0, xd.ai, s))) return e;
+  XgFlags ev{};  // every env, by env index
+  const CrDev dd = dev_for_launch();
+  const unsigned nbe = (unsigned)((B + XGT - 1) / XGT);
+  e = dispatch_obs(d.obs_kind, [&](auto okc) -> int {
+    constexpr int OK = decltype(okc)::value;
+    hipLaunchKernelGGL(xg_apply_resets<OK>, dim3(nbe), dim3(XGT), d.tab_bytes, s, dd, ev, (const int32_t*)xd.gi,
+                       (const int32_t*)xd.ai, obs);
+    return GP_OK;
+  });
+  if (e) return e;
+  return xg_finish(s);
+}
+
+int CRoomsBackend::xg_rollout(int K, const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc,
+                              hipStream_t s) {
+  xg_slot = 0;
+  CrDev dd = dev_for_launch();
+  dd.rp_u = xd.u;  // the per-env draws of the call sequence, consumed by the replay step
+  dd.rp_goal = xd.gi;
+  dd.rp_agent = xd.ai;
+  dd.rp_noise = xd.noise;
+  dd.rp_wall = xd.wall;
+  const unsigned nbe = (unsigned)((B + XGT - 1) / XGT);
+  const size_t osz = (size_t)d.obs_width * (d.obs_kind == GP_OBS_F32 ? (d.obs_f64 ? 8 : 4)
+                                            : (d.obs_kind == GP_OBS_HANSEN || d.obs_kind == GP_OBS_TABLE ? 4 : 1));
+  const XgFlags fd = xg_flags(1), fs = xg_flags(2);  // wall hits of the dry step, resets of the step
+  int e;
+  for (int k = 0; k < K; ++k) {
+    const size_t off = (size_t)k * B;
+    uint8_t* ob = (uint8_t*)obs + off * osz;
+    // _sample_action's draws (crooms.py:175-198)
+    if (d.action_kind != 0) {
+      XgCall a = xg_call(B, 0, 1);
+      hipLaunchKernelGGL(xg_uniforms, dim3(nbe), dim3(XGT), 0, s, a, xd.u);
+      xg_slot ^= 1;
+    }
+    if ((d.action_kind == 0 || d.action_std != 0.0) &&
+        (e = xg_normals(2 * B, 0, 1, d.action_std, xd.noise, s)))
+      return e;
+    // the dry step: which envs hit a wall; their noise normal(0.5, (n_oob, 2)) (crooms.py:321-325)
+    e = dispatch_obs(d.obs_kind, [&](auto okc) -> int {
+      constexpr int OK = decltype(okc)::value;
+      hipLaunchKernelGGL(xg_dry<OK>, dim3(nbe), dim3(XGT), d.tab_bytes, s, dd, fd, act, off);
+      return GP_OK;
+    });
+    if (e || (e = xg_normals(0, 1, 2, 0.5, xd.wall, s))) return e;
+    // the step itself with the wall noise in place, resets deferred; then the resetting envs' goals / agents
+    e = dispatch_obs(d.obs_kind, [&](auto okc) -> int {
+      constexpr int OK = decltype(okc)::value;
+      hipLaunchKernelGGL(xg_step<OK>, dim3(nbe), dim3(XGT), d.tab_bytes, s, dd, fd, fs, act, off, (void*)ob, rew,
+                         term, trunc);
+      return GP_OK;
+    });
+    if (e) return e;
+    if (!d.goal_fixed && (e = xg_choices(0, 2, xd.gi, s))) return e;
+    if (!d.agent_fixed && (e = xg_choices(0, 2, xd.ai, s))) return e;
+    e = dispatch_obs(d.obs_kind, [&](auto okc) -> int {
+      constexpr int OK = decltype(okc)::value;
+      hipLaunchKernelGGL(xg_apply_resets<OK>, dim3(nbe), dim3(XGT), d.tab_bytes, s, dd, fs, (const int32_t*)xd.gi,
+                         (const int32_t*)xd.ai, (void*)ob);
+      return GP_OK;
+    });
+    if (e) return e;
+  }
+  return xg_finish(s);
 }
 
 // The device stream state and the window jump table wj[j] = j LCG steps (j = 0..XW) for its increment.
@@ -1659,6 +2478,11 @@ int CRoomsBackend::x_upload_rng(const RngHost& r) {
   }
   GP_HIP_CHECK(hipDeviceSynchronize());
   GP_HIP_CHECK(hipMemcpy(x_wj.p, wj.data(), sizeof(PcgJump) * wj.size(), hipMemcpyHostToDevice));
+  if (xg_jt.p) {
+    const std::vector<PcgJump> jt = build_jump_tables(r.inc);
+    GP_HIP_CHECK(hipMemcpy(xg_jt.p, jt.data(), sizeof(PcgJump) * jt.size(), hipMemcpyHostToDevice));
+  }
+  xg_slot = 0;
   CrRng h{hi64(r.state), lo64(r.state), hi64(r.inc), lo64(r.inc), r.has_u32, r.uinteger, 0u, 0u};
   GP_HIP_CHECK(hipMemcpy(x_rng.p, &h, sizeof(CrRng), hipMemcpyHostToDevice));
   return GP_OK;
@@ -1676,14 +2500,21 @@ __global__ void zig_words_kernel(const uint64_t* __restrict__ w, int64_t nw, dou
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const ZigTabs t{d_zig, reinterpret_cast<const double*>(d_zig + 256), reinterpret_cast<const double*>(d_zig + 512)};
   int64_t pos = 0;
-  auto next = [&]() -> uint64_t { return pos < nw ? w[pos++] : 0ull; };
+  bool dry = false;  // a wedge / tail draw of the current normal ran past the words
+  auto next = [&]() -> uint64_t {
+    if (pos < nw) return w[pos++];
+    dry = true;
+    return 0ull;
+  };
   for (int64_t i = 0; i < n; ++i) {
     if (pos >= nw) {
       out[i] = __builtin_nan("");
       continue;
     }
     const uint64_t r = w[pos++];
-    out[i] = zig_normal(t, r, next);
+    dry = false;
+    const double z = zig_normal(t, r, next);
+    out[i] = dry ? __builtin_nan("") : z;
   }
   *used = pos;
 }
@@ -1789,12 +2620,6 @@ extern "C" int gp_normal_tail_counts(uint64_t key, int64_t n, const double* thr,
 
 std::unique_ptr<EnvBackend> make_crooms_backend(const gp_crooms_config* cfg, int64_t B, int device, int rng_mode,
                                                 int* err) {
-  if (rng_mode == GP_RNG_NUMPY && B > GP_CR_NUMPY_MAX_ENVS) {
-    gp_set_error("crooms: rng_mode numpy (the reference's own stream, one workgroup) takes at most %d envs; "
-                 "use philox (same laws) for larger batches", GP_CR_NUMPY_MAX_ENVS);
-    *err = GP_E_INVALID;
-    return nullptr;
-  }
   if (B < 1 || B > (int64_t)1 << 30) {
     gp_set_error("crooms: num_envs %lld out of range", (long long)B);
     *err = GP_E_INVALID;

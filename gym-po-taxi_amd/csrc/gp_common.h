@@ -51,13 +51,15 @@ static inline PcgJump pcg_jump_params(u128 delta, u128 inc) {
 #define JT_RADIX_BITS 6
 #define JT_RADIX 64
 
-// Jump state s by n (< 2^30) LCG steps using the tables (gathers from global memory, L1/L2 hot).
+// Jump state s by n (< 2^30) LCG steps using the tables (gathers from global memory, L1/L2 hot). The
+// levels' entries are loaded up front (independent loads in flight together), then applied in order.
 __device__ __forceinline__ u128 pcg_jump(const PcgJump* __restrict__ jt, u128 s, uint32_t n) {
+  PcgJump e[JT_LEVELS];
 #pragma unroll
-  for (int L = 0; L < JT_LEVELS; ++L) {
-    uint32_t d = (n >> (JT_RADIX_BITS * L)) & (JT_RADIX - 1);
-    if (d) s = apply_jump(jt[L * JT_RADIX + d], s);
-  }
+  for (int L = 0; L < JT_LEVELS; ++L) e[L] = jt[L * JT_RADIX + ((n >> (JT_RADIX_BITS * L)) & (JT_RADIX - 1))];
+#pragma unroll
+  for (int L = 0; L < JT_LEVELS; ++L)
+    if ((n >> (JT_RADIX_BITS * L)) & (JT_RADIX - 1)) s = apply_jump(e[L], s);
   return s;
 }
 

@@ -227,7 +227,8 @@ int gp_query(const gp_env* env, const char* key, int64_t* value);
  * Replaces numpy's Generator.standard_normal (numpy/random/src/distributions/distributions.c,
  * random_standard_normal; the reference draws rng.normal at gym_po/envs/rooms/crooms.py:175-178, :324).
  * gp_standard_normal_words: numpy's algorithm (256-layer ziggurat) over the caller's u64 word stream, in
- *   order, on one device lane: words device u64[nwords], out device f64[n] (NaN once the words run out),
+ *   order, on one device lane: words device u64[nwords], out device f64[n] (NaN for every normal whose
+ *   words run out, mid-draw included),
  *   *used (host) = words consumed. Over numpy's raw PCG64 words it returns numpy's normals.
  * gp_normal_tail_counts: n normals of the philox-mode sampler keyed by `key` (gp_seed's Philox key words),
  *   never stored: counts[j] = #{|z| > thr[j]} (host arrays, nthr <= 8), moments = {sum z, sum z^2}. Syncs. */

@@ -252,6 +252,22 @@ def test_device_ziggurat_tail_heavy_stream_exact(gpu_device):
     np.testing.assert_array_equal(got.view(np.uint64), want.view(np.uint64))
 
 
+def test_device_ziggurat_words_run_out_mid_normal(gpu_device):
+    """A normal whose wedge / tail draws run past the caller's words is NaN, not a value built from
+    zero words; with every word it needs it is numpy's value."""
+    from oracle.ziggurat import standard_normals
+    words = np.random.PCG64(5).random_raw(256) & np.uint64(0xFFFFFFFFFFFFFF00)  # layer 0: many multi-word
+    used = [standard_normals(words, k)[1] for k in range(40)]
+    j = next(k for k in range(39) if used[k + 1] - used[k] > 1)  # normal j takes more than one word
+    want = np.asarray(standard_normals(words, j + 1)[0], np.float64)
+    got, _ = _device_normals(words[:used[j + 1] - 1].copy(), j + 2, gpu_device)
+    np.testing.assert_array_equal(got[:j].view(np.uint64), want[:j].view(np.uint64))
+    assert np.isnan(got[j:]).all()
+    got, u = _device_normals(words[:used[j + 1]].copy(), j + 1, gpu_device)
+    assert u == used[j + 1]
+    np.testing.assert_array_equal(got.view(np.uint64), want.view(np.uint64))
+
+
 def test_philox_normal_tail_mass(gpu_device):
     """The philox-mode sampler has the normal law's tails: exceedance counts of |z| beyond 3..6.5 sigma over
     2^36 draws within 6 Poisson standard deviations of n * erfc(t / sqrt 2) (the former float32 Box-Muller

@@ -1,4 +1,5 @@
-"""GPU parity of C-ROOMS exact mode (rng_mode="numpy", csrc/crooms.hip crooms_numpy_rollout).
+"""GPU parity of C-ROOMS exact mode (rng_mode="numpy", csrc/crooms.hip: crooms_numpy_rollout for B <= 4096, the
+multi-workgroup xg_* draw-call kernels above).
 
 The device draws the reference's own PCG64 stream word for word — rng.random / rng.normal (numpy's
 256-layer ziggurat, a data-dependent number of words per normal) / rng.choice (buffered 32-bit Lemire) in
@@ -77,8 +78,13 @@ ORACLE_CASES = [
     ({"obs_type": "hansen8", "action_type": "ordinal", "layout": "16", "goal_xy": None, "time_limit": 20}, 1500, 45, 1),
     ({"obs_type": "grid", "action_type": "cardinal", "action_std": 0.0, "time_limit": 15}, 999, 40, 40),
     ({"obs_type": "goal_room", "layout": "8b", "goal_xy": None, "time_limit": 12}, 4099, 30, 5),
-    # many windows per draw call (2^17 normals per step): slow attempts at window ends, ~10^3 tail draws
+    # B > 4096: the multi-workgroup path (grid-wide draw calls, cluster-resolved ziggurat chains)
     ({"obs_type": "vector_mdp", "action_std": 0.5, "time_limit": 6}, 65536, 12, 6),
+    ({"obs_type": "vector_goal_mdp", "goal_xy": None, "use_velocity": True, "time_limit": 25}, 30001, 30, 3),
+    ({"obs_type": "hansen8", "action_type": "ordinal", "layout": "16", "goal_xy": None, "time_limit": 20}, 20000, 25, 5),
+    ({"obs_type": "grid", "action_type": "cardinal", "action_std": 0.0, "time_limit": 9}, 8193, 20, 20),
+    # BASELINE configs[4]'s size: 2^21 envs (4M normals per step, ~1e3 tail normals, wall resamples)
+    ({"obs_type": "vector_mdp"}, 1 << 21, 4, 2),
 ]
 
 

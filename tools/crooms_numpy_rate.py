@@ -1,4 +1,5 @@
-"""Throughput of C-ROOMS exact mode (rng_mode='numpy', one workgroup) beside philox mode, same config.
+"""Throughput of C-ROOMS exact mode (rng_mode='numpy': one workgroup up to 4096 envs, the multi-workgroup draw
+calls above) beside philox mode, same config.
 
 Usage (GPU box): python tools/crooms_numpy_rate.py  -> one JSON line per (mode, B).
 """
@@ -13,7 +14,8 @@ import torch  # noqa: E402
 from gym_po_amd import CRoomsEnv  # noqa: E402
 
 
-def rate(mode, B, K=50, reps=3):
+def rate(mode, B, K=None, reps=3):
+    K = K or (50 if B <= 65536 else 8)
     env = CRoomsEnv(B, obs_type="vector_mdp", rng_mode=mode)
     env.reset(seed=0)
     a = torch.rand((K, B, 2), device=env.device) * 2 - 1
@@ -29,6 +31,6 @@ def rate(mode, B, K=50, reps=3):
 
 
 if __name__ == "__main__":
-    for B in (1024, 4096, 65536):
+    for B in [int(x) for x in sys.argv[1:]] or (1024, 4096, 65536, 1 << 21):
         for mode in ("numpy", "philox"):
             print(json.dumps(rate(mode, B)), flush=True)
