@@ -46,8 +46,13 @@ def build(force=False, debug=False, verbose=True, stamps=False):
     objdir = os.path.join(HERE, "build", "stamps" if stamps else ("debug" if debug else "release"))
     os.makedirs(objdir, exist_ok=True)
 
+    headers = [d for d in deps() if not d.endswith(".hip")]
+
     def compile_one(src):
         obj = os.path.join(objdir, os.path.basename(src).replace(".hip", ".o"))
+        if (not force and os.path.exists(obj)
+                and all(os.path.getmtime(d) <= os.path.getmtime(obj) for d in [src, __file__] + headers)):
+            return obj  # this object is newer than its source, every header and this script's flags
         cmd = [hipcc] + flags + ["-c", src, "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)

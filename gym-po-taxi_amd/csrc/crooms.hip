@@ -23,6 +23,7 @@
 // Kernels: a persistent, grid-stride rollout kernel (tables staged in LDS once per block, 512-env
 // tiles, K steps per tile, 2 envs per thread).
 #include <algorithm>
+#include <cassert>
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -202,6 +203,10 @@ struct ZigTabs {
   const double* fi;
 };
 __device__ __forceinline__ double u53_of(uint64_t w) { return (double)(w >> 11) * (1.0 / 9007199254740992.0); }
+// zig_dry(next): the word source ran out (only the diagnostic source below can); a tail loop fed by an exhausted
+// source would otherwise spin forever on zero words (0 > 0 never accepts).
+template <class NEXT>
+__device__ __forceinline__ bool zig_dry(const NEXT&) { return false; }
 template <class NEXT>
 __device__ __forceinline__ double zig_slow(const ZigTabs& t, uint64_t r, NEXT& next) {
   for (;;) {
@@ -215,7 +220,7 @@ __device__ __forceinline__ double zig_slow(const ZigTabs& t, uint64_t r, NEXT& n
       for (;;) {
         const double xx = -GP_ZIG_INV_R * zlog1p_neg(u53_of(next()));
         const double yy = -zlog1p_neg(u53_of(next()));
-        if (yy + yy > xx * xx) return ((rabs >> 8) & 1u) ? -(GP_ZIG_R + xx) : GP_ZIG_R + xx;
+        if (yy + yy > xx * xx || zig_dry(next)) return ((rabs >> 8) & 1u) ? -(GP_ZIG_R + xx) : GP_ZIG_R + xx;
       }
     }
     if ((t.fi[idx - 1] - t.fi[idx]) * u53_of(next()) + t.fi[idx] < zexp(-0.5 * x * x)) return x;
@@ -1834,19 +1839,28 @@ struct CRoomsBackend : EnvBackend {
   int xg_slot = 0;               // the stream-state slot holding the current state (0 between API calls)
   bool xg_on() const { return rng_mode == GP_RNG_NUMPY && B > XG_MIN_ENVS; }
   // count sets in xg_cnt: 0 = the draw calls' positions, 1 = dry-step wall hits, 2 = resetting envs
+  // One count set: acc (8-B atomics) | gs | bc, the set's size rounded up to 256 B so that every set's acc
+  // array stays 8-byte aligned (a misaligned 64-bit atomic faults the queue; with an odd group count the
+  // unrounded 12 * ng + 4 * cap bytes put set 1 on a 4-byte boundary).
+  size_t xg_cnt_groups() const {
+    const size_t nbp = (size_t)xg_P / XGT, cap = std::max(nbp, (size_t)xg_nbe);
+    return cap / 64 + 1;
+  }
+  size_t xg_cnt_set_bytes() const {
+    const size_t nbp = (size_t)xg_P / XGT, cap = std::max(nbp, (size_t)xg_nbe), ng = xg_cnt_groups();
+    return (8 * ng + 4 * ng + 4 * cap + 255) & ~(size_t)255;
+  }
   XgCounts xg_counts(int k) {
-    const size_t nbp = (size_t)xg_P / XGT, cap = std::max(nbp, (size_t)xg_nbe), ng = cap / 64 + 1;
-    uint8_t* base = xg_cnt.as<uint8_t>() + (size_t)k * (8 * ng + 4 * ng + 4 * cap);
+    const size_t ng = xg_cnt_groups();
+    uint8_t* base = xg_cnt.as<uint8_t>() + (size_t)k * xg_cnt_set_bytes();
     XgCounts c{};
     c.acc = reinterpret_cast<unsigned long long*>(base);
     c.gs = reinterpret_cast<uint32_t*>(base + 8 * ng);
     c.bc = reinterpret_cast<uint32_t*>(base + 12 * ng);
+    assert(((uintptr_t)c.acc & 7u) == 0);
     return c;
   }
-  size_t xg_cnt_bytes() const {
-    const size_t nbp = (size_t)xg_P / XGT, cap = std::max(nbp, (size_t)xg_nbe), ng = cap / 64 + 1;
-    return 3 * (8 * ng + 4 * ng + 4 * cap);
-  }
+  size_t xg_cnt_bytes() const { return 3 * xg_cnt_set_bytes(); }
   XgFlags xg_flags(int k) {  // k = 1 wall hits, 2 resets
     XgFlags f{};
     f.bits = xg_ebits.as<uint64_t>() + (size_t)(k - 1) * xg_nbe * XGW;
@@ -2493,30 +2507,38 @@ int CRoomsBackend::x_upload_rng(const RngHost& r) {
 // ---- diagnostics of the normal sampler (C ABI below) ----
 namespace {
 
+// The caller's words in order; past the end it returns 0 and sets `dry` (a wedge / tail draw of the current
+// normal ran past the words: that normal is NaN, and zig_dry ends its tail loop).
+struct ZigWordSource {
+  const uint64_t* w;
+  int64_t nw, pos;
+  bool dry;
+  __device__ uint64_t operator()() {
+    if (pos < nw) return w[pos++];
+    dry = true;
+    return 0ull;
+  }
+};
+__device__ __forceinline__ bool zig_dry(const ZigWordSource& s) { return s.dry; }
+
 // numpy's standard_normal over a caller word stream, one lane, in order (numpy consumes the words
 // sequentially and a normal may take several).
 __global__ void zig_words_kernel(const uint64_t* __restrict__ w, int64_t nw, double* __restrict__ out, int64_t n,
                                  int64_t* __restrict__ used) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const ZigTabs t{d_zig, reinterpret_cast<const double*>(d_zig + 256), reinterpret_cast<const double*>(d_zig + 512)};
-  int64_t pos = 0;
-  bool dry = false;  // a wedge / tail draw of the current normal ran past the words
-  auto next = [&]() -> uint64_t {
-    if (pos < nw) return w[pos++];
-    dry = true;
-    return 0ull;
-  };
+  ZigWordSource next{w, nw, 0, false};
   for (int64_t i = 0; i < n; ++i) {
-    if (pos >= nw) {
+    if (next.pos >= nw) {
       out[i] = __builtin_nan("");
       continue;
     }
-    const uint64_t r = w[pos++];
-    dry = false;
+    const uint64_t r = w[next.pos++];
+    next.dry = false;
     const double z = zig_normal(t, r, next);
-    out[i] = dry ? __builtin_nan("") : z;
+    out[i] = next.dry ? __builtin_nan("") : z;
   }
-  *used = pos;
+  *used = next.pos;
 }
 
 // n normals of the philox-mode sampler (counter (i, 0, 0, TAG_NOISE) for the pair 2i, 2i+1, as

@@ -77,13 +77,22 @@ static inline uint32_t lemire_threshold(uint32_t n) { return (uint32_t)((0xFFFFF
 struct Philox4 {
   uint32_t x[4];
 };
+// a ^ b ^ c: ONE gfx950 v_bitop3_b32 (truth table 0x96) on the device, where the compiler emits two v_xor_b32
+// (gfx950 has no v_xor3_b32); Philox4x32-10 spends 2 of its 3 VALU ops per output word per round here.
+GP_HD uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#else
+  return a ^ b ^ c;
+#endif
+}
 GP_HD Philox4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
   const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
     uint64_t p0 = (uint64_t)M0 * c0, p1 = (uint64_t)M1 * c2;
     uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0, hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
-    uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    uint32_t n0 = xor3(hi1, c1, k0), n2 = xor3(hi0, c3, k1);
     c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
     k0 += W0; k1 += W1;
   }
