@@ -66,6 +66,7 @@ struct CrDev {
   uint32_t key0, key1;
   double cell, half_cell, hi_y, hi_x, s_thr, action_std, action_power;
   double inv_cell;       // 1 / cell when cell is a power of two (then y * inv_cell == y / cell exactly), else 0
+  double gcy, gcx;       // fixed goal: its square's centre goal_y + 0.5, goal_x + 0.5 (as the device computes it)
   float r_step, r_wall, r_goal;
   const uint8_t* tabs;   // packed tables, staged into LDS
   int32_t off_wall, off_valid, off_thr, off_t1, off_t2, off_hbase, off_hvec, off_doff, off_window, tab_bytes;
@@ -331,6 +332,7 @@ struct Cells {
 
 // coord / cell_size, exactly as numpy divides (a multiply when cell_size is a power of two)
 __device__ __forceinline__ double per_cell(const CrDev& p, double v) {
+  if (p.inv_cell == 1.0) return v;  // uniform: the default cell size (v * 1.0 == v, two f64 multiplies saved)
   return p.inv_cell != 0.0 ? v * p.inv_cell : v / p.cell;
 }
 
@@ -469,8 +471,10 @@ __device__ __forceinline__ StepOut crooms_env_step(const CrDev& p, const uint8_t
       mx = mx + nx;
     }
   }
-  my = my * p.action_power;
-  mx = mx * p.action_power;
+  if (p.action_power != 1.0) {  // uniform: x * 1.0 == x, so the default power skips two f64 multiplies
+    my = my * p.action_power;
+    mx = mx * p.action_power;
+  }
   // _apply_action (crooms.py:300-331)
   double py, px;
   if (p.use_velocity) {
@@ -502,7 +506,9 @@ __device__ __forceinline__ StepOut crooms_env_step(const CrDev& p, const uint8_t
     vx = 0.0;
   }
   // reward / termination (crooms.py:289-297)
-  const double gyc = (double)(int16_t)(g & 0xFFFF) + 0.5, gxc = (double)(int16_t)(g >> 16) + 0.5;
+  // the goal square's centre (a fixed goal's from the kernel arguments: uniform, no per-env conversion)
+  const double gyc = p.goal_fixed ? p.gcy : (double)(int16_t)(g & 0xFFFF) + 0.5;
+  const double gxc = p.goal_fixed ? p.gcx : (double)(int16_t)(g >> 16) + 0.5;
   const double dy = ay - gyc, dx = ax - gxc;
   const double s = dy * dy + dx * dx;
   o.term = s <= p.s_thr ? 1 : 0;
@@ -1328,7 +1334,7 @@ __device__ __forceinline__ void xg_put_state(CrRng* st, int wr, const CrRng& old
 __device__ __forceinline__ u128 xg_base_state(const XgCall& a, const CrRng& s0, int q0, uint64_t* bstate) {
   __shared__ uint64_t bb[2];
   if (threadIdx.x == 0) {
-    const u128 b = pcg_jump(a.jt, mk128(s0.s_hi, s0.s_lo), (uint32_t)q0);
+    const u128 b = pcg_jump_ilp(a.jt, mk128(s0.s_hi, s0.s_lo), (uint32_t)q0);
     bb[0] = hi64(b);
     bb[1] = lo64(b);
     if (bstate) {
@@ -1451,7 +1457,7 @@ __device__ __noinline__ int xg_on_chain_abs(const XgCall& a, const XgView& v, in
       span = v.span[i];
       return true;
     }
-    const u128 X = pcg_jump(a.jt, S, (uint32_t)p + 1u);
+    const u128 X = pcg_jump_ilp(a.jt, S, (uint32_t)p + 1u);
     double z;
     if (zig_fast(zt, pcg_output(X), z)) return false;
     double vv;
@@ -1491,7 +1497,7 @@ __global__ __launch_bounds__(XGT) void xg_norm_classify(XgCall a) {
   const CrRng s0 = a.st[a.rd];
   const int t = threadIdx.x, lane = t & 63;
   if (t == 64) {  // the halo's base state (wave 1) beside the block's (thread 0, in xg_base_state)
-    const u128 h = q0 >= XG_LOOK ? pcg_jump(a.jt, mk128(s0.s_hi, s0.s_lo), (uint32_t)(q0 - XG_LOOK)) : (u128)0;
+    const u128 h = q0 >= XG_LOOK ? pcg_jump_ilp(a.jt, mk128(s0.s_hi, s0.s_lo), (uint32_t)(q0 - XG_LOOK)) : (u128)0;
     hb[0] = hi64(h);
     hb[1] = lo64(h);
   }
@@ -1598,7 +1604,7 @@ __global__ __launch_bounds__(XGT) void xg_norm_write(XgCall a) {
   a.dst[r] = 0.0 + a.scale * val;  // numpy: loc + scale * standard_normal
   if (r == n - 1) {
     const uint32_t endpos = (uint32_t)q + (fq ? 1u : (uint32_t)a.span[q]);
-    xg_put_state(a.st, a.wr, s0, pcg_jump(a.jt, mk128(s0.s_hi, s0.s_lo), endpos), s0.has_u32, s0.uinteger);
+    xg_put_state(a.st, a.wr, s0, pcg_jump_ilp(a.jt, mk128(s0.s_hi, s0.s_lo), endpos), s0.has_u32, s0.uinteger);
   }
 }
 
@@ -1654,7 +1660,7 @@ __global__ __launch_bounds__(XGT) void xg_cho_write(XgCall a) {
       const uint32_t e = c == 0 ? 0u : 2u * (uint32_t)q + (uint32_t)c;  // the last candidate consumed
       const uint32_t words = (e + 1u) / 2u;
       // numpy's next_uint32 buffers the high half of every word it draws and keeps it after handing it out
-      xg_put_state(a.st, a.wr, s0, pcg_jump(a.jt, mk128(s0.s_hi, s0.s_lo), words), (e & 1u),
+      xg_put_state(a.st, a.wr, s0, pcg_jump_ilp(a.jt, mk128(s0.s_hi, s0.s_lo), words), (e & 1u),
                    e ? (uint32_t)(w >> 32) : s0.uinteger);
     }
     ++r;
@@ -1667,7 +1673,7 @@ __global__ __launch_bounds__(XGT) void xg_uniforms(XgCall a, uint64_t* __restric
   const int q0 = blockIdx.x * XGT;
   const CrRng s0 = a.st[a.rd];
   const u128 S = mk128(s0.s_hi, s0.s_lo);
-  if (blockIdx.x == 0 && threadIdx.x == 0) xg_put_state(a.st, a.wr, s0, pcg_jump(a.jt, S, (uint32_t)n), s0.has_u32,
+  if (blockIdx.x == 0 && threadIdx.x == 0) xg_put_state(a.st, a.wr, s0, pcg_jump_ilp(a.jt, S, (uint32_t)n), s0.has_u32,
                                                          s0.uinteger);
   if (q0 >= n) return;
   const u128 sb = xg_base_state(a, s0, q0, nullptr);
@@ -2198,6 +2204,8 @@ int CRoomsBackend::build(const gp_crooms_config* cfg) {
   d.goal_fixed = cfg->goal_fixed != 0;
   d.goal_y = cfg->goal_y;
   d.goal_x = cfg->goal_x;
+  d.gcy = (double)(int16_t)(cfg->goal_y & 0xFFFF) + 0.5;  // what the packed int16 goal word decodes to
+  d.gcx = (double)(int16_t)(cfg->goal_x & 0xFFFF) + 0.5;
   d.agent_fixed = cfg->agent_fixed != 0;
   d.agent_y = cfg->agent_y;
   d.agent_x = cfg->agent_x;

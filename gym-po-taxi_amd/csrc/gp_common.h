@@ -51,9 +51,20 @@ static inline PcgJump pcg_jump_params(u128 delta, u128 inc) {
 #define JT_RADIX_BITS 6
 #define JT_RADIX 64
 
-// Jump state s by n (< 2^30) LCG steps using the tables (gathers from global memory, L1/L2 hot). The
-// levels' entries are loaded up front (independent loads in flight together), then applied in order.
+// Jump state s by n (< 2^30) LCG steps using the tables (gathers from global memory, L1/L2 hot), one level's
+// entry at a time (few live registers: the grid kernels' rare paths call this inside register-tight loops).
 __device__ __forceinline__ u128 pcg_jump(const PcgJump* __restrict__ jt, u128 s, uint32_t n) {
+#pragma unroll
+  for (int L = 0; L < JT_LEVELS; ++L) {
+    const uint32_t d = (n >> (JT_RADIX_BITS * L)) & (JT_RADIX - 1);
+    if (d) s = apply_jump(jt[L * JT_RADIX + d], s);
+  }
+  return s;
+}
+// The same with every level's entry loaded up front (independent loads in flight together, then applied in
+// order): for kernels with registers to spare (the C-ROOMS exact mode's draw calls). In the fused grid kernel
+// the 40 extra live VGPRs of this form made every step ~40% slower (K = 128: 4.72 -> 6.67 us/step).
+__device__ __forceinline__ u128 pcg_jump_ilp(const PcgJump* __restrict__ jt, u128 s, uint32_t n) {
   PcgJump e[JT_LEVELS];
 #pragma unroll
   for (int L = 0; L < JT_LEVELS; ++L) e[L] = jt[L * JT_RADIX + ((n >> (JT_RADIX_BITS * L)) & (JT_RADIX - 1))];

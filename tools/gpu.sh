@@ -10,6 +10,8 @@
 #   bash tools/gpu.sh stamps [B K]             phase stamps of the fused numpy kernel (GP_STAMPS build)
 #   bash tools/gpu.sh ab "V1 V2 ..." [B K...]  in-call A/B of library variants (tools/build_variant.sh) at K steps
 #   bash tools/gpu.sh copycal                  FETCH_SIZE / WRITE_SIZE calibration on a plain device copy
+#   bash tools/gpu.sh measure                 driver-config + steady headline lines, MEASURE_WL workloads, VALU costs,
+#                                              CRATE="B ..." C-ROOMS exact-mode rates
 #   bash tools/gpu.sh multi                    bench.py's N>1 path with 2 gloo ranks on one GPU
 # Env: PMC_KERNEL / PMC_CFG / PMC_WORKLOAD for pmc (defaults: the headline kernel and config).
 set -o pipefail
@@ -78,6 +80,18 @@ case "$task" in
       run 120 $O/$P.log rocprofv3 --pmc $P --output-format csv -d $O/$P -o p -- python3 tools/pmc_copy_check.py
     done
     python3 tools/pmc_copy_check.py --summarize $O ;;
+  measure)  # one call, several lines: the driver-config headline, steady state, crooms, anttag, taxi, VALU costs
+    run 300 $O/b_driver.log python3 bench.py --no-cpu-baseline --steps 20 --warmup 5
+    last_json $O/b_driver.log 1200
+    run 300 $O/b_steady.log python3 bench.py --no-cpu-baseline --steps 1280 --warmup 256 --chunk 128
+    last_json $O/b_steady.log 600
+    for w in ${MEASURE_WL:-crooms}; do
+      run 300 $O/b_$w.log python3 bench.py --no-cpu-baseline --workload $w
+      last_json $O/b_$w.log 900
+    done
+    [ -x tools/mb_valu.bin ] && run 60 $O/mb_valu.txt tools/mb_valu.bin && cat $O/mb_valu.txt
+    [ -n "$CRATE" ] && run 300 $O/crooms_rate.jsonl python3 tools/crooms_numpy_rate.py $CRATE && cat $O/crooms_rate.jsonl
+    true ;;
   multi)
     GP_BENCH_BACKEND=gloo run 300 $O/multi2.log python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
       --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 256 --warmup 128 --envs 262144 --no-cpu-baseline

@@ -59,6 +59,38 @@ __global__ void k(uint32_t* out, uint64_t* cyc, uint32_t seed) {
 #define OPX(j) asm volatile("v_add_co_u32 %0, vcc, %0, %1\n\tv_addc_co_u32 %2, vcc, %2, %1, vcc" : "+v"(a##j) : "v"(c), "v"(a0) : "vcc");
       CH8(OPX)
 #undef OPX
+    } else if constexpr (OP == 10) {
+#define OPX(j) asm volatile("v_bitop3_b32 %0, %0, %1, %1 bitop3:0x96" : "+v"(a##j) : "v"(c));
+      CH8(OPX)
+#undef OPX
+    } else if constexpr (OP == 11) {
+#define OPX(j) asm volatile("v_log_f32 %0, %0" : "+v"(a##j));
+      CH8(OPX)
+#undef OPX
+    } else if constexpr (OP == 12) {
+#define OPX(j) asm volatile("v_sin_f32 %0, %0" : "+v"(a##j));
+      CH8(OPX)
+#undef OPX
+    } else if constexpr (OP == 13) {
+#define OPX(j) asm volatile("v_sqrt_f32 %0, %0" : "+v"(a##j));
+      CH8(OPX)
+#undef OPX
+    } else if constexpr (OP == 14) {
+#define OPX(j) asm volatile("v_fma_f64 %0, %0, %1, %1" : "+v"(w##j) : "v"(w0));
+      CH8(OPX)
+#undef OPX
+    } else if constexpr (OP == 15) {
+#define OPX(j) asm volatile("v_mul_f64 %0, %0, %1" : "+v"(w##j) : "v"(w0));
+      CH8(OPX)
+#undef OPX
+    } else if constexpr (OP == 16) {
+#define OPX(j) asm volatile("v_floor_f64 %0, %0" : "+v"(w##j));
+      CH8(OPX)
+#undef OPX
+    } else if constexpr (OP == 17) {
+#define OPX(j) asm volatile("v_fma_f32 %0, %0, %1, %1" : "+v"(a##j) : "v"(c));
+      CH8(OPX)
+#undef OPX
     }
   }
   const uint64_t t1 = clock64();
@@ -91,11 +123,13 @@ double run(int tpb) {
 int main() {
   const char* names[] = {"v_add_u32", "v_mul_lo_u32", "v_mul_hi_u32", "v_mad_u64_u32", "v_lshlrev_b64",
                          "v_alignbit_b32", "v_cmp_gt_u64 + v_cndmask", "v_cmp_gt_u32 + v_cndmask",
-                         "v_lshl_add_u64", "v_add_co + v_addc_co"};
+                         "v_lshl_add_u64", "v_add_co + v_addc_co", "v_bitop3_b32", "v_log_f32", "v_sin_f32",
+                         "v_sqrt_f32", "v_fma_f64", "v_mul_f64", "v_floor_f64", "v_fma_f32"};
   for (int tpb : {256, 512}) {
-    double r[10] = {run<0>(tpb), run<1>(tpb), run<2>(tpb), run<3>(tpb), run<4>(tpb),
-                    run<5>(tpb), run<6>(tpb), run<7>(tpb), run<8>(tpb), run<9>(tpb)};
-    for (int i = 0; i < 10; ++i)
+    double r[18] = {run<0>(tpb), run<1>(tpb), run<2>(tpb), run<3>(tpb), run<4>(tpb), run<5>(tpb),
+                    run<6>(tpb), run<7>(tpb), run<8>(tpb), run<9>(tpb), run<10>(tpb), run<11>(tpb),
+                    run<12>(tpb), run<13>(tpb), run<14>(tpb), run<15>(tpb), run<16>(tpb), run<17>(tpb)};
+    for (int i = 0; i < 18; ++i)
       printf("waves/SIMD %d  %-28s %6.2f clock64 units per wave-op  (%.2fx v_add_u32)\n", tpb / 256, names[i], r[i],
              r[i] / r[0]);
   }
