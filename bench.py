@@ -360,8 +360,9 @@ def main():
 
     # live roofline: HIP events bracketing every step-kernel launch on its stream
     env.set_profiling(True)
-    # whole launches of the timed region's shape (C steps each), so steps_per_launch is exactly C
-    prof_steps = C * max(3, min(2000 // C, max(args.steps // (2 * C), 1)))
+    # whole launches of the timed region's shape (C steps each), so steps_per_launch is exactly C; at least 10
+    # launches (a 3-launch average of 20-step launches moved by ±4% between runs of one build)
+    prof_steps = C * max(10, min(2000 // C, max(args.steps // (2 * C), 1)))
     run(prof_steps)
     kms, nk = env.profile_read()
     rms, nr = env.profile_read_resolver()

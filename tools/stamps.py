@@ -98,8 +98,5 @@ rep("env: staging written (11->12)", e12 - e11)
 rep("env: J_B applied (12->13)", e13 - e12)
 rep("env: B2 wait (13->4)", a[:, :, 4] - e13)
 if (a[:, :, 15] > 0).all():
-    rep("env: early counts (0->14)", a[:, :, 14] - a[:, :, 0])
-    rep("env: early flags+ballots (0->15)", a[:, :, 15] - a[:, :, 0])
-    rep("env: early resolve (15->14)", a[:, :, 14] - a[:, :, 15])
-    rep("env: transitions after early (14->1)", a[:, :, 1] - a[:, :, 14])
-    rep("ctrl: early done -> publish (14->6)", a[:, :, 6] - a[:, :, 14])
+    rep("ctrl: lists ready -> jumps done (14->15)", a[:, :, 15] - a[:, :, 14])
+    rep("ctrl: jumps done -> cells stored (15->9)", a[:, :, 9] - a[:, :, 15])
