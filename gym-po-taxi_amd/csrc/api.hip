@@ -208,6 +208,8 @@ int gp_debug_set(const char* key, int64_t value) {
   else if (!strcmp(key, "spin_limit")) g_dbg.spin_limit = value > 0 ? (uint32_t)value : 0u;
   else if (!strcmp(key, "fault_block")) g_dbg.fault_block = (int)value;
   else if (!strcmp(key, "fused_tile")) g_dbg.fused_tile = (int)value;
+  else if (!strcmp(key, "generic_kernels")) g_dbg.generic_kernels = value != 0;
+  else if (!strcmp(key, "no_spw")) g_dbg.no_spw = value != 0;
   else {
     gp_set_error("gp_debug_set: unknown key '%s'", key);
     return GP_E_INVALID;

@@ -400,10 +400,20 @@ __device__ __forceinline__ void write_obs(const CrDev& p, const uint8_t* lds, in
   }
 }
 
+// Compile-time specialisation of the philox rollout (SPEC = 1: BASELINE configs[4]'s shape -- continuous float32
+// (y, x) actions, no velocity, a fixed goal): these configuration fields become constants, so the step loop carries
+// none of the other configurations' uniform branches, zero-initialisations or their SGPRs (the generic kernel
+// spilled SGPRs to VGPR lanes inside the loop). SPEC = 0 reads them from the arguments.
+template <int SPEC> __device__ __forceinline__ int cr_action_kind(const CrDev& p) { return SPEC ? 0 : p.action_kind; }
+template <int SPEC> __device__ __forceinline__ bool cr_action_f64(const CrDev& p) { return SPEC ? false : p.action_f64 != 0; }
+template <int SPEC> __device__ __forceinline__ bool cr_velocity(const CrDev& p) { return SPEC ? false : p.use_velocity != 0; }
+template <int SPEC> __device__ __forceinline__ bool cr_goal_fixed(const CrDev& p) { return SPEC ? true : p.goal_fixed != 0; }
+
 // reset of one env: goal then agent (crooms.py:217-244, 268-274)
+template <int SPEC = 0>
 __device__ __forceinline__ void reset_env(const CrDev& p, const uint8_t* lds, const Draws& d, double& ay, double& ax,
                                           double& vy, double& vx, uint32_t& g) {
-  if (!p.goal_fixed) {
+  if (!cr_goal_fixed<SPEC>(p)) {
     const uint32_t yx = tab<uint32_t>(lds, p.off_valid)[d.gi];  // y | x << 16: no integer divide
     g = yx;
   }
@@ -431,7 +441,7 @@ struct StepOut {
 // One env-step of CRoomsEnv.step (crooms.py:276-331). DEFER: a terminated / truncated env is left for the
 // caller to reset (its reset draws are not known yet; the exact mode's stream walk). wix (replay): the pair of
 // the wall-noise buffer this env reads when it hits a wall (default: its own, env).
-template <bool REPLAY, bool DEFER = false>
+template <bool REPLAY, bool DEFER = false, int SPEC = 0>
 __device__ __forceinline__ StepOut crooms_env_step(const CrDev& p, const uint8_t* lds, int env, bool live,
                                                    uint64_t step, double a0, double a1, int ad, double& ay,
                                                    double& ax, double& vy, double& vx, uint32_t& g, int32_t& el,
@@ -447,9 +457,9 @@ __device__ __forceinline__ StepOut crooms_env_step(const CrDev& p, const uint8_t
   Philox4 nblk;
   bool nhave = false;
   double ny = 0.0, nx = 0.0;
-  if (live && (p.action_kind == 0 || p.action_std != 0.0))
+  if (live && (cr_action_kind<SPEC>(p) == 0 || p.action_std != 0.0))
     draw_normals<REPLAY>(p, env, step, 0, p.action_std, ny, nx, nblk, nhave);
-  if (p.action_kind == 0) {
+  if (cr_action_kind<SPEC>(p) == 0) {
     my = a0 + ny;
     mx = a1 + nx;
   } else {
@@ -477,7 +487,7 @@ __device__ __forceinline__ StepOut crooms_env_step(const CrDev& p, const uint8_t
   }
   // _apply_action (crooms.py:300-331)
   double py, px;
-  if (p.use_velocity) {
+  if (cr_velocity<SPEC>(p)) {
     vy = fmin(fmax(vy + my, -MAX_VELOCITY), MAX_VELOCITY);
     vx = fmin(fmax(vx + mx, -MAX_VELOCITY), MAX_VELOCITY);
     py = ay + vy;
@@ -507,8 +517,8 @@ __device__ __forceinline__ StepOut crooms_env_step(const CrDev& p, const uint8_t
   }
   // reward / termination (crooms.py:289-297)
   // the goal square's centre (a fixed goal's from the kernel arguments: uniform, no per-env conversion)
-  const double gyc = p.goal_fixed ? p.gcy : (double)(int16_t)(g & 0xFFFF) + 0.5;
-  const double gxc = p.goal_fixed ? p.gcx : (double)(int16_t)(g >> 16) + 0.5;
+  const double gyc = cr_goal_fixed<SPEC>(p) ? p.gcy : (double)(int16_t)(g & 0xFFFF) + 0.5;
+  const double gxc = cr_goal_fixed<SPEC>(p) ? p.gcx : (double)(int16_t)(g >> 16) + 0.5;
   const double dy = ay - gyc, dx = ax - gxc;
   const double s = dy * dy + dx * dx;
   o.term = s <= p.s_thr ? 1 : 0;
@@ -521,8 +531,8 @@ __device__ __forceinline__ StepOut crooms_env_step(const CrDev& p, const uint8_t
     lens += (uint32_t)el;
     el = 0;
     if constexpr (!DEFER) {
-      if (p.action_kind == 0) draw_ints<REPLAY>(p, env, step, d);
-      reset_env(p, lds, d, ay, ax, vy, vx, g);
+      if (cr_action_kind<SPEC>(p) == 0) draw_ints<REPLAY>(p, env, step, d);
+      reset_env<SPEC>(p, lds, d, ay, ax, vy, vx, g);
     }
   }
   return o;
@@ -555,7 +565,7 @@ __device__ void cr_metrics(const CrDev& p, float rsum, uint32_t eps, uint32_t le
 }
 
 // ---- the rollout kernel: K steps for every env; 2 consecutive envs per thread ----
-template <int OK, bool REPLAY>
+template <int OK, bool REPLAY, int SPEC = 0>
 __global__ __launch_bounds__(TPB, GP_CR_WAVES) void crooms_rollout(CrDev p, int K, uint64_t step0, const void* __restrict__ act,
                                                       void* __restrict__ obs, float* __restrict__ rew,
                                                       uint8_t* __restrict__ term, uint8_t* __restrict__ trunc) {
@@ -575,9 +585,9 @@ __global__ __launch_bounds__(TPB, GP_CR_WAVES) void crooms_rollout(CrDev p, int 
       const bool live = env < p.B;
       ay[i] = live ? p.ay[env] : 0.5;
       ax[i] = live ? p.ax[env] : 0.5;
-      vy[i] = (live && p.use_velocity) ? p.vy[env] : 0.0;
-      vx[i] = (live && p.use_velocity) ? p.vx[env] : 0.0;
-      g[i] = live ? (p.goal_fixed ? ((uint32_t)(p.goal_y & 0xFFFF) | ((uint32_t)(p.goal_x & 0xFFFF) << 16))
+      vy[i] = (live && cr_velocity<SPEC>(p)) ? p.vy[env] : 0.0;
+      vx[i] = (live && cr_velocity<SPEC>(p)) ? p.vx[env] : 0.0;
+      g[i] = live ? (cr_goal_fixed<SPEC>(p) ? ((uint32_t)(p.goal_y & 0xFFFF) | ((uint32_t)(p.goal_x & 0xFFFF) << 16))
                                   : p.goal[env])
                   : 0u;
       el[i] = live ? p.el[env] : 0;
@@ -589,8 +599,8 @@ __global__ __launch_bounds__(TPB, GP_CR_WAVES) void crooms_rollout(CrDev p, int 
       const bool full = env0 + EPT - 1 < p.B && (off & 1) == 0;  // pair-aligned rew / flag stores
 #pragma unroll
       for (int i = 0; i < EPT; ++i) { a0[i] = a1[i] = 0.0; ad[i] = 0; }
-      if (p.action_kind == 0) {
-        if (p.action_f64) {
+      if (cr_action_kind<SPEC>(p) == 0) {
+        if (cr_action_f64<SPEC>(p)) {
           const double* A = (const double*)act + 2 * (off + env0);
 #pragma unroll
           for (int i = 0; i < EPT; ++i)
@@ -630,7 +640,7 @@ __global__ __launch_bounds__(TPB, GP_CR_WAVES) void crooms_rollout(CrDev p, int 
       for (int i = 0; i < EPT; ++i) {
         const int env = env0 + i;
         const bool live = env < p.B;
-        StepOut o = crooms_env_step<REPLAY>(p, lds, env, live, step0 + (uint64_t)k, a0[i], a1[i], ad[i], ay[i], ax[i],
+        StepOut o = crooms_env_step<REPLAY, false, SPEC>(p, lds, env, live, step0 + (uint64_t)k, a0[i], a1[i], ad[i], ay[i], ax[i],
                                             vy[i], vx[i], g[i], el[i], rsum, eps, lens);
         r[i] = o.rew;
         tm[i] = o.term;
@@ -645,9 +655,9 @@ __global__ __launch_bounds__(TPB, GP_CR_WAVES) void crooms_rollout(CrDev p, int 
         for (int i = 0; i < EPT; ++i)
           if (env0 + i < p.B) { rew[off + env0 + i] = r[i]; term[off + env0 + i] = tm[i]; trunc[off + env0 + i] = tr[i]; }
       }
-      const size_t ob = (size_t)k * p.B * (size_t)p.obs_width * (OK == GP_OBS_F32 ? (p.obs_f64 ? 8 : 4)
+      const size_t ob = (size_t)k * p.B * (size_t)p.obs_width * (OK == GP_OBS_F32 ? ((SPEC == 0 && p.obs_f64) ? 8 : 4)
                                                                    : (OK == GP_OBS_HANSEN || OK == GP_OBS_TABLE ? 4 : 1));
-      if (OK == GP_OBS_F32 && !p.obs_f64 && p.obs_width == 2 && full) {
+      if (OK == GP_OBS_F32 && (SPEC == 1 || !p.obs_f64) && p.obs_width == 2 && full) {
         // vector_mdp (configs[4]): both envs' float32 (y, x) in one 16-B store
         *reinterpret_cast<float4*>((float*)((uint8_t*)obs + ob) + 2 * (size_t)env0) =
             make_float4((float)ay[0], (float)ax[0], (float)ay[1], (float)ax[1]);
@@ -663,8 +673,8 @@ __global__ __launch_bounds__(TPB, GP_CR_WAVES) void crooms_rollout(CrDev p, int 
       if (env >= p.B) continue;
       p.ay[env] = ay[i];
       p.ax[env] = ax[i];
-      if (p.use_velocity) { p.vy[env] = vy[i]; p.vx[env] = vx[i]; }
-      if (!p.goal_fixed) p.goal[env] = g[i];
+      if (cr_velocity<SPEC>(p)) { p.vy[env] = vy[i]; p.vx[env] = vx[i]; }
+      if (!cr_goal_fixed<SPEC>(p)) p.goal[env] = g[i];
       p.el[env] = el[i];
     }
   }
@@ -1999,6 +2009,12 @@ struct CRoomsBackend : EnvBackend {
     GP_HIP_CHECK(hipGetLastError());
     return GP_OK;
   }
+  // the configuration crooms_rollout<GP_OBS_F32, false, 1> is compiled for (cr_action_kind & co.)
+  bool generic = false;  // gp_debug_set("generic_kernels") at creation
+  bool spec1() const {
+    return !generic && d.obs_kind == GP_OBS_F32 && !d.obs_f64 && d.action_kind == 0 && !d.action_f64 && !d.use_velocity &&
+           d.goal_fixed;
+  }
   CrDev dev_for_launch() const {
     CrDev dd = d;
     dd.rp_u = rp_u;
@@ -2075,6 +2091,9 @@ struct CRoomsBackend : EnvBackend {
       if (rep)
         hipLaunchKernelGGL((crooms_rollout<OK, true>), dim3(grid), dim3(TPB), d.tab_bytes, s, dd, K, st, act, obs,
                            rew, term, trunc);
+      else if (OK == GP_OBS_F32 && spec1())  // configs[4]'s shape, compiled for it
+        hipLaunchKernelGGL((crooms_rollout<GP_OBS_F32, false, 1>), dim3(grid), dim3(TPB), d.tab_bytes, s, dd, K, st,
+                           act, obs, rew, term, trunc);
       else
         hipLaunchKernelGGL((crooms_rollout<OK, false>), dim3(grid), dim3(TPB), d.tab_bytes, s, dd, K, st, act, obs,
                            rew, term, trunc);
@@ -2153,6 +2172,7 @@ static double sq_threshold(double thr) {
 }
 
 int CRoomsBackend::build(const gp_crooms_config* cfg) {
+  generic = gp_debug_knobs().generic_kernels != 0;
   static const int DY8[8] = {-1, -1, 0, 1, 1, 1, 0, -1}, DX8[8] = {0, 1, 1, 1, 0, -1, -1, -1};
   const int H = cfg->height, W = cfg->width, nc = H * W;
   if (H < 3 || W < 3 || nc >= 32768 || !cfg->cells) {

@@ -28,6 +28,8 @@ struct GpDebugKnobs {
   int disable_fused = 0, no_staging = 0, xmode = 1, fault_block = -1;
   int fused_tile = 0;       // GRID fused kernel: envs per tile (512 / 1024 / 2048); 0 = chosen by size
   uint32_t spin_limit = 0;  // 0 = the kernel's default
+  int generic_kernels = 0;  // CROOMS: 1 = never the compile-time-specialised philox rollout (A/B and parity tests)
+  int no_spw = 0;           // GRID fused kernel: 1 = no speculative word windows (A/B and parity tests)
 };
 const GpDebugKnobs& gp_debug_knobs();
 

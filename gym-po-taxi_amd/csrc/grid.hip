@@ -42,6 +42,7 @@ struct alignas(64) GridCtl {
   uint32_t err;                         // bit0: spin timeout
   uint32_t b_total;                     // resets resolved by the last K2 (diagnostic)
   uint32_t step;                        // numpy-mode steps taken (fused-kernel granule tags)
+  uint32_t fb_last;                     // fused kernel: reset words b of the last step (next launch's window centre)
 };
 
 // Per-block metric accumulators (each persistent block owns one slot: no atomics).
@@ -110,6 +111,7 @@ struct GridDev {
   int32_t xmode;            // fused exchange: 0 = block-0 aggregator + per-tile words, 1 = all-gather
   uint32_t spin_limit;      // polls before a cross-block wait gives up and flags GridCtl::err
   int32_t fault_block;      // test knob (GP_FAULT_BLOCK): this block never publishes (forces the timeout); -1 off
+  int32_t spw_on;           // staged fused kernel: the store waves precompute speculative word windows (SPW_*)
   // philox / replay
   uint32_t key0, key1;
   const uint64_t* rp_u;
@@ -907,6 +909,18 @@ constexpr int LDS_TABLE_BUDGET = 96 * 1024;
 // Output staging (scalar obs kinds, <= 2 tiles per block): per tile obs int32[FEPB], reward f32[FEPB],
 // terminated u8[FEPB], truncated u8[FEPB], in dynamic LDS after the tables.
 constexpr int STG_TILE_BYTES = FEPB * 10;
+// Speculative word windows of the staged fused kernel. A step's resetter words sit at stream positions that are
+// only known once the all-gather has delivered the tile prefixes; but the words themselves depend only on the
+// post-random(B) state SB, known at the step's start. So while the exchange is in flight the (otherwise idle) store
+// waves evaluate, per tile, the u64 outputs of a window of SPW_NJ draws centred on the tile's predicted position
+// (the previous step's reset total b spread over the tiles in proportion), and SPW_NU candidates for the next
+// step's state J_used(SB) and J_used's coefficients centred on the predicted used = b / 2. After the gather the
+// control wave reads its resetters' words and J_used from LDS instead of evaluating two dependent radix-256 jumps
+// per lane; lanes whose position falls outside a window (or a window not ready) take the jump path as before.
+constexpr int SPW_NJ = 384;  // u64 draws per tile window (768 words: +-4 sigma of the prefix prediction at 1M envs)
+constexpr int SPW_NU = 256;  // next-state candidates (+-128 u64 draws around the predicted J_used)
+constexpr int SPW_CAND_U64 = 6;  // a_hi, a_lo, c_hi, c_lo, s_hi, s_lo
+__host__ __device__ constexpr int spw_bytes(int qpt) { return (qpt * SPW_NJ + SPW_NU * SPW_CAND_U64) * 8; }
 constexpr int R_ENV = 0, R_CTRL = 1, R_PASS = 2;  // fused_resets roles: env wave, control wave, store wave
 template <int OK, int QPT>
 constexpr bool fused_staged() { return QPT <= 2 && (OK == GP_OBS_HANSEN || OK == GP_OBS_TABLE); }
@@ -962,6 +976,11 @@ struct FusedShared {
   uint32_t drawn;                // the control wave drew this step's resetter cells before B2
   uint32_t rdone;                // env waves done listing their resetters in renv (monotone)
   int32_t dof[8];                // goal-direction cell offsets (Hansen goal multiplier)
+  uint64_t spw_sb[2];            // SPW: this step's post-random(B) state (control wave, before B1)
+  uint32_t spw_h0, spw_b;        // SPW: has_uint32 at the step start, the previous step's reset words
+  uint32_t spw_done;             // SPW: store waves done with their windows (monotone, FSTW per step)
+  uint32_t spw_n0[FMAXQ];        // SPW: first draw number of each tile's window (0: no window)
+  uint32_t spw_u0;               // SPW: first candidate's used
   uint16_t renv[2][FEPB];        // STG: env (in tile) of resetter rank r of tile q
   uint32_t pos[FEPB];            // slow path: accepted-word positions of one tile's resetters
   uint32_t pos2[FEPB];
@@ -1307,8 +1326,15 @@ __device__ __forceinline__ void stage_reset_obs_r(const GridDev& p, const LTabs&
 template <int OK, int QPT, bool STG>
 __device__ __forceinline__ void ctrl_fast_finish(const GridDev& p, FusedShared& sh, const LTabs& tb, const u128 SB,
                                                  const Stream& st, uint32_t b, uint32_t tq, uint32_t pre, char* stg,
-                                                 const int (&dof)[8]) {
+                                                 const int (&dof)[8], const uint64_t* spw = nullptr, int kstamp = 64) {
   const int lane = threadIdx.x & 63;
+  // SPW (spw != nullptr: the store waves' windows for this step are complete): the windows' bases
+  uint32_t sn0[QPT], su0 = 0xFFFFFFFFu;
+  if (spw) {
+#pragma unroll
+    for (int q = 0; q < QPT; ++q) sn0[q] = sh.spw_n0[q];
+    su0 = sh.spw_u0;
+  }
   const bool rgoal = p.fixed_goal < 0;
   const uint32_t nsel = rgoal ? (uint32_t)p.n_goal_valid : (uint32_t)p.n_agent_valid;
   uint32_t tc[QPT], P[QPT], cum[QPT + 1];
@@ -1342,21 +1368,51 @@ __device__ __forceinline__ void ctrl_fast_finish(const GridDev& p, FusedShared& 
     const bool buffered = st.h0 && w == 0;  // numpy's buffered half-word
     const uint32_t ww = w - st.h0;
     const uint32_t n = extra ? used : (cellj && !buffered ? (ww >> 1) + 1u : 0u);
-    const PcgJump jlo = t8[n & 255u], jhi = t8[256u + ((n >> 8) & 255u)];
     // the env slot of this resetter (STG), loaded alongside the jump tables, off the dependent chain
     const int slot = STG ? (int)sh.renv[q][min(r, (uint32_t)FEPB - 1u)] : 0;
-    PcgJump J1 = jlo, J2 = jhi;
-    u128 X0 = SB;
-    if (extra && lane == 61) {
-      J1 = PcgJump{0, 1, 0, 0};
-      J2.c_hi = 0; J2.c_lo = 0;
-      X0 = mk128(jlo.a_hi, jlo.a_lo);
-    } else if (extra && lane == 62) {
-      J1 = PcgJump{0, 1, 0, 0};
-      X0 = mk128(jlo.c_hi, jlo.c_lo);
+    u128 X = 0;
+    uint64_t x = 0;
+    bool have = false, xout = false;  // X (and x) from a window: no jump
+    if (spw) {
+      if (extra) {
+        const uint32_t d = used - su0;
+        if (d < (uint32_t)SPW_NU) {
+          const uint64_t* c = spw + QPT * SPW_NJ + (size_t)d * SPW_CAND_U64 + (lane == 61 ? 0 : (lane == 62 ? 2 : 4));
+          X = mk128(c[0], c[1]);
+          have = true;
+        }
+      } else if (!cellj || buffered) {
+        have = xout = true;  // nothing to jump
+      } else {
+        const uint32_t d = n - sn0[q];
+        if (sn0[q] && d < (uint32_t)SPW_NJ) {
+          x = spw[q * SPW_NJ + d];
+          have = xout = true;
+        }
+      }
     }
-    const u128 X = apply_jump(J2, apply_jump(J1, X0));
-    const uint64_t x = pcg_output(X);
+    if (!have) {  // a lane outside the windows (or no windows): the two dependent radix-256 jumps
+      const PcgJump jlo = t8[n & 255u], jhi = t8[256u + ((n >> 8) & 255u)];
+      PcgJump J1 = jlo, J2 = jhi;
+      u128 X0 = SB;
+      if (extra && lane == 61) {
+        J1 = PcgJump{0, 1, 0, 0};
+        J2.c_hi = 0; J2.c_lo = 0;
+        X0 = mk128(jlo.a_hi, jlo.a_lo);
+      } else if (extra && lane == 62) {
+        J1 = PcgJump{0, 1, 0, 0};
+        X0 = mk128(jlo.c_hi, jlo.c_lo);
+      }
+      X = apply_jump(J2, apply_jump(J1, X0));
+    }
+    if (!xout) x = pcg_output(X);
+#ifdef GP_STAMPS
+    if (it == 0 && kstamp < 64) {  // stamps slot 15: the first pass's jumps are done (diagnostic build only)
+      unsigned long long t_;
+      asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_) : "v"(x) : "memory");
+      if (lane == 0) p.dbg[((size_t)blockIdx.x * 64 + kstamp) * 16 + 15] = t_;
+    }
+#endif
     if (cellj) {
       const uint32_t word = buffered ? st.u0 : ((ww & 1u) ? (uint32_t)(x >> 32) : (uint32_t)x);
       const uint32_t v = lemire_value(word, nsel);
@@ -1685,7 +1741,10 @@ __device__ __forceinline__ void fused_env(const GridDev& p_in, FusedShared& sh, 
     if (tid < NA * NA) const_cast<uint64_t*>(s_thr)[tid] = GP_TRIMS ? thr_on_u64(p.thr[tid]) : p.thr[tid];
     if (tid < 4) sh.jB[tid] = (&p.fjB->a_hi)[tid];
     if (tid < 8) sh.dof[tid] = (OK == GP_OBS_HANSEN && p.doff && tid < p.obs_dirs) ? p.doff[tid] : 0x7FFFFFFF;
-    if (tid == 0) sh.rdone = 0;
+    if (tid == 0) {
+      sh.rdone = 0;
+      sh.spw_done = 0;
+    }
     lds_image_copy_range(dyn, p.limg, 0, p.lds.jt.off, tid, FENVW * 64);
     __syncthreads();
     LSTAMP(1);
@@ -2006,6 +2065,7 @@ __device__ __forceinline__ void fused_ctrl(const GridDev& p_in, FusedShared& sh,
   st.U0 = (uint32_t)p.B;
   const uint32_t step_base = C->step;
   const PcgJump jB = *p.fjB;
+  uint32_t bprev = C->fb_last;  // SPW: the reset words of the previous step (window centres)
   // lane l checks tile q = 2c + (l >> 5); lane ll = l & 31 holds u64 #(tau*31 - 1 + ll) of the
   // post-random(B) stream, i.e. jump(s0, B + tau*31 + ll)
   u128 CS[NC];
@@ -2053,6 +2113,12 @@ __device__ __forceinline__ void fused_ctrl(const GridDev& p_in, FusedShared& sh,
     }
     const uint32_t wrej = __any((int)crej) ? 1u : 0u;
     const u128 SB = apply_jump(jB, st.s0);  // state after random(B): base of the word stream
+    if (STG && p.spw_on && lane == 0) {  // what the store waves build this step's windows from (after B1)
+      sh.spw_sb[0] = hi64(SB);
+      sh.spw_sb[1] = lo64(SB);
+      sh.spw_h0 = st.h0;
+      sh.spw_b = bprev;
+    }
     lds_barrier();  // B1
     // ---- 2. publish this block's granule ----
     uint32_t tq = 0;
@@ -2150,8 +2216,16 @@ __device__ __forceinline__ void fused_ctrl(const GridDev& p_in, FusedShared& sh,
         __builtin_amdgcn_s_sleep(1);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
     }
+    bprev = b;
+    if (lane == 0) RSTAMP(14);
     if (drawn) {
-      ctrl_fast_finish<OK, QPT, STG>(p, sh, tb, SB, st, b, tq, mypre, stg, cdof);  // cells + next state, before B2
+      const uint64_t* spw = nullptr;  // the store waves' windows, if complete (never waited for)
+      if (STG && p.spw_on &&
+          __hip_atomic_load(&sh.spw_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= (uint32_t)FSTW * (k + 1)) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+        spw = reinterpret_cast<const uint64_t*>(stg + QPT * STG_TILE_BYTES);
+      }
+      ctrl_fast_finish<OK, QPT, STG>(p, sh, tb, SB, st, b, tq, mypre, stg, cdof, spw, k);  // cells + next state, before B2
     } else if (known) {
       publish_next(tb, sh, SB, ncalls ? b : 0u, st.h0, st.u0, lane == 0);
     }
@@ -2184,6 +2258,7 @@ __device__ __forceinline__ void fused_ctrl(const GridDev& p_in, FusedShared& sh,
     C->has_u32 = st.h0;
     C->uinteger = st.u0;
     C->step = step_base + (uint32_t)K;
+    C->fb_last = bprev;
   }
 }
 
@@ -2282,6 +2357,56 @@ __device__ __forceinline__ void fused_idle(const GridDev& p, FusedShared& sh, co
   }
 }
 
+// SPW: the store waves' windows for this step (after B1, while the exchange is in flight; see SPW_NJ). 128
+// lanes: 3 consecutive draws of each tile window and 2 next-state candidates each.
+template <int QPT>
+__device__ __forceinline__ void spw_fill(const GridDev& p, FusedShared& sh, const LTabs& tb, uint64_t* spw, int sl,
+                                         const u128 inc) {
+  const int G = (int)gridDim.x, nt = p.fnt;
+  const u128 SB = mk128(sh.spw_sb[0], sh.spw_sb[1]);
+  const uint32_t h0 = sh.spw_h0, bp = sh.spw_b;
+  const PcgJump* t8 = tb.jt8();
+#pragma unroll
+  for (int q = 0; q < QPT; ++q) {
+    const int tau = q * G + (int)blockIdx.x;
+    uint32_t n0 = 0;
+    if (tau < nt) {
+      // predicted first word of the tile (b spread over the tiles in proportion) plus half its expected count
+      const uint32_t cw = (uint32_t)(((uint64_t)bp * (uint32_t)tau) / (uint32_t)nt) + bp / (2u * (uint32_t)nt);
+      const uint32_t cn = ((cw > h0 ? cw - h0 : 0u) >> 1) + 1u;  // its u64 draw number
+      n0 = cn > (uint32_t)SPW_NJ / 2 ? cn - (uint32_t)SPW_NJ / 2 : 1u;
+      if (n0 + (uint32_t)SPW_NJ > 65536u) n0 = 0;  // beyond the radix-256 jumps: no window
+    }
+    if (n0) {
+      const uint32_t n = n0 + 3u * (uint32_t)sl;
+      u128 X = apply_jump(t8[256u + (n >> 8)], apply_jump(t8[n & 255u], SB));
+      uint64_t* w = spw + q * SPW_NJ + 3 * sl;
+      w[0] = pcg_output(X);
+      X = pcg_step(X, inc);
+      w[1] = pcg_output(X);
+      X = pcg_step(X, inc);
+      w[2] = pcg_output(X);
+    }
+    if (sl == 0) sh.spw_n0[q] = n0;
+  }
+  uint32_t up, hp;
+  words_to_draws(bp, h0, up, hp);
+  const uint32_t u0 = up > (uint32_t)SPW_NU / 2 ? up - (uint32_t)SPW_NU / 2 : 0u;
+  if (u0 + (uint32_t)SPW_NU <= 65536u) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const uint32_t u = u0 + 2u * (uint32_t)sl + (uint32_t)i;
+      const PcgJump J = compose_jump(t8[256u + (u >> 8)], t8[u & 255u]);
+      const u128 x = apply_jump(J, SB);
+      uint64_t* c = spw + QPT * SPW_NJ + (size_t)(u - u0) * SPW_CAND_U64;
+      c[0] = J.a_hi; c[1] = J.a_lo; c[2] = J.c_hi; c[3] = J.c_lo; c[4] = hi64(x); c[5] = lo64(x);
+    }
+  }
+  if (sl == 0) sh.spw_u0 = u0 + (uint32_t)SPW_NU <= 65536u ? u0 : 0xFFFFFFFFu;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  if ((sl & 63) == 0) __hip_atomic_fetch_add(&sh.spw_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // The store waves of the fused kernel. They take part in every block barrier (fused_resets role
 // R_PASS) and, with STG, move step k's staged outputs from LDS to HBM right after step k's resets,
 // i.e. while the env waves advance and run step k+1's VALU-bound transitions, so that the outputs'
@@ -2301,6 +2426,7 @@ __device__ __forceinline__ void fused_store(const GridDev& p, FusedShared& sh, c
   int32_t dov[QPT][4];
   const uint32_t dc[QPT] = {};
   (void)dov;
+  const u128 inc = mk128(p.ctl->inc_hi, p.ctl->inc_lo);
   if constexpr (GP_PRO2) {
     __syncthreads();  // the prologue barrier; then the PCG jump tables behind the first step's transitions
     lds_image_copy_range(const_cast<char*>(tb.dyn), p.limg, p.lds.jt.off, p.lds.total, sl, FSTW * 64);
@@ -2309,6 +2435,10 @@ __device__ __forceinline__ void fused_store(const GridDev& p, FusedShared& sh, c
     const uint32_t tag0 = (step_base + (uint32_t)k + 1u) * 4u;
     uint64_t* slots = p.fslot + (size_t)((step_base + (uint32_t)k) & 1u) * 3 * G;
     lds_barrier();  // B1
+    if constexpr (STG) {
+      if (p.spw_on) spw_fill<QPT>(p, sh, tb, reinterpret_cast<uint64_t*>(const_cast<char*>(stg) + QPT * STG_TILE_BYTES),
+                                  sl, inc);
+    }
     lds_barrier();  // B2
     fused_resets<OK, QPT, R_PASS>(p, sh, tb, st, (u128)0, jB, slots, tag0, du, di, dc, dc, du, dp);
     if constexpr (STG) {
@@ -2599,6 +2729,7 @@ struct GridBackend : EnvBackend {
     if (!strcmp(key, "fused_blocks")) *v = fused_G;
     else if (!strcmp(key, "fused_tiles_per_block")) *v = fused_qpt;
     else if (!strcmp(key, "fused_staged")) *v = fused_stg ? 1 : 0;
+    else if (!strcmp(key, "fused_spw")) *v = d.spw_on;
     else if (!strcmp(key, "fused_tile_envs")) *v = d.ftile;
     else return EnvBackend::query(key, v);
     return GP_OK;
@@ -2645,7 +2776,8 @@ struct GridBackend : EnvBackend {
 #endif
   template <int OK, int QPT, bool STG>
   void launch_fused_qs(int K, const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc, hipStream_t s) {
-    const size_t lds = (size_t)d.lds.total + (STG ? (size_t)QPT * STG_TILE_BYTES : 0);
+    const size_t lds = (size_t)d.lds.total +
+                       (STG ? (size_t)QPT * STG_TILE_BYTES + (d.spw_on ? (size_t)spw_bytes(QPT) : 0) : 0);
     // SMALL: tiles of 512 / 1024 envs (runtime size, idle env waves); only with <= 2 tiles per block
     if constexpr (QPT <= 2) {
       if (d.ftile != FEPB) {
@@ -3255,6 +3387,14 @@ int GridBackend::build(const gp_grid_config* cfg) {
         GP_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
             &occ2, grid_rollout_numpy<GP_OBS_HANSEN, 2, 8, true, false>, FTPB, d.lds.total + 2 * STG_TILE_BYTES));
         fused_stg = occ2 >= 1;
+        // SPW windows (one reset call per step: the fast cell draw) when they fit beside the staging area
+        if (fused_stg && (d.fixed_goal < 0) != (d.fixed_agent < 0) && !dbg.no_spw) {
+          int occ3 = 0;
+          GP_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+              &occ3, grid_rollout_numpy<GP_OBS_HANSEN, 2, 8, true, false>, FTPB,
+              d.lds.total + 2 * STG_TILE_BYTES + spw_bytes(2)));
+          d.spw_on = occ3 >= 1;
+        }
       }
     }
   }

@@ -266,7 +266,8 @@ int gp_profile_read_resolver(gp_env* env, double* total_ms, int64_t* n_launches)
  *   env waves store outputs directly), "xmode" (fused exchange variant, default 1), "spin_limit" (polls
  *   before a cross-block wait gives up, 0 = default), "fault_block" (this block never publishes: forces
  *   the timeout path; -1 = off), "fused_tile" (GRID fused kernel envs per tile: 512, 1024 or 2048; 0 = by
- *   size). gp_debug_reset restores the defaults. Unknown key: GP_E_INVALID. */
+ *   size), "no_spw" (GRID fused kernel: 1 = no speculative word windows), "generic_kernels" (CROOMS: 1 = the generic philox rollout even where a compile-time-specialised one
+ *   exists). gp_debug_reset restores the defaults. Unknown key: GP_E_INVALID. */
 int gp_debug_set(const char* key, int64_t value);
 void gp_debug_reset(void);
 

@@ -69,14 +69,21 @@ def _check_chunks(env, ora, chunks, action_seed, n_act):
     np.testing.assert_array_equal(e, ora.elapsed)
 
 
-# (1, 4, 20): bench.py's driver sequence (two warmup launches of 1 and W - 1 = 4 steps, then the timed 20)
-@pytest.mark.parametrize("chunks,time_limit", [((20, 128), 500), ((128, 7), 500), ((20, 20), 20), ((1, 4, 20), 500)])
-def test_bench_kernel_staged_k_step_launches_bit_exact(chunks, time_limit, gpu_device):
+# (1, 4, 20): bench.py's driver sequence (two warmup launches of 1 and W - 1 = 4 steps, then the timed 20).
+# spw: the store waves' speculative word windows (the bench path; SPW_NJ in csrc/grid.hip) on, or forced off. The
+# first steps after a reset use windows centred on a stale reset total (lanes outside them take the jump path),
+# time_limit=20 puts mass resets far outside every window.
+@pytest.mark.parametrize("chunks,time_limit,spw", [((20, 128), 500, 1), ((128, 7), 500, 1), ((20, 20), 20, 1),
+                                                   ((1, 4, 20), 500, 1), ((1, 4, 20), 500, 0)])
+def test_bench_kernel_staged_k_step_launches_bit_exact(chunks, time_limit, spw, gpu_device):
     from gym_po_amd import MultistoryFourRoomsEnv
-    env = MultistoryFourRoomsEnv(B_BENCH, grid_z=1, obs_type="hansen", time_limit=time_limit, device=gpu_device)
+    from gym_po_amd._lib import debug_knobs
+    with debug_knobs(no_spw=1 - spw):
+        env = MultistoryFourRoomsEnv(B_BENCH, grid_z=1, obs_type="hansen", time_limit=time_limit, device=gpu_device)
     G, q, stg, tile = _staged_geometry(env)
     if G * q * tile != B_BENCH or not stg:
         pytest.skip(f"this GPU does not give the bench geometry (G={G}, tiles/block={q}, staged={stg})")
+    assert env.query("fused_spw") == spw
     ora = gridworld.FourRoomsOracle(B_BENCH, 1, obs_type="hansen", time_limit=time_limit)
     o_g = _reset_obs(env, 2024)
     np.testing.assert_array_equal(o_g.astype(np.int64), np.asarray(ora.reset_seed(2024)).astype(np.int64))

@@ -171,6 +171,30 @@ def test_philox_rollout_equals_single_steps(gpu_device):
         assert torch.equal(x, y)
 
 
+@pytest.mark.parametrize("B,K", [(1 << 21, 16), (100003, 9)])
+def test_philox_specialised_kernel_equals_generic(B, K, gpu_device):
+    """configs[4]'s shape (continuous float32 actions, vector_mdp, fixed goal, no velocity) runs a compile-time
+    specialised philox rollout (crooms_rollout<GP_OBS_F32, false, 1>); the generic kernel (forced by the
+    `generic_kernels` debug knob) must produce the same outputs and state bit for bit, at the config size and on
+    a ragged size."""
+    import torch
+    from gym_po_amd._lib import debug_knobs
+    kw = {"obs_type": "vector_mdp"}
+    a = make_env(kw, B)
+    with debug_knobs(generic_kernels=1):
+        b = make_env(kw, B)
+    a.reset(seed=21)
+    b.reset(seed=21)
+    acts = torch.rand((K, B, 2), device=gpu_device) * 2 - 1
+    for x, y in zip(a.rollout(acts), b.rollout(acts)):
+        assert torch.equal(x, y)
+    for x, y in zip(a.get_state(), b.get_state()):
+        assert torch.equal(x, y)
+    ma, mb = a.metrics(), b.metrics()
+    assert {k: v for k, v in ma.items() if k != "return_sum"} == {k: v for k, v in mb.items() if k != "return_sum"}
+    assert ma["return_sum"] == pytest.approx(mb["return_sum"], rel=1e-6)
+
+
 def test_philox_action_noise_law(gpu_device):
     """Zero actions from cell centres far from walls: the displacement is the action noise N(0, 0.2)."""
     import torch

@@ -63,6 +63,15 @@ case "$task" in
   stamps)
     run 120 $O/stamps.log python tools/stamps.py ${1:-1048576} ${2:-128}
     grep -v amdgpu.ids $O/stamps.log ;;
+  knobab)  # in-call A/B of gp_debug_set knob sets on one library: bash tools/gpu.sh knobab "no_spw=0 no_spw=1" [B K..]
+    SETS=$1
+    shift
+    for rep in 1 2; do
+      for S in $SETS; do
+        GP_KNOBS=$S run 120 $O/lat_$S.log python -u tools/latency_probe.py ${@:-1048576 20 128}
+        echo "== $rep $S"; grep "B=" $O/lat_$S.log
+      done
+    done ;;
   ab)
     VARS=$1
     shift

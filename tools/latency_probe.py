@@ -58,7 +58,12 @@ def med(fn, reps=100):
 print(f"empty torch op + sync: median {med(lambda: x.add_(1))[0]:.1f} us", flush=True)
 from gym_po_amd import MultistoryFourRoomsEnv  # noqa: E402
 
-env = MultistoryFourRoomsEnv(B, grid_z=1, obs_type="hansen", device=dev)
+# GP_KNOBS="no_spw=1,..." : gp_debug_set knobs for the env (in-call A/B of kernel variants in one library)
+from gym_po_amd._lib import debug_knobs  # noqa: E402
+knobs = dict((kv.split("=")[0], int(kv.split("=")[1])) for kv in os.environ.get("GP_KNOBS", "").split(",") if kv)
+with debug_knobs(**knobs):
+    env = MultistoryFourRoomsEnv(B, grid_z=1, obs_type="hansen", device=dev)
+print(f"knobs {knobs}", flush=True)
 env.reset(seed=0)
 for K in Ks:
     acts = torch.randint(0, 4, (K, B), device=dev, dtype=torch.int32)
