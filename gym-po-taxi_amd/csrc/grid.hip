@@ -1324,7 +1324,7 @@ __device__ __forceinline__ void stage_reset_obs_r(const GridDev& p, const LTabs&
 }
 
 template <int OK, int QPT, bool STG>
-__device__ __forceinline__ void ctrl_fast_finish(const GridDev& p, FusedShared& sh, const LTabs& tb, const u128 SB,
+__device__ __forceinline__ uint32_t ctrl_fast_finish(const GridDev& p, FusedShared& sh, const LTabs& tb, const u128 SB,
                                                  const Stream& st, uint32_t b, uint32_t tq, uint32_t pre, char* stg,
                                                  const int (&dof)[8], const uint64_t* spw = nullptr, int kstamp = 64) {
   const int lane = threadIdx.x & 63;
@@ -1353,6 +1353,7 @@ __device__ __forceinline__ void ctrl_fast_finish(const GridDev& p, FusedShared& 
   // a_hi * a_lo (lane 61) and increment a_hi * c_lo + c_hi (lane 62), and s0' = J_used(SB) (lane 63),
   // so that the whole wave pays for one jump chain instead of four.
   constexpr uint32_t XL = 61;
+  uint32_t jumped = 0;  // some lane took the jump path (diagnostics)
   const uint32_t ncell = cum[QPT];
   const uint32_t npass = ncell <= XL ? 1u : 1u + (ncell - XL + 63u) / 64u;
   const PcgJump* t8 = tb.jt8();
@@ -1376,7 +1377,7 @@ __device__ __forceinline__ void ctrl_fast_finish(const GridDev& p, FusedShared& 
     if (spw) {
       if (extra) {
         const uint32_t d = used - su0;
-        if (d < (uint32_t)SPW_NU) {
+        if (su0 != 0xFFFFFFFFu && d < (uint32_t)SPW_NU) {  // (0xFFFFFFFF: the store waves built no candidates)
           const uint64_t* c = spw + QPT * SPW_NJ + (size_t)d * SPW_CAND_U64 + (lane == 61 ? 0 : (lane == 62 ? 2 : 4));
           X = mk128(c[0], c[1]);
           have = true;
@@ -1404,6 +1405,7 @@ __device__ __forceinline__ void ctrl_fast_finish(const GridDev& p, FusedShared& 
         X0 = mk128(jlo.c_hi, jlo.c_lo);
       }
       X = apply_jump(J2, apply_jump(J1, X0));
+      jumped = 1u;
     }
     if (!xout) x = pcg_output(X);
 #ifdef GP_STAMPS
@@ -1436,6 +1438,7 @@ __device__ __forceinline__ void ctrl_fast_finish(const GridDev& p, FusedShared& 
       }
     }
   }
+  return __any((int)jumped) ? 1u : 0u;
 }
 
 template <int OK, int QPT, bool STG>
@@ -2066,6 +2069,7 @@ __device__ __forceinline__ void fused_ctrl(const GridDev& p_in, FusedShared& sh,
   const uint32_t step_base = C->step;
   const PcgJump jB = *p.fjB;
   uint32_t bprev = C->fb_last;  // SPW: the reset words of the previous step (window centres)
+  uint32_t d_ready = 0, d_nojump = 0;  // GP_STAMPS diagnostics: steps with the windows ready / with no lane jumping
   // lane l checks tile q = 2c + (l >> 5); lane ll = l & 31 holds u64 #(tau*31 - 1 + ll) of the
   // post-random(B) stream, i.e. jump(s0, B + tau*31 + ll)
   u128 CS[NC];
@@ -2225,7 +2229,9 @@ __device__ __forceinline__ void fused_ctrl(const GridDev& p_in, FusedShared& sh,
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
         spw = reinterpret_cast<const uint64_t*>(stg + QPT * STG_TILE_BYTES);
       }
-      ctrl_fast_finish<OK, QPT, STG>(p, sh, tb, SB, st, b, tq, mypre, stg, cdof, spw, k);  // cells + next state, before B2
+      const uint32_t jmp = ctrl_fast_finish<OK, QPT, STG>(p, sh, tb, SB, st, b, tq, mypre, stg, cdof, spw, k);
+      d_ready += spw ? 1u : 0u;
+      d_nojump += jmp ? 0u : 1u;
     } else if (known) {
       publish_next(tb, sh, SB, ncalls ? b : 0u, st.h0, st.u0, lane == 0);
     }
@@ -2260,6 +2266,15 @@ __device__ __forceinline__ void fused_ctrl(const GridDev& p_in, FusedShared& sh,
     C->step = step_base + (uint32_t)K;
     C->fb_last = bprev;
   }
+#ifdef GP_STAMPS
+  if (lane == 0) {  // launch region slots 6, 7: steps with the SPW windows ready, steps where no lane jumped
+    p.dbg[(size_t)256 * 64 * 16 + (size_t)blockIdx.x * 8 + 6] = d_ready;
+    p.dbg[(size_t)256 * 64 * 16 + (size_t)blockIdx.x * 8 + 7] = d_nojump;
+  }
+#else
+  (void)d_ready;
+  (void)d_nojump;
+#endif
 }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));

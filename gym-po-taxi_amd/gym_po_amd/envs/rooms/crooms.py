@@ -7,9 +7,14 @@ with float32 (default) or float64 I/O.
 
 RNG: `"philox"` (default) draws the reference's laws from a counter-based generator (every env-step
 independent, full-chip kernels); `"numpy"` draws the reference's own PCG64 stream word for word (numpy's
-ziggurat normals and buffered Lemire choices, seed-identical with the reference; one workgroup resolves
-the data-dependent word counts, so it is meant for small batches, at most 2^20 envs); `"replay"` takes
-the reference stream's values per env (bit-exact parity tests).
+ziggurat normals and buffered Lemire choices, seed-identical with the reference; up to 4,096 envs one
+workgroup resolves the data-dependent word counts, above that every draw call is resolved over all of its
+stream positions by grid-wide kernels, at any size: ~2e9 env-steps/s at 2^21 envs, ~50x below philox);
+`"replay"` takes the reference stream's values per env (bit-exact parity tests).
+
+Philox-mode normals are Box-Muller on float32 hardware log2 / sqrt / sin / cos (a 53-bit u1, so the radius
+reaches 8.57 sigma), scaled in float64: the noise has float32 precision (~1e-7 relative) while the state is
+float64 -- the reference's law, not its values (csrc/crooms.hip box_muller_pair).
 
 Extra keyword arguments beyond the reference: `device`, `rng_mode`, `dtype` (torch.float32 (default)
 or torch.float64 for the continuous actions and observations).

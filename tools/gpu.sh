@@ -101,6 +101,24 @@ case "$task" in
     [ -x tools/mb_valu.bin ] && run 60 $O/mb_valu.txt tools/mb_valu.bin && cat $O/mb_valu.txt
     [ -n "$CRATE" ] && run 300 $O/crooms_rate.jsonl python3 tools/crooms_numpy_rate.py $CRATE && cat $O/crooms_rate.jsonl
     true ;;
+  final)  # round-end evidence on the committed build: suite + smoke, rocprof of the driver command, PMC, bench lines
+    R=${ROUND:-r03}
+    run 1000 $O/tests.log python -u -m pytest -x -v --timeout 300 --timeout-method thread tests -m gpu
+    tail -n 1 $O/tests.log
+    run 300 $O/smoke.log python -c "import __graft_entry__ as g; g.smoke()"
+    run 300 $O/prof.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o p -- python3 bench.py --no-cpu-baseline --steps 20 --warmup 5
+    cp $(find $O/prof -name "*kernel_stats.csv" | head -1) $O/driver_kernel_stats.csv
+    i=0
+    for C in FETCH_SIZE WRITE_SIZE; do
+      i=$((i+1))
+      run 300 $O/p$i.log rocprofv3 --pmc $C --output-format csv -d $O/pmc/p$i -o p -- python3 bench.py --no-cpu-baseline --steps 20 --warmup 5
+    done
+    python3 tools/pmc_to_json.py $O/pmc grid_rollout_numpy fourrooms_hansen4_B1048576_numpy $O/pmc.json fourrooms 20
+    cp $O/pmc.json profiles/${R}_pmc_fourrooms_hansen4_B1048576_numpy_K20.json
+    run 600 $O/bench_default.log python3 bench.py
+    last_json $O/bench_default.log 3000
+    run 300 $O/bench_driver.log python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline
+    last_json $O/bench_driver.log 3000 ;;
   multi)
     GP_BENCH_BACKEND=gloo run 300 $O/multi2.log python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
       --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 256 --warmup 128 --envs 262144 --no-cpu-baseline

@@ -22,11 +22,22 @@ steps_per_launch = float(sys.argv[6])
 vals = {"FETCH_SIZE": [], "WRITE_SIZE": []}
 for fn in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
     with open(fn) as f:
-        for row in csv.DictReader(f):
-            if pat in row.get("Kernel_Name", "") and row["Counter_Name"] in vals:
-                vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
+        rows = [r for r in csv.DictReader(f) if pat in r.get("Kernel_Name", "") and r["Counter_Name"] in vals]
+    rows.sort(key=lambda r: int(r.get("Dispatch_Id", 0) or 0))  # launch order (the same in every pass)
+    for r in rows:
+        vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
 if not vals["FETCH_SIZE"] or not vals["WRITE_SIZE"]:
     sys.exit(f"no FETCH_SIZE/WRITE_SIZE rows for {pat!r} under {root}")
+# A bench command launches a few shorter warmup chunks (1 and W - 1 steps) before its C-step launches: keep the
+# launches whose WRITE_SIZE is within 5% of the median (the C-step ones), and the same launches of the FETCH pass
+# (the passes run the same command, so launch i is the same launch in both).
+import statistics  # noqa: E402
+med = statistics.median(vals["WRITE_SIZE"])
+keep = [i for i, v in enumerate(vals["WRITE_SIZE"]) if abs(v - med) <= 0.05 * med]
+if len(vals["FETCH_SIZE"]) == len(vals["WRITE_SIZE"]):
+    vals = {k: [v[i] for i in keep] for k, v in vals.items()}
+else:
+    vals["WRITE_SIZE"] = [vals["WRITE_SIZE"][i] for i in keep]
 fetch_kib = sum(vals["FETCH_SIZE"]) / len(vals["FETCH_SIZE"])
 write_kib = sum(vals["WRITE_SIZE"]) / len(vals["WRITE_SIZE"])
 here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

@@ -50,6 +50,9 @@ L6 = raw[NS:].reshape(256, 8)[:G, 4:6] * 10
 print(f"  env prologue after the barrier: action rows done median {np.median(L6[:, 0] - L4[:, 1]):.0f} ns, lane "
       f"states ready median {np.median(L6[:, 1] - L4[:, 1]):.0f} ns (max over blocks {np.max(L6[:, 1] - t0)} ns from "
       f"first entry)")
+L7 = raw[NS:].reshape(256, 8)[:G, 6:8]
+print(f"  SPW: steps with the windows ready per block median {np.median(L7[:, 0]):.0f} of {K}, steps with no lane "
+      f"jumping median {np.median(L7[:, 1]):.0f} (min over blocks {L7[:, 1].min()})")
 st_k = a[:G, :min(K, 64), 0] * 10 - t0
 print("  step k start, max over blocks (ns from first entry), k = 0..7:", [int(x) for x in st_k.max(0)[:8]])
 env.set_profiling(True)
