@@ -12,6 +12,12 @@ for p in (ROOT, os.path.join(ROOT, "gym-po-taxi_amd"), os.path.join(ROOT, "tests
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (run via gpurun)")
     config.addinivalue_line("markers", "slow: longer CPU test")
+    config.addinivalue_line("markers", "gpu_first: runs before every other test (spawns GPU worker processes, which "
+                                       "is only allowed before this process initialises the GPU)")
+
+
+def pytest_collection_modifyitems(config, items):
+    items.sort(key=lambda it: 0 if it.get_closest_marker("gpu_first") else 1)  # stable: the rest keep their order
 
 
 @pytest.fixture(scope="session")
