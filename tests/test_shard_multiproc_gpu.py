@@ -42,9 +42,8 @@ def _worker(rank, world, port, out):
         dist.destroy_process_group()
 
 
-# Opt-in (GP_MULTIPROC_TEST=1) until it has passed on the GPU pool: written at the end of round 3 while no box was
-# obtainable, and a first test that fails would stop the whole `-x` GPU gate.
-@pytest.mark.skipif(os.environ.get("GP_MULTIPROC_TEST") != "1", reason="opt-in: GP_MULTIPROC_TEST=1")
+# Passed on the MI355X pool (profiles/r03_gpu_test_multiproc_shards.txt); GP_MULTIPROC_TEST=0 skips it.
+@pytest.mark.skipif(os.environ.get("GP_MULTIPROC_TEST") == "0", reason="disabled: GP_MULTIPROC_TEST=0")
 @pytest.mark.timeout(300)
 def test_two_processes_device_shards_gloo(tmp_path):
     import torch
