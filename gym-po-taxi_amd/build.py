@@ -6,6 +6,7 @@ hipcc cross-compiles without a GPU. Sources: csrc/*.hip (+ the C ABI header in i
 Rebuilds only when a source is newer than the library.
 """
 import glob
+import hashlib
 import os
 import subprocess
 import sys
@@ -43,7 +44,10 @@ def build(force=False, debug=False, verbose=True, stamps=False):
         flags.insert(0, "-DGP_STAMPS")
     if debug:
         flags.append("-g")
-    objdir = os.path.join(HERE, "build", "stamps" if stamps else ("debug" if debug else "release"))
+    # objects are keyed on the compiler and every flag (arch included): a changed GP_OFFLOAD_ARCH / HIPCC never
+    # links objects built for another target
+    key = hashlib.sha1(" ".join([hipcc] + flags).encode()).hexdigest()[:10]
+    objdir = os.path.join(HERE, "build", ("stamps" if stamps else ("debug" if debug else "release")) + "-" + key)
     os.makedirs(objdir, exist_ok=True)
 
     headers = [d for d in deps() if not d.endswith(".hip")]

@@ -32,6 +32,8 @@ const char* gp_derr_text(uint32_t flags) {
   if (flags & GP_DERR_TIMEOUT)
     strncat(buf, "a persistent kernel's cross-block wait timed out (blocks not co-resident?); ",
             sizeof(buf) - strlen(buf) - 1);
+  if (flags & GP_DERR_OVERFLOW)
+    strncat(buf, "more rejected choice() words in one step than the windowed kernel lists; ", sizeof(buf) - strlen(buf) - 1);
   if (flags & GP_DERR_STREAM)
     strncat(buf, "a numpy normal needed more words than one stream window holds; ", sizeof(buf) - strlen(buf) - 1);
   return buf;
@@ -210,6 +212,9 @@ int gp_debug_set(const char* key, int64_t value) {
   else if (!strcmp(key, "fused_tile")) g_dbg.fused_tile = (int)value;
   else if (!strcmp(key, "generic_kernels")) g_dbg.generic_kernels = value != 0;
   else if (!strcmp(key, "no_spw")) g_dbg.no_spw = value != 0;
+  else if (!strcmp(key, "no_wgrid")) g_dbg.no_wgrid = value != 0;
+  else if (!strcmp(key, "wg_halo")) g_dbg.wg_halo = (int)value;
+  else if (!strcmp(key, "wg_bias")) g_dbg.wg_bias = (int)value;
   else {
     gp_set_error("gp_debug_set: unknown key '%s'", key);
     return GP_E_INVALID;
@@ -376,6 +381,7 @@ int gp_plan_run(gp_plan* plan) {
     gp_set_error("gp_plan_run: null plan");
     return GP_E_INVALID;
   }
+  (void)hipSetDevice(plan->env->be->device);  // the env's device, whatever the calling thread's current one is
   return plan->env->be->rollout(plan->K, plan->act, plan->obs, plan->rew, plan->term, plan->trunc, plan->stream);
 }
 

@@ -30,6 +30,9 @@ struct GpDebugKnobs {
   uint32_t spin_limit = 0;  // 0 = the kernel's default
   int generic_kernels = 0;  // CROOMS: 1 = never the compile-time-specialised philox rollout (A/B and parity tests)
   int no_spw = 0;           // GRID fused kernel: 1 = no speculative word windows (A/B and parity tests)
+  int no_wgrid = 0;         // GRID: 1 = never the windowed kernel (wgrid.hip): the older fused kernel instead
+  int wg_halo = 0;          // GRID windowed kernel: window halo (256 or 512 draws); 0 = default
+  int wg_bias = 0;          // GRID windowed kernel: added to the predicted reset count (forces window misses)
 };
 const GpDebugKnobs& gp_debug_knobs();
 

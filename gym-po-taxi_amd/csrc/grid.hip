@@ -26,6 +26,7 @@
 #include <cmath>
 
 #include "gp_internal.h"
+#include "grid_shared.h"
 
 namespace {
 
@@ -34,22 +35,6 @@ constexpr int EPT = 4;
 constexpr int EPB = TPB * EPT;
 constexpr uint32_t SPIN_LIMIT = 1u << 24;  // default polls before a persistent wait gives up (GP_SPIN_LIMIT)
 constexpr int MAX_TPB2 = 1024;  // max tiles per K2 block (B <= 256 * 1024 * EPB)
-
-struct alignas(64) GridCtl {
-  uint64_t s_hi, s_lo, inc_hi, inc_lo;  // numpy-mode PCG64 state at step start, increment
-  uint32_t has_u32, uinteger;           // numpy's buffered 32-bit half
-  uint32_t epoch;                       // K2 launches so far (tags the per-block flags)
-  uint32_t err;                         // bit0: spin timeout
-  uint32_t b_total;                     // resets resolved by the last K2 (diagnostic)
-  uint32_t step;                        // numpy-mode steps taken (fused-kernel granule tags)
-  uint32_t fb_last;                     // fused kernel: reset words b of the last step (next launch's window centre)
-};
-
-// Per-block metric accumulators (each persistent block owns one slot: no atomics).
-struct alignas(32) MetricSlot {
-  double return_sum;
-  unsigned long long episodes, length_sum, env_steps;
-};
 
 struct GridLdsTab {
   int32_t off, bytes;
@@ -1624,7 +1609,7 @@ __device__ __forceinline__ uint64_t pcg_output_ab(u128 s) {
 }
 // A 53-bit threshold t as a threshold on the full 64-bit draw x: (x >> 11) > t  <=>  x > (t << 11) | 0x7FF
 // (t >= 2^53, a cumulative sum of 1.0, is never exceeded: saturate).
-__device__ __forceinline__ uint64_t thr_on_u64(uint64_t t) {
+__host__ __device__ __forceinline__ uint64_t thr_on_u64(uint64_t t) {
   return t >= (1ull << 53) ? ~0ull : ((t << 11) | 0x7FFull);
 }
 // Sanitised action -> byte offset of its threshold row in s_thr (numpy negative indexing; out-of-range
@@ -2506,7 +2491,10 @@ __global__ __launch_bounds__(FTPB) void grid_rollout_numpy(GridDev p_in, int K, 
     if (tid < NA * NA) s_thr[tid] = GP_TRIMS ? thr_on_u64(p.thr[tid]) : p.thr[tid];
     lds_image_copy(dyn, p.limg, p.lds.total);
     if (tid < 4) sh.jB[tid] = (&p.fjB->a_hi)[tid];
-    if (tid == 0) sh.rdone = 0;
+    if (tid == 0) {
+      sh.rdone = 0;
+      sh.spw_done = 0;
+    }
     if (tid < 8) sh.dof[tid] = (OK == GP_OBS_HANSEN && p.doff && tid < p.obs_dirs) ? p.doff[tid] : 0x7FFFFFFF;
     __syncthreads();
     LSTAMP(1);
@@ -2715,6 +2703,12 @@ struct GridBackend : EnvBackend {
       b_tja, b_tjw, b_ae, b_goal, b_ctl, b_tcount, b_tlist, b_rflag, b_mslot, b_ftj, b_flt4, b_fjB, b_fslot, b_dbg, b_self, b_jt8,
       b_limg, b_ofix, b_avo;
   int fused_G = 0, fused_qpt = 0;  // fused numpy rollout geometry (0 = not eligible)
+  // windowed numpy rollout (wgrid.hip): G blocks of E = 512 * NS envs; 0 = not eligible
+  int wg_G = 0, wg_E = 0, wg_NS = 0, wg_H = 0;
+  size_t wg_lds = 0;
+  WgParams wg{};
+  std::vector<char> wg_img;        // LDS image of its tables (the PCG jump parts rebuilt on every seed)
+  DevBuf b_wgp, b_wlimg, b_wjlane, b_wjrej, b_wjblk, b_wslots;
   bool fused_stg = false;          // outputs staged in LDS and written by the store waves
   // replay pointers for the next step
   const uint64_t* rp_u = nullptr;
@@ -2746,6 +2740,10 @@ struct GridBackend : EnvBackend {
     else if (!strcmp(key, "fused_staged")) *v = fused_stg ? 1 : 0;
     else if (!strcmp(key, "fused_spw")) *v = d.spw_on;
     else if (!strcmp(key, "fused_tile_envs")) *v = d.ftile;
+    else if (!strcmp(key, "wgrid")) *v = wg_G > 0 ? 1 : 0;
+    else if (!strcmp(key, "wgrid_blocks")) *v = wg_G;
+    else if (!strcmp(key, "wgrid_block_envs")) *v = wg_E;
+    else if (!strcmp(key, "wgrid_halo")) *v = wg_H;
     else return EnvBackend::query(key, v);
     return GP_OK;
   }
@@ -2789,6 +2787,24 @@ struct GridBackend : EnvBackend {
     return n;
   }
 #endif
+  // the windowed kernel's 16-B output stores need 16-B aligned bases (torch allocations are)
+  bool wgrid_ok(const void* act, const void* obs, const void* rew, const void* term, const void* trunc) const {
+    auto al = [](const void* x, uintptr_t m) { return ((uintptr_t)x & (m - 1)) == 0; };
+    return wg_G && al(act, 4) && al(obs, 16) && al(rew, 16) && al(term, 16) && al(trunc, 16);
+  }
+  int launch_wgrid(int K, const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc, hipStream_t s) {
+    const WgArgs a{b_wgp.as<WgParams>(), K, (const int32_t*)act, (int32_t*)obs, rew, term, trunc};
+    timer.begin(s);
+    const int e = wgrid_launch(a, wg_NS, d.nact, wg_G, wg_lds, s);
+    timer.end(s);
+    if (e != hipSuccess) {
+      gp_set_error("wgrid launch: %s", hipGetErrorString((hipError_t)e));
+      return GP_E_HIP;
+    }
+    return GP_OK;
+  }
+  int build_wgrid(const std::vector<uint16_t>& move, const std::vector<uint64_t>& thr, const std::vector<int32_t>& ocell);
+  int upload_wgrid();
   template <int OK, int QPT, bool STG>
   void launch_fused_qs(int K, const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc, hipStream_t s) {
     const size_t lds = (size_t)d.lds.total +
@@ -2897,6 +2913,10 @@ int GridBackend::upload_rng() {
     GP_HIP_CHECK(hipMemcpy(b_ftj.p, ft.data(), ft.size() * sizeof(PcgJump), hipMemcpyHostToDevice));
     GP_HIP_CHECK(hipMemcpy(b_fjB.p, jb, sizeof(jb), hipMemcpyHostToDevice));
   }
+  if (wg_G) {
+    int e = upload_wgrid();
+    if (e) return e;
+  }
   return refresh_lds_image();
 }
 
@@ -2917,6 +2937,136 @@ int GridBackend::refresh_lds_image() {
       (e = put(d.lds.ofix, d.ofix)) || (e = put(d.lds.avo, d.avo)))
     return e;
   GP_HIP_CHECK(hipDeviceSynchronize());
+  return GP_OK;
+}
+
+// The windowed kernel's geometry and static tables (eligibility already checked by build()). B must split into
+// G <= #CUs blocks of E = 512 * NS envs (NS in 1, 2, 4, 8), the smallest E that does (so that every CU has a block).
+int GridBackend::build_wgrid(const std::vector<uint16_t>& move, const std::vector<uint64_t>& thr,
+                             const std::vector<int32_t>& ocell) {
+  const GpDebugKnobs& dbg = gp_debug_knobs();
+  hipDeviceProp_t prop;
+  GP_HIP_CHECK(hipGetDeviceProperties(&prop, device));
+  const int cus = std::min(prop.multiProcessorCount, 256);
+  int E = 0;
+  for (int e = 512; e <= 4096; e *= 2)
+    if (B % e == 0 && B / e <= cus) {
+      E = e;
+      break;
+    }
+  if (!E) return GP_OK;  // not eligible: the older fused kernel serves this size
+  for (int c : ocell)
+    if (c < INT32_MIN / 2 || c > INT32_MAX / 2) return GP_OK;
+  const int H = dbg.wg_halo == 512 ? 512 : 256;
+  const int nc = d.ncells, na = d.nact;
+  // LDS image: j32 | jt8 | move | thr | ocell | avalid, 16-B aligned pieces
+  WgLds L{};
+  int off = 0;
+  auto put = [&](int32_t& o, size_t bytes) {
+    o = off;
+    off += (int)((bytes + 15) / 16 * 16);
+  };
+  put(L.j32, sizeof(PcgJump) * 32);
+  put(L.jt8, sizeof(PcgJump) * 512);
+  put(L.move, (size_t)nc * na * 2);
+  put(L.thr, (size_t)na * na * 8);
+  put(L.ocell, (size_t)nc * 4);
+  put(L.avalid, agent_valid_h.size() * 2);
+  L.total = off;
+  const size_t lds = (size_t)wg_dyn_bytes(L.total, E, H);
+  if (!wgrid_fits(E / 512, na, lds)) return GP_OK;
+  wg_img.assign((size_t)L.total, 0);
+  memcpy(wg_img.data() + L.move, move.data(), move.size() * 2);
+  std::vector<uint64_t> th(thr.size());
+  for (size_t i = 0; i < thr.size(); ++i) th[i] = thr_on_u64(thr[i]);
+  memcpy(wg_img.data() + L.thr, th.data(), th.size() * 8);
+  memcpy(wg_img.data() + L.ocell, ocell.data(), ocell.size() * 4);
+  memcpy(wg_img.data() + L.avalid, agent_valid_h.data(), agent_valid_h.size() * 2);
+  wg_G = (int)(B / E);
+  wg_E = E;
+  wg_NS = E / 512;
+  wg_H = H;
+  wg_lds = lds;
+  WgParams& w = wg;
+  w.B = (int32_t)B;
+  w.G = wg_G;
+  w.E = E;
+  w.NS = wg_NS;
+  w.nact = na;
+  w.ncells = nc;
+  w.n_agent = d.n_agent_valid;
+  w.goal = d.fixed_goal;
+  w.thr_agent = d.thr_agent;
+  w.time_limit = d.time_limit;
+  w.halo = H;
+  w.r_step = d.r_step;
+  w.r_wall = d.r_wall;
+  w.r_goal = d.r_goal;
+  w.spin_limit = d.spin_limit;
+  w.fault_block = d.fault_block;
+  w.rw_words = (E + 2 * H) / 512;
+  w.wg_bias = dbg.wg_bias;
+  w.lds = L;
+  int e;
+  if ((e = b_wgp.alloc(sizeof(WgParams))) || (e = b_wlimg.alloc((size_t)L.total)) ||
+      (e = b_wjlane.alloc(sizeof(PcgJump) * 1024)) || (e = b_wjrej.alloc(sizeof(PcgJump) * 64 * (size_t)wg_G)) ||
+      (e = b_wjblk.alloc(sizeof(PcgJump) * (size_t)wg_G)) || (e = b_wslots.alloc(sizeof(uint64_t) * 4 * (size_t)wg_G)))
+    return e;
+  w.limg = b_wlimg.as<char>();
+  w.jlane = b_wjlane.as<PcgJump>();
+  w.jrej = b_wjrej.as<PcgJump>();
+  w.jblk = b_wjblk.as<PcgJump>();
+  w.slots = b_wslots.as<uint64_t>();
+  return GP_OK;
+}
+
+// The stream-dependent parts of the windowed kernel's tables (every seed: they depend on the PCG increment).
+int GridBackend::upload_wgrid() {
+  const u128 inc = rng.inc;
+  WgParams& w = wg;
+  auto compose = [](const PcgJump& j2, const PcgJump& j1) {  // j2 o j1
+    const u128 a = mk128(j2.a_hi, j2.a_lo) * mk128(j1.a_hi, j1.a_lo);
+    const u128 c = mk128(j2.a_hi, j2.a_lo) * mk128(j1.c_hi, j1.c_lo) + mk128(j2.c_hi, j2.c_lo);
+    return PcgJump{hi64(a), lo64(a), hi64(c), lo64(c)};
+  };
+  PcgJump* j32 = reinterpret_cast<PcgJump*>(wg_img.data() + w.lds.j32);
+  PcgJump* jt8 = reinterpret_cast<PcgJump*>(wg_img.data() + w.lds.jt8);
+  for (int i = 0; i < 32; ++i) j32[i] = pcg_jump_params((u128)i, inc);
+  for (int i = 0; i < 256; ++i) {
+    jt8[i] = pcg_jump_params((u128)i, inc);
+    jt8[256 + i] = pcg_jump_params((u128)(256 * i), inc);
+  }
+  std::vector<PcgJump> jl(1024), jr((size_t)64 * wg_G), jb(wg_G);
+  const PcgJump one = pcg_jump_params((u128)1, inc), j32s = pcg_jump_params((u128)32, inc);
+  jl[0] = PcgJump{0, 1, 0, 0};
+  jl[1] = one;
+  for (int l = 1; l < 512; ++l) {
+    jl[2 * l] = compose(one, jl[2 * (l - 1)]);            // lg
+    jl[2 * l + 1] = compose(j32s, jl[2 * (l - 1) + 1]);   // 32 lg + 1
+  }
+  const PcgJump j62 = pcg_jump_params((u128)62, inc);
+  PcgJump row = one;  // 62 beta + 1
+  for (int b = 0; b < wg_G; ++b) {
+    PcgJump x = row;
+    for (int l = 0; l < 64; ++l) {
+      jr[(size_t)b * 64 + l] = x;
+      x = compose(one, x);
+    }
+    row = compose(j62, row);
+    jb[b] = pcg_jump_params((u128)std::max(0, wg_E * b - wg_H), inc);
+  }
+  w.jB = pcg_jump_params((u128)B, inc);
+  w.j512 = pcg_jump_params((u128)512, inc);
+  w.jt64 = d.jt;
+  w.dbg = d.dbg;
+  w.ctl = d.ctl;
+  w.mslot = d.mslot;
+  w.ae = d.ae;
+  GP_HIP_CHECK(hipMemcpy(b_wlimg.p, wg_img.data(), wg_img.size(), hipMemcpyHostToDevice));
+  GP_HIP_CHECK(hipMemcpy(b_wjlane.p, jl.data(), jl.size() * sizeof(PcgJump), hipMemcpyHostToDevice));
+  GP_HIP_CHECK(hipMemcpy(b_wjrej.p, jr.data(), jr.size() * sizeof(PcgJump), hipMemcpyHostToDevice));
+  GP_HIP_CHECK(hipMemcpy(b_wjblk.p, jb.data(), jb.size() * sizeof(PcgJump), hipMemcpyHostToDevice));
+  GP_HIP_CHECK(hipMemcpy(b_wgp.p, &w, sizeof(WgParams), hipMemcpyHostToDevice));
   return GP_OK;
 }
 
@@ -3012,6 +3162,7 @@ int GridBackend::step(const void* act, void* obs, float* rew, uint8_t* term, uin
   int e = dispatch_obs(d.obs_kind, [&](auto okc) -> int {
     constexpr int OK = decltype(okc)::value;
     if (rng_mode == GP_RNG_NUMPY) {
+      if (wgrid_ok(act, obs, rew, term, trunc)) return launch_wgrid(1, act, obs, rew, term, trunc, s);
       if (fused_ok(act, obs, rew, term, trunc)) return launch_fused<OK>(1, act, obs, rew, term, trunc, s);
       timer.begin(s);
       hipLaunchKernelGGL(grid_step_numpy<OK>, dim3(d.nblk), dim3(TPB), 0, s, d, (const int32_t*)act, obs, rew, term,
@@ -3046,6 +3197,13 @@ int GridBackend::step(const void* act, void* obs, float* rew, uint8_t* term, uin
 
 int GridBackend::rollout(int K, const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc,
                          hipStream_t s) {
+  if (rng_mode == GP_RNG_NUMPY && wgrid_ok(act, obs, rew, term, trunc)) {
+    if (!has_reset) {
+      gp_set_error("rollout() before reset()");
+      return GP_E_STATE;
+    }
+    return launch_wgrid(K, act, (int32_t*)obs, rew, term, trunc, s);
+  }
   if (rng_mode == GP_RNG_NUMPY && fused_ok(act, obs, rew, term, trunc) && B % 4 == 0) {
     if (!has_reset) {
       gp_set_error("rollout() before reset()");
@@ -3413,7 +3571,16 @@ int GridBackend::build(const gp_grid_config* cfg) {
       }
     }
   }
-  nslots = std::max({d.nblk, grid_persist, fused_G});
+  // the windowed numpy rollout (wgrid.hip): a fixed goal, random agent spawns and a scalar obs that is a
+  // function of the agent cell (Hansen with the goal multiplier folded in, or table[agent] + table2[goal])
+  if (rng_mode == GP_RNG_NUMPY && d.fixed_goal >= 0 && d.fixed_agent < 0 && d.n_agent_valid >= 2 &&
+      (cfg->obs_kind == GP_OBS_HANSEN || cfg->obs_kind == GP_OBS_TABLE) && !dbg.no_wgrid && !dbg.disable_fused) {
+    std::vector<int32_t> ocell(nc);
+    for (int c = 0; c < nc; ++c)
+      ocell[c] = cfg->obs_kind == GP_OBS_HANSEN ? ofix[c] : t1[c] + (t2.empty() ? 0 : t2[d.fixed_goal]);
+    if (int e2 = build_wgrid(move, thr, ocell)) return e2;
+  }
+  nslots = std::max({d.nblk, grid_persist, fused_G, wg_G});
   if ((e = b_jt.alloc(sizeof(PcgJump) * JT_LEVELS * JT_RADIX)) || (e = b_lt4.alloc(sizeof(PcgJump) * TPB)) ||
       (e = b_lt2.alloc(sizeof(PcgJump) * TPB)) || (e = b_tja.alloc(sizeof(PcgJump) * (size_t)d.nblk)) ||
       (e = b_tjw.alloc(sizeof(PcgJump) * (size_t)d.nblk)) || (e = b_ae.alloc(sizeof(uint32_t) * (B + 4))) ||

@@ -119,11 +119,16 @@ class NativeVecEnv:
         (extended_taxi.py:248); negatives in [-n, 0) wrap as numpy indexing does. Device tensors are checked
         on the device instead (GP_DERR_ACTION -> GymPoError from check() / metrics()), without a sync."""
         n = getattr(getattr(self, "single_action_space", None), "n", None)
-        if n is None or self._action_dtype != "int32" or a.size == 0:
+        if n is None or self._action_dtype != "int32":
+            return
+        if a.dtype.kind not in "iub":  # numpy refuses non-integer index arrays (before any bounds check)
+            raise IndexError("arrays used as indices must be of integer (or boolean) type")
+        if a.size == 0:
             return
         lo, hi = a.min(), a.max()
         if hi >= n or lo < -n:
-            bad = int(hi) if hi >= n else int(lo)
+            flat = a.reshape(-1)
+            bad = int(flat[np.flatnonzero((flat >= n) | (flat < -n))[0]])  # numpy names the first in index order
             raise IndexError(f"index {bad} is out of bounds for axis 0 with size {n}")
 
     def _post_obs(self, obs):

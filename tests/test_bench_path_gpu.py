@@ -70,20 +70,26 @@ def _check_chunks(env, ora, chunks, action_seed, n_act):
 
 
 # (1, 4, 20): bench.py's driver sequence (two warmup launches of 1 and W - 1 = 4 steps, then the timed 20).
-# spw: the store waves' speculative word windows (the bench path; SPW_NJ in csrc/grid.hip) on, or forced off. The
-# first steps after a reset use windows centred on a stale reset total (lanes outside them take the jump path),
-# time_limit=20 puts mass resets far outside every window.
-@pytest.mark.parametrize("chunks,time_limit,spw", [((20, 128), 500, 1), ((128, 7), 500, 1), ((20, 20), 20, 1),
-                                                   ((1, 4, 20), 500, 1), ((1, 4, 20), 500, 0)])
-def test_bench_kernel_staged_k_step_launches_bit_exact(chunks, time_limit, spw, gpu_device):
+# kernel "wgrid": the windowed rollout (csrc/wgrid.hip), which bench.py times; "fused": the older fused kernel
+# (no_wgrid knob; its speculative word windows SPW_NJ on or forced off). The first steps after a reset predict
+# the window from a stale reset total (exact regeneration), time_limit=20 puts mass resets (every env truncated
+# in one step: the slow path's coverage rounds) inside the launches.
+@pytest.mark.parametrize("kernel,chunks,time_limit,spw", [
+    ("wgrid", (20, 128), 500, 1), ("wgrid", (128, 7), 500, 1), ("wgrid", (20, 20), 20, 1), ("wgrid", (1, 4, 20), 500, 1),
+    ("fused", (20, 128), 500, 1), ("fused", (20, 20), 20, 1), ("fused", (1, 4, 20), 500, 0)])
+def test_bench_kernel_staged_k_step_launches_bit_exact(kernel, chunks, time_limit, spw, gpu_device):
     from gym_po_amd import MultistoryFourRoomsEnv
     from gym_po_amd._lib import debug_knobs
-    with debug_knobs(no_spw=1 - spw):
+    with debug_knobs(no_spw=1 - spw, no_wgrid=kernel != "wgrid"):
         env = MultistoryFourRoomsEnv(B_BENCH, grid_z=1, obs_type="hansen", time_limit=time_limit, device=gpu_device)
-    G, q, stg, tile = _staged_geometry(env)
-    if G * q * tile != B_BENCH or not stg:
-        pytest.skip(f"this GPU does not give the bench geometry (G={G}, tiles/block={q}, staged={stg})")
-    assert env.query("fused_spw") == spw
+    assert env.query("wgrid") == (kernel == "wgrid")
+    if kernel == "wgrid":
+        assert (env.query("wgrid_blocks"), env.query("wgrid_block_envs")) == (256, 4096)
+    else:
+        G, q, stg, tile = _staged_geometry(env)
+        if G * q * tile != B_BENCH or not stg:
+            pytest.skip(f"this GPU does not give the bench geometry (G={G}, tiles/block={q}, staged={stg})")
+        assert env.query("fused_spw") == spw
     ora = gridworld.FourRoomsOracle(B_BENCH, 1, obs_type="hansen", time_limit=time_limit)
     o_g = _reset_obs(env, 2024)
     np.testing.assert_array_equal(o_g.astype(np.int64), np.asarray(ora.reset_seed(2024)).astype(np.int64))
@@ -109,13 +115,13 @@ def test_bench_kernel_random_goal_staged_k_steps(gpu_device):
 @pytest.mark.parametrize("B,force_tile", [(1 << 17, 0), (1 << 18, 0), (1 << 17, 2048), (1 << 18, 512),
                                           (3 << 17, 0)])
 def test_strong_scaling_shard_sizes_staged_bit_exact(B, force_tile, gpu_device):
-    """The per-GPU shard of a strong-scaling run (1M envs over 8 / 4 GPUs): 2^17 / 2^18 envs get tiles of 512 /
+    """(The older fused kernel; the windowed kernel's shard sizes: test_wgrid_gpu.py.) The per-GPU shard of a strong-scaling run (1M envs over 8 / 4 GPUs): 2^17 / 2^18 envs get tiles of 512 /
     1024 envs (2 / 4 env waves per block) so that every CU has one; also forced to 2048-env tiles (64 blocks of
     8 env waves) and 512-env tiles (two tiles per block), and 3 * 2^17 (1024-env tiles, 1.5 per CU). K = 20
     then 128 steps per launch, bit-exact."""
     from gym_po_amd import MultistoryFourRoomsEnv
     from gym_po_amd._lib import debug_knobs
-    with debug_knobs(fused_tile=force_tile):
+    with debug_knobs(fused_tile=force_tile, no_wgrid=1):
         env = MultistoryFourRoomsEnv(B, grid_z=1, obs_type="hansen", device=gpu_device)
     G, q, stg, tile = _staged_geometry(env)
     assert G * (q - 1) * tile < B <= G * q * tile, (G, q, stg, tile)

@@ -14,17 +14,21 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("fused", [True, False])
-def test_spin_timeout_raises_instead_of_silent_results(fused, gpu_device):
+@pytest.mark.parametrize("kernel", ["wgrid", "fused", "two_kernel"])
+def test_spin_timeout_raises_instead_of_silent_results(kernel, gpu_device):
+    """wgrid: the windowed rollout's granule all-gather; fused: the older fused kernel's; two_kernel: the
+    reset resolver's per-block flags."""
     import torch
     from gym_po_amd import MultistoryFourRoomsEnv
     from gym_po_amd._lib import GymPoError, debug_knobs
     B = 2048 * 8
-    with debug_knobs(disable_fused=not fused):
+    knobs = dict(disable_fused=kernel == "two_kernel", no_wgrid=kernel != "wgrid")
+    with debug_knobs(**knobs):
         env_ok = MultistoryFourRoomsEnv(B, grid_z=1, obs_type="hansen", device=gpu_device)
-    with debug_knobs(disable_fused=not fused, spin_limit=4000, fault_block=1):
+    with debug_knobs(**knobs, spin_limit=4000, fault_block=1):
         env = MultistoryFourRoomsEnv(B, grid_z=1, obs_type="hansen", device=gpu_device)
-    assert (env.query("fused_blocks") > 0) == fused
+    assert (env.query("fused_blocks") > 0) == (kernel != "two_kernel")
+    assert env.query("wgrid") == (kernel == "wgrid")
     env.reset(seed=3)
     acts = torch.randint(0, 4, (6, B), dtype=torch.int32, device=gpu_device)
     env.rollout(acts)  # asynchronous: returns; the failure is on the device

@@ -29,3 +29,26 @@ def test_out_of_range_host_actions_raise_numpys_index_error(n):
 
 def test_continuous_actions_not_range_checked():
     _env(None, "float32")._check_host_actions(np.array([[5.0, -7.0]]))
+
+
+@pytest.mark.parametrize("n", [4, 8])
+def test_first_offending_action_named_like_numpy(n):
+    e = _env(n)
+    table = np.zeros((n, n))
+    a = np.array([0, -n - 3, 2 * n, 1])  # an early too-negative index, a later too-large one
+    with pytest.raises(IndexError) as ours:
+        e._check_host_actions(a)
+    with pytest.raises(IndexError) as ref:
+        table[a]
+    assert str(ours.value) == str(ref.value)
+
+
+def test_float_host_actions_raise_like_numpy():
+    e = _env(4)
+    table = np.zeros((4, 4))
+    a = np.array([0.0, 1.0])
+    with pytest.raises(IndexError) as ours:
+        e._check_host_actions(a)
+    with pytest.raises(IndexError) as ref:
+        table[a]
+    assert str(ours.value) == str(ref.value)

@@ -47,8 +47,11 @@ def _worker(rank, world, port, out):
 @pytest.mark.timeout(300)
 def test_two_processes_device_shards_gloo(tmp_path):
     import torch
-    if torch.cuda.is_initialized():
-        pytest.skip("this process already initialised the GPU: spawning from it is not allowed here")
+    from gym_po_amd import _lib
+    # torch's own flag, and whether this process has loaded the native library (whose first handle initialises HIP
+    # outside torch): either means the GPU may be initialised here, and spawning from it is not allowed
+    if torch.cuda.is_initialized() or _lib._lib is not None:
+        pytest.skip("this process may already have initialised the GPU: spawning from it is not allowed here")
     import torch.multiprocessing as mp
     out = str(tmp_path / "m.npy")
     mp.spawn(_worker, args=(2, _free_port(), out), nprocs=2, join=True)

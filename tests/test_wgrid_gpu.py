@@ -1,0 +1,174 @@
+"""GPU parity of the windowed numpy-exact rollout (csrc/wgrid.hip), the kernel bench.py times.
+
+Every case compares each step's obs / reward / terminated / truncated, the final env state and the final PCG64
+state (incl. numpy's buffered half-word) with the numpy oracle (pinned to reference fixtures by
+tests/test_oracle_golden.py), through K-step launches of the C-ABI plan (`rollout_plan`) exactly as bench.py
+drives them. Reference semantics: msrooms.py:369-413, rooms.py:177-222, action_utils.py:84-90.
+
+What each case forces:
+- block sizes E = 512 / 1024 / 2048 / 4096 envs (the strong-scaling shards of 1M envs over 8 / 4 / 2 GPUs);
+- a window halo of 512 draws, and a prediction bias that puts every step's window outside its halo (the exact
+  regeneration after the exchange);
+- a Lemire rejection planted in the choice() stream inside a launch (the slow path: rejected positions listed,
+  every resetter placed exactly);
+- ordinal actions (8 thresholds per row) and table obs (ROOMS layouts).
+"""
+import numpy as np
+import pytest
+
+from oracle import gridworld
+from oracle.pcg64 import MASK128, lemire_threshold, pcg_advance_params, pcg_output
+
+pytestmark = pytest.mark.gpu
+
+
+def _rng_tuple(st):
+    s, inc = st["state"]["state"], st["state"]["inc"]
+    m = (1 << 64) - 1
+    return [s >> 64, s & m, inc >> 64, inc & m, st["has_uint32"], st["uinteger"]]
+
+
+def _reset_obs(env, seed):
+    r = env.reset(seed=seed)
+    return (r[0] if isinstance(r, tuple) else r).cpu().numpy()
+
+
+def _check_chunks(env, ora, chunks, action_seed, n_act, before_chunk=None):
+    import torch
+    rng = np.random.default_rng(action_seed)
+    for ci, K in enumerate(chunks):
+        if before_chunk:
+            before_chunk(ci)
+        a_np = rng.integers(0, n_act, (K, env.num_envs)).astype(np.int32)
+        run, (obs, rew, term, trunc) = env.rollout_plan(torch.as_tensor(a_np, device=env.device))
+        run()
+        o, r, d, t = (x.cpu().numpy() for x in (obs, rew, term, trunc))
+        for k in range(K):
+            oo, ro, do, tro = ora.step_seeded(a_np[k].astype(np.int64))
+            np.testing.assert_array_equal(o[k].astype(np.int64), np.asarray(oo).astype(np.int64),
+                                          err_msg=f"obs chunk {ci} K={K} k={k}")
+            np.testing.assert_array_equal(r[k], ro, err_msg=f"rew chunk {ci} k={k}")
+            np.testing.assert_array_equal(d[k], do, err_msg=f"term chunk {ci} k={k}")
+            np.testing.assert_array_equal(t[k], tro, err_msg=f"trunc chunk {ci} k={k}")
+    env.check()
+    assert _rng_tuple(env.rng_state) == _rng_tuple(ora.gen.bit_generator.state)
+    a, g, e = (x.cpu().numpy() for x in env.get_state())
+    np.testing.assert_array_equal(a, np.ravel_multi_index(tuple(ora.agent.T), ora.grid.shape))
+    np.testing.assert_array_equal(e, ora.elapsed)
+
+
+def _fourrooms(B, device, **kw):
+    from gym_po_amd import MultistoryFourRoomsEnv
+    return MultistoryFourRoomsEnv(B, grid_z=1, obs_type="hansen", device=device, **kw)
+
+
+@pytest.mark.parametrize("B,E", [(1 << 17, 512), (1 << 18, 1024), (1 << 19, 2048), (3 << 17, 2048), (8192, 512)])
+def test_wgrid_block_sizes_bit_exact(B, E, gpu_device):
+    env = _fourrooms(B, gpu_device)
+    assert env.query("wgrid") == 1
+    assert env.query("wgrid_block_envs") == E and env.query("wgrid_blocks") * E == B
+    ora = gridworld.FourRoomsOracle(B, 1, obs_type="hansen")
+    np.testing.assert_array_equal(_reset_obs(env, 31).astype(np.int64), np.asarray(ora.reset_seed(31)).astype(np.int64))
+    _check_chunks(env, ora, (20, 33, 1), action_seed=3, n_act=4)
+    m = env.metrics()
+    assert m["env_steps"] == B * 54
+
+
+@pytest.mark.parametrize("knobs", [dict(wg_halo=512), dict(wg_bias=3000), dict(wg_bias=-600)])
+def test_wgrid_halo_and_forced_window_misses(knobs, gpu_device):
+    """wg_bias shifts every step's predicted reset count (3000 resets = ~1500 draws, far beyond the 256-draw
+    halo; -600 wraps to a huge count): each step's window is regenerated exactly after the exchange."""
+    from gym_po_amd._lib import debug_knobs
+    B = 1 << 20
+    with debug_knobs(**knobs):
+        env = _fourrooms(B, gpu_device)
+    assert env.query("wgrid") == 1
+    assert env.query("wgrid_halo") == knobs.get("wg_halo", 256)
+    ora = gridworld.FourRoomsOracle(B, 1, obs_type="hansen")
+    np.testing.assert_array_equal(_reset_obs(env, 5).astype(np.int64), np.asarray(ora.reset_seed(5)).astype(np.int64))
+    _check_chunks(env, ora, (12, 5), action_seed=9, n_act=4)
+
+
+def _rejected_word(n, k=1):
+    thr = lemire_threshold(n)
+    for kk in range(k, k + 10000):
+        r = -(-(kk << 32) // n)
+        if r < (1 << 32) and (r * n) & 0xFFFFFFFF < thr:
+            return r
+    raise AssertionError
+
+
+def _rotl(x, r):
+    return ((x << r) | (x >> ((64 - r) & 63))) & ((1 << 64) - 1)
+
+
+def _state_with_output_half(half_value, half, seed):
+    rng = np.random.default_rng(seed)
+    hi = int(rng.integers(0, 2 ** 63)) * 2 + 1
+    other = int(rng.integers(0, 2 ** 32))
+    x = (other << 32) | half_value if half == 0 else (half_value << 32) | other
+    lo = hi ^ _rotl(x, hi >> 58)
+    s = (hi << 64) | lo
+    assert pcg_output(s) == x
+    return s
+
+
+@pytest.mark.parametrize("word", [3, 2001, 40000])
+def test_wgrid_planted_rejection_inside_launch(word, gpu_device):
+    """The PCG64 state is set so that half-word `word` of the next step's choice() stream is a rejected Lemire
+    draw (word 40000 lies beyond the first 124 G half-words: a coverage round is needed only if that step resets
+    more envs than that, otherwise the flag alone takes the slow path). Then one 9-step launch and one of 3."""
+    B = 1 << 20
+    env = _fourrooms(B, gpu_device)
+    ora = gridworld.FourRoomsOracle(B, 1, obs_type="hansen")
+    _reset_obs(env, 7)
+    ora.reset_seed(7)
+    n = len(ora.valid_agent)
+
+    def plant(ci):
+        if ci != 1:
+            return
+        inc = ora.gen.bit_generator.state["state"]["inc"]
+        q, half = word >> 1, word & 1
+        s_star = _state_with_output_half(_rejected_word(n), half, word)
+        a, c = pcg_advance_params((1 << 128) - (B + q + 1), inc)
+        st = {"bit_generator": "PCG64", "state": {"state": (a * s_star + c) & MASK128, "inc": inc},
+              "has_uint32": 0, "uinteger": 0}
+        env.rng_state = st
+        ora.gen.bit_generator.state = st
+
+    _check_chunks(env, ora, (4, 9, 3), action_seed=21, n_act=4, before_chunk=plant)
+
+
+@pytest.mark.parametrize("kind,kw,B", [
+    ("rooms", dict(layout="4", obs_type="hansen"), 1 << 18),       # ordinal (8 actions), binary Hansen-4
+    ("rooms", dict(layout="4", obs_type="mdp"), 1 << 17),          # table obs
+    ("fourrooms", dict(grid_z=1, obs_type="mdp"), 1 << 18),        # table obs, cardinal
+])
+def test_wgrid_other_fixed_goal_configs(kind, kw, B, gpu_device):
+    from gym_po_amd import MultistoryFourRoomsEnv, RoomsEnv
+    if kind == "rooms":
+        env = RoomsEnv(B, **kw, device=gpu_device)
+        ora = gridworld.RoomsOracle(B, **kw)
+    else:
+        env = MultistoryFourRoomsEnv(B, **kw, device=gpu_device)
+        ora = gridworld.FourRoomsOracle(B, **kw)
+    assert env.query("wgrid") == 1
+    np.testing.assert_array_equal(_reset_obs(env, 13).astype(np.int64), np.asarray(ora.reset_seed(13)).astype(np.int64))
+    _check_chunks(env, ora, (16, 16), action_seed=4, n_act=env.single_action_space.n)
+
+
+def test_wgrid_single_steps_equal_rollout(gpu_device):
+    """env.step (K = 1 launches of the same kernel) equals one K-step rollout, outputs and RNG state."""
+    import torch
+    B, K = 1 << 16, 24
+    e1, e2 = _fourrooms(B, gpu_device), _fourrooms(B, gpu_device)
+    e1.reset(seed=8)
+    e2.reset(seed=8)
+    acts = torch.randint(0, 4, (K, B), device=gpu_device, dtype=torch.int32)
+    o1, r1, d1, t1 = e1.rollout(acts)
+    for k in range(K):
+        o2, r2, d2, t2, _ = e2.step(acts[k])
+        assert torch.equal(o1[k], o2) and torch.equal(r1[k], r2) and torch.equal(d1[k], d2) and torch.equal(t1[k], t2)
+    assert e1.rng_state == e2.rng_state
+    assert e1.metrics() == e2.metrics()

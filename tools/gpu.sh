@@ -119,6 +119,12 @@ case "$task" in
     last_json $O/bench_default.log 3000
     run 300 $O/bench_driver.log python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline
     last_json $O/bench_driver.log 3000 ;;
+  micro)  # VALU / PCG64 generation costs and the launch fixed costs (prebuilt tools/*.bin), then the latency probe
+    for b in mb_pcg mb_valu mb_lat mb_launch; do
+      [ -x tools/$b.bin ] && run 120 $O/$b.txt tools/$b.bin && cat $O/$b.txt
+    done
+    run 200 $O/lat.log python -u tools/latency_probe.py ${@:-1048576 1 20 128}
+    grep "B=" $O/lat.log ;;
   multi)
     GP_BENCH_BACKEND=gloo run 300 $O/multi2.log python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
       --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 256 --warmup 128 --envs 262144 --no-cpu-baseline
