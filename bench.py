@@ -62,14 +62,15 @@ def _anttag(B, dev, mode):
 
 
 # The headline (BASELINE.json configs[1]) and the other single-GPU configs, measured the same way.
-# bytes: algorithmic bytes per env-step of a fused rollout launch; state: bytes per env
-# read + written once per launch.
+# bytes: algorithmic bytes per env-step of a fused rollout launch; state: bytes per env read + written
+# once per launch in SURVEY.md §8(d)'s canonical layout (agent / goal / elapsed int32 = 12 B each way: "14 B + 24/K";
+# C-ROOMS 20 B each way). The kernels keep a packed 4-8 B state, so their own traffic is below this count.
 WORKLOADS = {
-    "fourrooms": dict(make=_fourrooms, envs=1 << 20, n_actions=4, mode="numpy", bytes=14, state=8, chunk=128,
+    "fourrooms": dict(make=_fourrooms, envs=1 << 20, n_actions=4, mode="numpy", bytes=14, state=24, chunk=128,
                       metric=HEADLINE_METRIC, dtype="int32",
                       desc="configs[1]: FourRooms 11x11 (FR_MAP) Hansen-4 obs, {B} envs per GPU, "
                            "MultistoryFourRoomsEnv(grid_z=1, obs_type='hansen')"),
-    "taxi": dict(make=_taxi_onehot, envs=1 << 22, n_actions=5, mode="philox", bytes=4 + 320 + 4 + 1 + 1, state=8,
+    "taxi": dict(make=_taxi_onehot, envs=1 << 22, n_actions=5, mode="philox", bytes=4 + 320 + 4 + 1 + 1, state=24,
                  metric="env steps/sec, PO-Taxi 5x5 Hansen one-hot obs (uint8[320]) at 4M envs per GPU",
                  dtype="uint8", kernel="taxi_rollout<16,false>", chunk=4,
                  desc="configs[2]: PO-Taxi 5x5 (TAXI_MAP) Hansen obs one-hot uint8[B,320], {B} envs per GPU, "
@@ -79,7 +80,7 @@ WORKLOADS = {
                    dtype="f64 state / f32 I/O", kernel="crooms_rollout<GP_OBS_F32,false>", chunk=128,
                    desc="configs[4]: C-ROOMS layout 4, yx actions f32 U[-1,1]^2, vector_mdp obs f32[B,2], {B} envs per "
                         "GPU, CRoomsEnv(obs_type='vector_mdp')"),
-    "anttag": dict(make=_anttag, envs=1 << 21, n_actions=5, mode="philox", bytes=4 + 16 + 4 + 1 + 1, state=8,
+    "anttag": dict(make=_anttag, envs=1 << 21, n_actions=5, mode="philox", bytes=4 + 16 + 4 + 1 + 1, state=24,
                    metric="env steps/sec, grid Ant-Tag 10x10 (build-defined), 2M envs per GPU (16M on 8 GPUs)",
                    dtype="int32", kernel="anttag_rollout<false>",
                    desc="configs[3]: grid Ant-Tag 10x10, {B} envs per GPU (2M x 8 GPUs = 16M), AntTagGridEnv()"),
@@ -93,7 +94,7 @@ def lib_hash():
 
 
 # sources that determine each measured kernel's code (PMC traffic is reused only for the same sources)
-KERNEL_SOURCES = {"fourrooms": ("grid.hip", "gp_common.h", "gp_internal.h"),
+KERNEL_SOURCES = {"fourrooms": ("wgrid.hip", "grid.hip", "grid_shared.h", "gp_common.h", "gp_internal.h"),
                   "taxi": ("taxi.hip", "gp_common.h", "gp_internal.h"),
                   "crooms": ("crooms.hip", "gp_common.h", "gp_internal.h", "ziggurat_tables.h"),
                   "anttag": ("anttag.hip", "gp_common.h", "gp_internal.h")}
@@ -145,30 +146,72 @@ def cpu_model():
     return None
 
 
+def effective_cpus():
+    """CPUs this process can really use: the scheduler affinity mask, capped by the cgroup CPU quota
+    (cgroup v2 `cpu.max` "quota period", v1 `cpu.cfs_quota_us` / `cpu.cfs_period_us`). Returns (effective,
+    os.cpu_count(), affinity, quota or None). A container that sees 256 CPUs may hold a quota of a few."""
+    count = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except Exception:  # noqa: BLE001
+        aff = count
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except Exception:  # noqa: BLE001
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except Exception:  # noqa: BLE001
+            pass
+    eff = aff if quota is None else max(1, min(aff, int(quota)))
+    return eff, count, aff, quota
+
+
 def cpu_baseline(workload="fourrooms", target_s=12.0, procs=None):
     """The numpy oracle (the reference's algorithm restated, fixture-pinned) on the host: one process on one
-    core, then P = os.cpu_count() independent processes, each on its own 2^16-env batch.
+    core, then P independent processes, each on its own 2^16-env batch, P = the CPUs this
+    process may really use (affinity and cgroup quota: effective_cpus; os.cpu_count() is reported beside it).
     The aggregate is every process's env-steps over the wall span from the first process's start to the last
     one's end (so processes that time-share fewer cores than P are not over-counted)."""
     one = _cpu_baseline_1(workload, target_s)
-    procs = procs or (os.cpu_count() or 1)
-    try:
-        usable = len(os.sched_getaffinity(0))
-    except Exception:  # noqa: BLE001
-        usable = None
+    eff, count, usable, quota = effective_cpus()
+    procs = procs or eff
     if procs <= 1:
+        one.update(cpu_count=count, cpus_usable=usable, cgroup_quota_cpus=quota)
         return one
     import multiprocessing as mp
     ctx = mp.get_context("spawn")  # fresh interpreters (numpy only): never fork a process that holds the GPU
-    t0 = time.perf_counter()
-    with ctx.Pool(procs) as pool:
-        res = pool.starmap(_cpu_baseline_1, [(workload, target_s, 1 << 16)] * procs)
-    wall = time.perf_counter() - t0
-    span = max(r["t_end"] for r in res) - min(r["t_start"] for r in res)
-    agg = sum(r["env_steps"] for r in res) / span
+
+    def pool_run(P):
+        t0 = time.perf_counter()
+        with ctx.Pool(P) as pool:
+            res = pool.starmap(_cpu_baseline_1, [(workload, target_s, 1 << 16)] * P)
+        wall = time.perf_counter() - t0
+        span = max(r["t_end"] for r in res) - min(r["t_start"] for r in res)
+        agg = sum(r["env_steps"] for r in res) / span
+        per_proc = [r["env_steps"] / max(r["t_end"] - r["t_start"], 1e-9) for r in res]
+        return res, wall, span, agg, per_proc
+
+    res, wall, span, agg, per_proc = pool_run(procs)
+    oversub = None
+    per1 = one["value"]  # one process alone (2^18 envs)
+    if sorted(per_proc)[len(per_proc) // 2] < 0.5 * per1 and procs > 1:
+        # the P processes time-shared fewer cores than P (a quota the files above do not show): measure again
+        # with as many processes as cores were actually available, so that `cores` states what ran
+        oversub = procs
+        procs = max(1, min(procs, int(round(agg / per1))))
+        res, wall, span, agg, per_proc = pool_run(procs)
     return {"value": agg, "unit": "env-steps/s", "cores": procs, "kind": "port",
-            "cpu_model": cpu_model(), "cpus_usable": usable,
-            "sample": f"P = os.cpu_count() = {procs} processes (sched affinity: {usable} CPUs) x "
+            "cpu_model": cpu_model(), "cpu_count": count, "cpus_usable": usable, "cgroup_quota_cpus": quota,
+            "per_process_median": float(sorted(per_proc)[len(per_proc) // 2]),
+            "oversubscribed_first_try": oversub,
+            "sample": f"P = {procs} processes (effective CPUs: affinity {usable}, cgroup quota {quota}, "
+                      f"os.cpu_count() {count}) x "
                       f"({res[0]['sample']}); aggregate = total env-steps / {span:.1f} s span ({wall:.1f} s pool "
                       f"wall); 1 process on 2^18 envs: {one['value']:.4g} env-steps/s. The oracle is the "
                       f"reference's numpy step restated (fixture-pinned); per core it runs ~1.5x faster than the "
@@ -419,6 +462,9 @@ def main():
         strong = {"global_envs": args.envs, "envs_per_gpu": Bs, "value": args.envs * args.steps / ts,
                   "ms_per_step": ts / args.steps * 1e3, "scaling": "strong"}
 
+    kernel_name = None
+    if args.workload == "fourrooms" and args.mode == "numpy" and env.query("wgrid"):
+        kernel_name = f"wgrid_rollout<{env.query('wgrid_block_envs') // 512},{W['n_actions']}>"
     total_steps = (args.envs if args.strong else B * world) * args.steps
     cfg_key = (f"fourrooms_hansen4_B{B}_{args.mode}" if args.workload == "fourrooms" else
                f"{args.workload}_B{B}_{args.mode}")
@@ -445,7 +491,7 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_over_algorithmic": traffic / bytes_per_launch if traffic else None,
                      "traffic_source": traffic_src,
-                     "kernel": W.get("kernel") or (("grid_rollout_numpy<GP_OBS_HANSEN,2,4,true>" if steps_per_launch > 1.5
+                     "kernel": W.get("kernel") or (kernel_name if kernel_name else ("grid_rollout_numpy<GP_OBS_HANSEN,2,4,true>" if steps_per_launch > 1.5
                                                    else "grid_step_numpy<GP_OBS_HANSEN>") if args.mode == "numpy"
                                                   else "grid_rollout_counter<GP_OBS_HANSEN,false>"),
                      "steps_per_launch": steps_per_launch,

@@ -33,6 +33,7 @@ struct GpDebugKnobs {
   int no_wgrid = 0;         // GRID: 1 = never the windowed kernel (wgrid.hip): the older fused kernel instead
   int wg_halo = 0;          // GRID windowed kernel: window halo (256 or 512 draws); 0 = default
   int wg_bias = 0;          // GRID windowed kernel: added to the predicted reset count (forces window misses)
+  int wg_tmode = 0;         // GRID windowed kernel: timing-study variants (wgrid.hip TM_*); some give wrong results
 };
 const GpDebugKnobs& gp_debug_knobs();
 

@@ -3006,11 +3006,12 @@ int GridBackend::build_wgrid(const std::vector<uint16_t>& move, const std::vecto
   w.fault_block = d.fault_block;
   w.rw_words = (E + 2 * H) / 512;
   w.wg_bias = dbg.wg_bias;
+  w.tmode = dbg.wg_tmode;
   w.lds = L;
   int e;
   if ((e = b_wgp.alloc(sizeof(WgParams))) || (e = b_wlimg.alloc((size_t)L.total)) ||
       (e = b_wjlane.alloc(sizeof(PcgJump) * 1024)) || (e = b_wjrej.alloc(sizeof(PcgJump) * 64 * (size_t)wg_G)) ||
-      (e = b_wjblk.alloc(sizeof(PcgJump) * (size_t)wg_G)) || (e = b_wslots.alloc(sizeof(uint64_t) * 4 * (size_t)wg_G)))
+      (e = b_wjblk.alloc(sizeof(PcgJump) * 2 * (size_t)wg_G)) || (e = b_wslots.alloc(sizeof(uint64_t) * 4 * (size_t)wg_G)))
     return e;
   w.limg = b_wlimg.as<char>();
   w.jlane = b_wjlane.as<PcgJump>();
@@ -3036,16 +3037,17 @@ int GridBackend::upload_wgrid() {
     jt8[i] = pcg_jump_params((u128)i, inc);
     jt8[256 + i] = pcg_jump_params((u128)(256 * i), inc);
   }
-  std::vector<PcgJump> jl(1024), jr((size_t)64 * wg_G), jb(wg_G);
+  std::vector<PcgJump> jl(1024), jr((size_t)64 * wg_G), jb(2 * (size_t)wg_G);
   const PcgJump one = pcg_jump_params((u128)1, inc), j32s = pcg_jump_params((u128)32, inc);
+  const PcgJump jBp1 = pcg_jump_params((u128)B + 1, inc);  // B + 1
   jl[0] = PcgJump{0, 1, 0, 0};
-  jl[1] = one;
+  jl[1] = jBp1;
   for (int l = 1; l < 512; ++l) {
     jl[2 * l] = compose(one, jl[2 * (l - 1)]);            // lg
-    jl[2 * l + 1] = compose(j32s, jl[2 * (l - 1) + 1]);   // 32 lg + 1
+    jl[2 * l + 1] = compose(j32s, jl[2 * (l - 1) + 1]);   // B + 32 lg + 1
   }
   const PcgJump j62 = pcg_jump_params((u128)62, inc);
-  PcgJump row = one;  // 62 beta + 1
+  PcgJump row = jBp1;  // B + 62 beta + 1
   for (int b = 0; b < wg_G; ++b) {
     PcgJump x = row;
     for (int l = 0; l < 64; ++l) {
@@ -3053,7 +3055,8 @@ int GridBackend::upload_wgrid() {
       x = compose(one, x);
     }
     row = compose(j62, row);
-    jb[b] = pcg_jump_params((u128)std::max(0, wg_E * b - wg_H), inc);
+    jb[2 * b] = pcg_jump_params((u128)B + (u128)(b ? wg_E * b - wg_H : 0), inc);
+    jb[2 * b + 1] = b ? pcg_jump_params((u128)(wg_E * b - wg_H + 1), inc) : PcgJump{0, 1, 0, 0};
   }
   w.jB = pcg_jump_params((u128)B, inc);
   w.j512 = pcg_jump_params((u128)512, inc);

@@ -41,11 +41,14 @@ struct WgParams {
   int32_t fault_block;          // test knob: this block never publishes (-1 off)
   int32_t rw_words;             // words per env lane per window fill: (E + 2H) / 512
   int32_t wg_bias;              // test knob: added to the predicted reset count (forces window misses); 0
+  int32_t tmode;                // timing-study knob (gp_debug_set wg_tmode; 0 in production): see wgrid.hip TM_*
   WgLds lds;
   const char* limg;             // [lds.total] LDS image of the tables
-  const PcgJump* jlane;         // [512][2]: jump by lg (window fill) and by 32 lg + 1 (coarse states), lg = env lane
-  const PcgJump* jrej;          // [G][64]: jump by 62 beta + l + 1 (rejection-check slice of block beta, lane l)
-  const PcgJump* jblk;          // [G]: jump by max(0, E beta - H) (window base of block beta)
+  // Per-lane / per-block constant jumps, all applied to S(x_t), the state at a step's start (B = num envs):
+  const PcgJump* jlane;         // [512][2]: by lg (window fill from its base) and by B + 32 lg + 1 (coarse state lg)
+  const PcgJump* jrej;          // [G][64]: by B + 62 beta + l + 1 (rejection-check slice of block beta, lane l)
+  const PcgJump* jblk;          // [G][2]: by B + E beta - H (beta > 0; B for beta 0): the next window's base after
+                                //   the choice() draws; by E beta - H + 1 (beta > 0; 0 for beta 0): a launch's first
   const PcgJump* jt64;          // radix-64 general jump tables (JT_LEVELS x 64) for the rare paths
   PcgJump jB, j512;             // jump by B (random(B)), by 512 (a lane's next window word)
   GridCtl* ctl;
@@ -67,7 +70,7 @@ struct WgArgs {  // one launch: K steps, caller-owned action [K][B] and output [
 
 // Dynamic LDS bytes of a launch (tables + window + coarse states + staging).
 __host__ __device__ constexpr int wg_dyn_bytes(int tables, int E, int H) {
-  return tables + (E + 2 * H) * 8 + 512 * 16 + 2 * E * 4;
+  return tables + (E + 2 * H) * 8 + 2 * 512 * 16 + 3 * E * 4;
 }
 // Launch on `s` (host; csrc/wgrid.hip). Returns hipError_t as int.
 int wgrid_launch(const WgArgs& a, int NS, int NA, int G, size_t dyn_lds, hipStream_t s);

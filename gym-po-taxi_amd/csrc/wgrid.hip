@@ -63,6 +63,14 @@ namespace {
   } while (0)
 #endif
 
+// Timing-study variants (WgParams::tmode, gp_debug_set "wg_tmode"; never set in production). TM_NOSTORE and TM_NOFILL
+// drop work (results invalid: measurement only); the others are alternative schedules with exact results.
+constexpr int TM_NOSTORE = 1;   // store waves skip the output copy
+constexpr int TM_NOFILL = 2;    // env waves skip the window fill (stale words)
+constexpr int TM_LATEACT = 4;   // env waves load the next step's actions after the transitions (default: before)
+constexpr int TM_THROTTLE = 8;  // store waves drain their stores after every 16-env chunk (vmcnt(0))
+constexpr int TM_BUSYPOLL = 16; // the all-gather polls without s_sleep
+
 constexpr int EW = 8;                 // env waves
 constexpr int SW = 2;                 // store waves
 constexpr int CWAVE = EW;             // the control wave
@@ -74,15 +82,22 @@ constexpr int MAXRP = 512;            // rejected half-word positions the slow p
 
 struct WgShared {
   uint64_t mask[8][EW];      // this step's resetter ballots by (slot k, env wave w)
-  uint32_t trans_done;       // env waves done with the step's transitions (monotone: EW per step)
-  uint32_t cs_done;          // env waves done with the coarse states
-  uint32_t r2s_done;         // env waves done listing their resetters in r2s
-  uint32_t sy_ready;         // control wave: S(y_t) and the window base of the step published (k + 1)
+  // monotone LDS counters: the waves never meet at a workgroup barrier inside the step loop
+  uint32_t trans_done;       // env waves done with a step's transitions (EW per step)
+  uint32_t cs_done;          // env waves done with a step's coarse states
+  uint32_t r2s_done;         // env waves done listing a step's resetters in r2s
+  uint32_t fill_done;        // env-wave window fills (and exact regenerations) completed
+  uint32_t res_done;         // env waves done taking a step's resetter cells (the staging is final)
+  uint32_t st_done;          // store-wave step copies completed (SW per step)
+  uint32_t sx_ready;         // control wave: step k's S(x) published (k + 1)
+  uint32_t sy_ready;         // control wave: step k's S(y) and step k+1's window base published (k + 1)
+  uint32_t cells_done;       // control wave: step k's exchange finished, its resetters' cells staged (k + 1)
   uint32_t pro;              // prologue: the first window's base is published
-  uint64_t sy_hi, sy_lo;     // S(y_t), the state after the step's random(B)
-  uint64_t rw_hi, rw_lo;     // base state of the window being filled (the next step's random(B) words)
+  uint64_t sx[2][2];         // by step parity: S(x_t) (hi, lo), the state at the step's start
+  uint64_t sy[2][2];         // by step parity: S(y_t) (hi, lo), the state after the step's random(B)
+  uint64_t rw[2][2];         // by parity of the step a window serves: its base state (hi, lo)
   int32_t rw_off[2];         // by step parity: env i of that step reads window word i + rw_off
-  uint32_t fix[2];           // by step parity, read after B2: bit 0 slow path, bit 1 window regeneration
+  uint32_t fix[2];           // by step parity: bit 0 slow path, bit 1 window regeneration
   uint32_t R, h, u, nrp;     // slow path: block prefix, has_uint32 / uinteger at the step start, # positions
   uint32_t rp[MAXRP];        // slow path: rejected half-word positions, ascending
   uint16_t r2s[4096];        // resetter rank in the block -> env slot
@@ -195,17 +210,18 @@ __device__ __forceinline__ u128 jump_any(const Tabs& tb, u128 s, uint32_t n) {
   return pcg_jump(tb.jt64, s, n);
 }
 
-// The window base for block beta when `used` u64 draws follow random(B): the state whose next output is the
-// window's word 0, and Heff = how many words of the window precede the block's first env word.
-__device__ __forceinline__ u128 rw_base(const Tabs& tb, const PcgJump& jb, u128 Sy, uint32_t used, int beta,
+// The base of the next step's window for block beta when the current step's choice() call uses `used` u64 draws:
+// the state whose next output is window word 0, from S(x_t) (jb = jblk[beta][0] folds in random(B) and E beta - H),
+// and heff = how many window words precede the block's first env word.
+__device__ __forceinline__ u128 rw_base(const Tabs& tb, const PcgJump& jb, u128 Sx, uint32_t used, int beta,
                                         int32_t& heff) {
   const int32_t H = tb.halo;
   if (beta == 0) {
     heff = min(H, (int32_t)used + 1);
-    return jump_any(tb, Sy, used + 1u - (uint32_t)heff);
+    return apply_jump(jb, jump_any(tb, Sx, used + 1u - (uint32_t)heff));
   }
-  heff = H;  // E beta >= 512 >= H: jblk[beta] = J_{E beta - H}
-  return apply_jump(jb, jump_any(tb, Sy, used + 1u));
+  heff = H;
+  return apply_jump(jb, jump_any(tb, Sx, used + 1u));
 }
 
 __device__ __forceinline__ bool spin_give_up(const WgParams& P, uint32_t& spins) {
@@ -224,12 +240,14 @@ __device__ __forceinline__ bool spin_give_up(const WgParams& P, uint32_t& spins)
 __device__ __forceinline__ uint64_t gran(uint32_t tag, uint32_t rej, uint32_t cnt) {
   return ((uint64_t)tag << 32) | ((uint64_t)min(rej, 255u) << 24) | (uint64_t)(cnt & 0xFFFFFFu);
 }
-// The control wave: publish this block's granule of (tag) and all-gather the G granules (lane l: blocks 4l..4l+3).
-__device__ __forceinline__ void exchange(const WgParams& P, uint64_t* slots, uint32_t tag, uint32_t rej, uint32_t cnt,
-                                         uint64_t (&g)[4]) {
-  const int lane = threadIdx.x & 63, G = (int)gridDim.x;
-  if (lane == 0 && (int)blockIdx.x != P.fault_block)
+// The control wave: publish this block's granule of (tag), then all-gather the G granules (lane l: blocks 4l..4l+3).
+__device__ __forceinline__ void publish(const WgParams& P, uint64_t* slots, uint32_t tag, uint32_t rej, uint32_t cnt) {
+  if ((threadIdx.x & 63) == 0 && (int)blockIdx.x != P.fault_block)
     __hip_atomic_store(&slots[blockIdx.x], gran(tag, rej, cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void gather(const WgParams& P, const uint64_t* slots, uint32_t tag, uint64_t (&g)[4]) {
+  const bool nap = !(P.tmode & TM_BUSYPOLL);
+  const int lane = threadIdx.x & 63, G = (int)gridDim.x;
   uint32_t pend = 0;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -251,34 +269,41 @@ __device__ __forceinline__ void exchange(const WgParams& P, uint64_t* slots, uin
         if (pend & (1u << j)) g[j] = (uint64_t)tag << 32;
       break;
     }
-    __builtin_amdgcn_s_sleep(1);
+    if (nap) __builtin_amdgcn_s_sleep(1);
   }
+}
+__device__ __forceinline__ void exchange(const WgParams& P, uint64_t* slots, uint32_t tag, uint32_t rej, uint32_t cnt,
+                                         uint64_t (&g)[4]) {
+  publish(P, slots, tag, rej, cnt);
+  gather(P, slots, tag, g);
 }
 
 __device__ __forceinline__ uint32_t gcnt(uint64_t g) { return (uint32_t)g & 0xFFFFFFu; }
 __device__ __forceinline__ uint32_t grej(uint64_t g) { return (uint32_t)(g >> 24) & 0xFFu; }
 
 // Per-launch view of the dynamic LDS (pointers resolved once) and the block geometry.
+constexpr int NSTG = 3;  // staging buffers: the store waves may trail the env waves by up to two steps
 struct Lds {
   uint64_t* RW;   // [E + 2H] window words
-  uint64_t* CS;   // [512][2] coarse states (lo, hi)
-  char* stg0;     // [2][E] staged u32 per env: cell | term << 16 | trunc << 17 | wall bump << 18
+  uint64_t* CS0;  // [2 step parities][512][2] coarse states (lo, hi)
+  char* stg0;     // [NSTG][E] staged u32 per env: cell | term << 16 | trunc << 17 | wall bump << 18
   __device__ __forceinline__ Lds(char* dyn, const WgParams& P, int E)
       : RW(reinterpret_cast<uint64_t*>(dyn + P.lds.total)),
-        CS(reinterpret_cast<uint64_t*>(dyn + P.lds.total + (size_t)(E + 2 * P.halo) * 8)),
-        stg0(dyn + P.lds.total + (size_t)(E + 2 * P.halo) * 8 + 512 * 16) {}
-  __device__ __forceinline__ char* stg(int k, int E) const { return stg0 + (size_t)(k & 1) * E * 4; }
+        CS0(reinterpret_cast<uint64_t*>(dyn + P.lds.total + (size_t)(E + 2 * P.halo) * 8)),
+        stg0(dyn + P.lds.total + (size_t)(E + 2 * P.halo) * 8 + 2 * 512 * 16) {}
+  __device__ __forceinline__ char* stg(int k, int E) const { return stg0 + (size_t)(k % NSTG) * E * 4; }
+  __device__ __forceinline__ uint64_t* CS(int k) const { return CS0 + (size_t)(k & 1) * 1024; }
 };
 
 // Slow path, control wave: append the rejected half-word positions of choice-stream slice sigma (u64 draws
 // 62 sigma + 1 .. 62 sigma + 62 after random(B), both halves; with a buffered half (h) slice 0 also owns hw 0).
-__device__ __forceinline__ void list_slice(const WgParams& P, WgShared& sh, const Tabs& tb, const Lds& L, uint32_t sigma,
-                                           u128 Sy, uint32_t h, uint32_t u) {
+__device__ __forceinline__ void list_slice(const WgParams& P, WgShared& sh, const Tabs& tb, const uint64_t* CS,
+                                           uint32_t sigma, u128 Sy, uint32_t h, uint32_t u) {
   const int lane = threadIdx.x & 63;
   bool rlo = false, rhi = false;
   if (lane < SLICE) {
     const uint32_t d = 62u * sigma + (uint32_t)lane;  // 0-based draw after random(B): state S(y + 1 + d)
-    const u128 s = d < 16384u ? draw_state(tb, L.CS, d) : pcg_jump(tb.jt64, Sy, d + 1u);
+    const u128 s = d < 16384u ? draw_state(tb, CS, d) : pcg_jump(tb.jt64, Sy, d + 1u);
     const uint64_t x = pcg_output(s);
     rlo = lemire_rejected((uint32_t)x, (uint32_t)P.n_agent, P.thr_agent);
     rhi = lemire_rejected((uint32_t)(x >> 32), (uint32_t)P.n_agent, P.thr_agent);
@@ -305,7 +330,7 @@ __device__ __forceinline__ void list_slice(const WgParams& P, WgShared& sh, cons
 }
 
 // The slices with rejections among the gathered granules (lane l holds blocks 4l..4l+3 of round r), ascending.
-__device__ __forceinline__ uint32_t list_flagged(const WgParams& P, WgShared& sh, const Tabs& tb, const Lds& L,
+__device__ __forceinline__ uint32_t list_flagged(const WgParams& P, WgShared& sh, const Tabs& tb, const uint64_t* CS,
                                                  const uint64_t (&g)[4], uint32_t r, u128 Sy, uint32_t h, uint32_t u) {
   const int G = (int)gridDim.x;
   uint32_t r4[4];
@@ -318,7 +343,7 @@ __device__ __forceinline__ uint32_t list_flagged(const WgParams& P, WgShared& sh
     any &= any - 1;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      if (__builtin_amdgcn_readlane((int)r4[j], l)) list_slice(P, sh, tb, L, r * (uint32_t)G + (uint32_t)(4 * l + j), Sy, h, u);
+      if (__builtin_amdgcn_readlane((int)r4[j], l)) list_slice(P, sh, tb, CS, r * (uint32_t)G + (uint32_t)(4 * l + j), Sy, h, u);
   }
   return tot;
 }
@@ -326,13 +351,13 @@ __device__ __forceinline__ uint32_t list_flagged(const WgParams& P, WgShared& sh
 // Slow path, control wave (a Lemire rejection in the step's choice() words, or more resets than the slices
 // cover): coverage rounds until every accepted word's position is known, the rejected positions listed in
 // sh.rp (ascending). Returns the half-words consumed. The env waves then place their own resetters.
-__device__ __forceinline__ uint32_t ctrl_slow(const WgParams& P, WgShared& sh, const Tabs& tb, const Lds& L, u128 Sy,
+__device__ __forceinline__ uint32_t ctrl_slow(const WgParams& P, WgShared& sh, const Tabs& tb, const uint64_t* CS, u128 Sy,
                                               uint32_t h, uint32_t u, uint32_t b, uint32_t ts, const uint64_t (&g0)[4]) {
   const int lane = threadIdx.x & 63, G = (int)gridDim.x, beta = (int)blockIdx.x;
   if (lane == 0) sh.nrp = 0;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
   __builtin_amdgcn_wave_barrier();
-  uint32_t rtot = list_flagged(P, sh, tb, L, g0, 0u, Sy, h, u);
+  uint32_t rtot = list_flagged(P, sh, tb, CS, g0, 0u, Sy, h, u);
   // coverage rounds: slices sigma = r G + beta of the half-words beyond the first 124 G
   uint32_t covered = 124u * (uint32_t)G;
   uint64_t* slots = P.slots + (size_t)(ts & 1u) * 2 * G;
@@ -347,7 +372,7 @@ __device__ __forceinline__ uint32_t ctrl_slow(const WgParams& P, WgShared& sh, c
     const uint32_t cnt = wave_sum(rj);
     uint64_t g[4];
     exchange(P, slots + (size_t)(r & 1u) * G, (ts << 6) | r, cnt, 0u, g);
-    rtot += list_flagged(P, sh, tb, L, g, r, Sy, h, u);
+    rtot += list_flagged(P, sh, tb, CS, g, r, Sy, h, u);
     covered += 124u * (uint32_t)G;
   }
   // half-words consumed: the position of accepted word b - 1, plus one
@@ -362,6 +387,11 @@ __device__ __forceinline__ uint32_t ctrl_slow(const WgParams& P, WgShared& sh, c
 }
 
 // ------------------------------------------------------------------ the control wave ----
+// Per step: S(x) published (sx_ready: the env waves' coarse states), the rejection check of its slice, the block's
+// reset count once the env waves' transitions are in, the granule published, S(y) and the next window's base
+// (sy_ready), the all-gather, the resetters' cells (cells_done), then the next step's S(x) = J_used(S(y)). Every
+// constant part of a jump (random(B), the block and lane offsets) is folded into per-lane / per-block tables, so
+// the chain from one exchange to the next publish is two table jumps and one per-lane jump.
 template <int NS, int NA>
 __device__ __forceinline__ void wg_ctrl(const WgParams& P, WgShared& sh, const Tabs& tb, const Lds& L, int K) {
   const int lane = threadIdx.x & 63, beta = (int)blockIdx.x, G = (int)gridDim.x;
@@ -372,62 +402,64 @@ __device__ __forceinline__ void wg_ctrl(const WgParams& P, WgShared& sh, const T
   uint32_t bprev = C->fb_last;
   const uint32_t ts0 = C->wstep + 1u;  // tag step of k = 0 (tags are never 0: the slots start zeroed)
   const PcgJump jr = P.jrej[(size_t)beta * 64 + lane];
-  const PcgJump jb = P.jblk[beta];
+  const PcgJump jb = P.jblk[2 * beta], jpro = P.jblk[2 * beta + 1];
   const PcgJump jB = P.jB;
   const uint32_t nag = (uint32_t)P.n_agent, thra = P.thr_agent;
   const int32_t H = P.halo;
   const uint32_t bias = (uint32_t)P.wg_bias;
   uint32_t* derr = &C->err;
   lds_barrier();  // P1: tables staged, counters zeroed
-  // the first window: step 0's random(B) words, exact (the window base seen from x_0 with "used" = 0)
-  {
-    int32_t heff;
-    const u128 s = rw_base(tb, jb, Sx, 0u, beta, heff);
-    if (lane == 0) {
-      sh.rw_hi = hi64(s);
-      sh.rw_lo = lo64(s);
-      sh.rw_off[0] = heff;
-      lds_release();
-      __hip_atomic_store(&sh.pro, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
+  // the first window: step 0's own random(B) words, exact: word 0 is S(x_0 + 1 + E beta - heff)
+  if (lane == 0) {
+    const u128 s = apply_jump(jpro, Sx);
+    sh.rw[0][0] = hi64(s);
+    sh.rw[0][1] = lo64(s);
+    sh.rw_off[0] = beta == 0 ? 1 : H;
+    lds_release();
+    __hip_atomic_store(&sh.pro, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   LSTAMP(P, 1);
-  lds_barrier();  // P2: the first window is filled
-  LSTAMP(P, 2);
   for (int k = 0; k < K; ++k) {
     const uint32_t ts = ts0 + (uint32_t)k;
-    const u128 Sy = apply_jump(jB, Sx);
-    // Lemire check of this block's slice of the choice() stream (u64 draws 62 beta + 1 .. + 62)
+    if (lane == 0) {
+      sh.sx[k & 1][0] = hi64(Sx);
+      sh.sx[k & 1][1] = lo64(Sx);
+      lds_release();
+      __hip_atomic_store(&sh.sx_ready, (uint32_t)k + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    // Lemire check of this block's slice of the choice() stream (u64 draws 62 beta + 1 .. + 62 after random(B))
     uint32_t rj = 0;
     if (lane < SLICE) {
-      const uint64_t x = pcg_output(apply_jump(jr, Sy));
+      const uint64_t x = pcg_output(apply_jump(jr, Sx));
       rj = (lemire_rejected((uint32_t)x, nag, thra) ? 1u : 0u) + (lemire_rejected((uint32_t)(x >> 32), nag, thra) ? 1u : 0u);
     } else if (lane == SLICE && beta == 0 && h) {
       rj = lemire_rejected(u, nag, thra) ? 1u : 0u;  // the buffered half is hw 0
     }
     const uint32_t rejc = wave_sum(rj);
-    // the next step's window, around the used predicted from the previous step's reset count
-    uint32_t used_p, hp;
-    words_to_draws(bprev + bias, h, used_p, hp);
-    int32_t heff_p;
-    const u128 Srw = rw_base(tb, jb, Sy, used_p, beta, heff_p);
-    if (lane == 0) {
-      sh.sy_hi = hi64(Sy);
-      sh.sy_lo = lo64(Sy);
-      sh.rw_hi = hi64(Srw);
-      sh.rw_lo = lo64(Srw);
-      lds_release();
-      __hip_atomic_store(&sh.sy_ready, (uint32_t)k + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
     WSTAMP(P, k, 6);
-    // this block's reset count
+    // this block's reset count, published
     lds_wait(&sh.trans_done, (uint32_t)EW * (uint32_t)(k + 1), derr);
     WSTAMP(P, k, 7);
     const uint32_t cb = wave_sum(lane < NS * EW ? (uint32_t)__builtin_popcountll(sh.mask[lane >> 3][lane & 7]) : 0u);
-    // publish and all-gather
-    uint64_t g[4];
+    uint64_t* slots = P.slots + (size_t)(ts & 1u) * 2 * G;
+    publish(P, slots, ts << 6, rejc, cb);
     WSTAMP(P, k, 8);
-    exchange(P, P.slots + (size_t)(ts & 1u) * 2 * G, ts << 6, rejc, cb, g);
+    // while the granules travel: S(y) and the next step's window, around the used predicted from the last b
+    const u128 Sy = apply_jump(jB, Sx);
+    uint32_t used_p, hp;
+    words_to_draws(bprev + bias, h, used_p, hp);
+    int32_t heff_p;
+    const u128 Srw = rw_base(tb, jb, Sx, used_p, beta, heff_p);
+    if (lane == 0) {
+      sh.sy[k & 1][0] = hi64(Sy);
+      sh.sy[k & 1][1] = lo64(Sy);
+      sh.rw[(k + 1) & 1][0] = hi64(Srw);
+      sh.rw[(k + 1) & 1][1] = lo64(Srw);
+      lds_release();
+      __hip_atomic_store(&sh.sy_ready, (uint32_t)k + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    uint64_t g[4];
+    gather(P, slots, ts << 6, g);
     WSTAMP(P, k, 9);
     const uint32_t bsum = gcnt(g[0]) + gcnt(g[1]) + gcnt(g[2]) + gcnt(g[3]);
     const uint32_t incl = wave_incl_scan(bsum);
@@ -443,11 +475,13 @@ __device__ __forceinline__ void wg_ctrl(const WgParams& P, WgShared& sh, const T
     const uint32_t rtot = wave_sum(grej(g[0]) + grej(g[1]) + grej(g[2]) + grej(g[3]));
     const bool slow = rtot != 0 || b > 124u * (uint32_t)G;
     uint32_t used, h2;
+    const uint64_t* CS = L.CS(k);
+    lds_wait(&sh.cs_done, (uint32_t)EW * (uint32_t)(k + 1), derr);
+    // (also before cells_done when nothing is drawn: every env wave has read this step's masks)
+    lds_wait(&sh.r2s_done, (uint32_t)EW * (uint32_t)(k + 1), derr);
     if (!slow) {
       words_to_draws(b, h, used, h2);
       if (cb) {  // this block's resetters' cells: rank q takes half-word R + q
-        lds_wait(&sh.cs_done, (uint32_t)EW * (uint32_t)(k + 1), derr);
-        lds_wait(&sh.r2s_done, (uint32_t)EW * (uint32_t)(k + 1), derr);
         uint16_t* st = reinterpret_cast<uint16_t*>(L.stg(k, E));
         for (uint32_t q = (uint32_t)lane; q < cb; q += 64u) {
           const uint32_t hw = R + q;
@@ -457,15 +491,14 @@ __device__ __forceinline__ void wg_ctrl(const WgParams& P, WgShared& sh, const T
             word = u;
           } else {
             const uint32_t hh = hw - h;
-            const uint64_t x = pcg_output(draw_state(tb, L.CS, hh >> 1));
+            const uint64_t x = pcg_output(draw_state(tb, CS, hh >> 1));
             word = (hh & 1u) ? (uint32_t)(x >> 32) : (uint32_t)x;
           }
           st[2 * slot] = (uint16_t)tb.avalid(lemire_value(word, nag));  // the low half of the staged word
         }
       }
     } else {
-      lds_wait(&sh.cs_done, (uint32_t)EW * (uint32_t)(k + 1), derr);
-      const uint32_t wtot = ctrl_slow(P, sh, tb, L, Sy, h, u, b, ts, g);
+      const uint32_t wtot = ctrl_slow(P, sh, tb, CS, Sy, h, u, b, ts, g);
       words_to_draws(wtot, h, used, h2);
       if (lane == 0) {
         sh.R = R;
@@ -473,27 +506,26 @@ __device__ __forceinline__ void wg_ctrl(const WgParams& P, WgShared& sh, const T
         sh.u = u;
       }
     }
-    // the next step's window offset; a window more than H off is regenerated exactly after B2
+    // the next step's window offset; a window more than H off is regenerated exactly by the env waves
     int32_t off = heff_p + (int32_t)used - (int32_t)used_p;
     uint32_t fix = slow ? 1u : 0u;
     if (k + 1 < K && (off < 0 || off > 2 * H)) {
       int32_t heff;
-      const u128 s = rw_base(tb, jb, Sy, used, beta, heff);
+      const u128 s = rw_base(tb, jb, Sx, used, beta, heff);
       off = heff;
       fix |= 2u;
       if (lane == 0) {
-        sh.rw_hi = hi64(s);
-        sh.rw_lo = lo64(s);
+        sh.rw[(k + 1) & 1][0] = hi64(s);
+        sh.rw[(k + 1) & 1][1] = lo64(s);
       }
     }
     if (lane == 0) {
       sh.rw_off[(k + 1) & 1] = off;
       sh.fix[k & 1] = fix;
+      lds_release();
+      __hip_atomic_store(&sh.cells_done, (uint32_t)k + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     WSTAMP(P, k, 10);
-    lds_barrier();  // B2
-    if (fix) lds_barrier();
-    WSTAMP(P, k, 11);
     // the next step's state S(x_{t+1}) = S(y_t + used)
     Sx = jump_any(tb, Sy, used);
     if (used) u = (uint32_t)(pcg_output(Sx) >> 32);  // numpy keeps the last drawn high half in uinteger
@@ -520,29 +552,29 @@ struct Acc {
 
 // Slow path: place this lane's resetters exactly (ranks -> positions past the listed rejections -> words).
 template <int NS>
-__device__ __forceinline__ void wg_env_slow(const WgParams& P, WgShared& sh, const Tabs& tb, const Lds& L, char* stg,
-                                            uint32_t dn, const uint32_t (&pre)[NS], const uint64_t (&bm)[NS],
-                                            uint32_t (&ae)[NS]) {
+__device__ __forceinline__ void wg_env_slow(const WgParams& P, WgShared& sh, const Tabs& tb, const uint64_t* CS,
+                                            int k, char* stg, uint32_t dn, const uint32_t (&pre)[NS],
+                                            const uint64_t (&bm)[NS], uint32_t (&ae)[NS]) {
   const int lg = threadIdx.x;
-  const u128 Sy = mk128(sh.sy_hi, sh.sy_lo);
+  const u128 Sy = mk128(sh.sy[k & 1][0], sh.sy[k & 1][1]);
   const uint32_t R = sh.R, h = sh.h, u = sh.u, n = sh.nrp;
 #pragma unroll
-  for (int k = 0; k < NS; ++k) {
-    if (!((dn >> k) & 1u)) continue;
-    uint32_t p = R + pre[k] + mbcnt(bm[k]);
+  for (int s = 0; s < NS; ++s) {
+    if (!((dn >> s) & 1u)) continue;
+    uint32_t p = R + pre[s] + mbcnt(bm[s]);
     for (uint32_t q = 0; q < n; ++q) p += sh.rp[q] <= p ? 1u : 0u;
     uint32_t word;
     if (h && p == 0) {
       word = u;
     } else {
       const uint32_t hh = p - h, d = hh >> 1;
-      const u128 s = d < 16384u ? draw_state(tb, L.CS, d) : pcg_jump(tb.jt64, Sy, d + 1u);
-      const uint64_t x = pcg_output(s);
+      const u128 st = d < 16384u ? draw_state(tb, CS, d) : pcg_jump(tb.jt64, Sy, d + 1u);
+      const uint64_t x = pcg_output(st);
       word = (hh & 1u) ? (uint32_t)(x >> 32) : (uint32_t)x;
     }
     const uint32_t cell = tb.avalid(lemire_value(word, (uint32_t)P.n_agent));
-    reinterpret_cast<uint16_t*>(stg)[2 * (k * 512 + lg)] = (uint16_t)cell;
-    ae[k] = cell;
+    reinterpret_cast<uint16_t*>(stg)[2 * (s * 512 + lg)] = (uint16_t)cell;
+    ae[s] = cell;
   }
 }
 
@@ -569,6 +601,7 @@ __device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Ta
   uint32_t* derr = &P.ctl->err;
   uint32_t* aeg = P.ae;
   const int nw = P.rw_words;
+  const int tmode = P.tmode;
   const PcgJump j512 = P.j512;
   // per-lane constant jumps: by lg (window fill) and by 32 lg + 1 (coarse state)
   const PcgJump jrw = P.jlane[2 * lg], jcs = P.jlane[2 * lg + 1];
@@ -586,20 +619,31 @@ __device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Ta
     acc.lens += ae[k] >> 16;  // episode lengths: + elapsed at the start - elapsed at the end + steps
   }
   lds_wait(&sh.pro, 1u, derr);
-  fill_window(L.RW, jrw, j512, nw, mk128(sh.rw_hi, sh.rw_lo), lg);
-  lds_barrier();  // P2
+  fill_window(L.RW, jrw, j512, nw, mk128(sh.rw[0][0], sh.rw[0][1]), lg);
+  lds_release();
+  if (lane == 0) lds_add(&sh.fill_done, 1u);
+  uint32_t fill_target = EW;
   uint64_t bm[NS];
   uint32_t pre[NS];
   for (int k = 0; k < K; ++k) {
     char* stg = L.stg(k, E);
+    if (k + 1 < K && !(tmode & TM_LATEACT)) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s) anext[s] = act[(size_t)(k + 1) * B + e0 + (size_t)s * 512 + lg];
+    }
+    lds_wait(&sh.fill_done, fill_target, derr);                  // every env wave's part of this step's window
+    if (k >= NSTG) lds_wait(&sh.st_done, (uint32_t)SW * (uint32_t)(k - NSTG + 1), derr);  // this staging buffer copied out
     if (w == 0) WSTAMP(P, k, 0);
     // ---- transitions (the critical path) ----
+    // Phased over the env slots so that their LDS round trips overlap: every slot's window word and threshold
+    // row first, then the effective actions, the move-table entries, and the staged outputs last (a store to
+    // the staging area between two slots' loads would order them: all of it is one LDS array to the compiler).
     const int32_t off = sh.rw_off[k & 1];
     uint32_t dn = 0;
+    uint32_t mvo[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-      const int i = s * 512 + lg;
-      const uint64_t x = L.RW[i + off];
+      const uint64_t x = L.RW[s * 512 + lg + off];
       const char* t = thr + arow[s];
       uint32_t eb = 0;  // 2 x effective action: #{j : x > thr[a][j]} (integer form of action_utils.py:84-90)
 #pragma unroll
@@ -608,44 +652,51 @@ __device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Ta
         eb = x > tt.x ? (uint32_t)(2 * (j + 1)) : eb;
         if (j + 2 < NA) eb = x > tt.y ? (uint32_t)(2 * (j + 2)) : eb;
       }
-      const uint32_t cell = ae[s] & 0xFFFFu;
-      const uint32_t m = *reinterpret_cast<const uint16_t*>(mv + cell * (2 * NA) + eb);
+      mvo[s] = (ae[s] & 0xFFFFu) * (2 * NA) + eb;
+    }
+    uint32_t mm[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) mm[s] = *reinterpret_cast<const uint16_t*>(mv + mvo[s]);
+    uint32_t sv[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const uint32_t m = mm[s];
       const uint32_t nc = m & 0x7FFFu, blocked = m >> 15;
       const uint32_t el = (ae[s] >> 16) + 1u;
       const bool term = nc == goal, trunc = el > tlim, done = term || trunc;
-      reinterpret_cast<uint32_t*>(stg)[i] = nc | ((uint32_t)term << 16) | ((uint32_t)trunc << 17) | (blocked << 18);
+      sv[s] = nc | ((uint32_t)term << 16) | ((uint32_t)trunc << 17) | (blocked << 18);
       ae[s] = done ? nc : (nc | (el << 16));
       bm[s] = ballot(done);
       dn |= (uint32_t)done << s;
       acc.ngoal += term ? 1u : 0u;
       acc.nwall += (blocked && !term) ? 1u : 0u;
     }
-    acc.eps += (uint32_t)__builtin_popcount(dn);
     if (lane == 0) {
 #pragma unroll
       for (int s = 0; s < NS; ++s) sh.mask[s][w] = bm[s];
     }
+#pragma unroll
+    for (int s = 0; s < NS; ++s) reinterpret_cast<uint32_t*>(stg)[s * 512 + lg] = sv[s];
+    acc.eps += (uint32_t)__builtin_popcount(dn);
     lds_release();
     if (lane == 0) lds_add(&sh.trans_done, 1u);
     if (w == 0) WSTAMP(P, k, 1);
     // the next step's actions (one step ahead)
-    if (k + 1 < K) {
+    if (k + 1 < K && (tmode & TM_LATEACT)) {
 #pragma unroll
       for (int s = 0; s < NS; ++s) anext[s] = act[(size_t)(k + 1) * B + e0 + (size_t)s * 512 + lg];
     }
     // ---- while the exchange runs: coarse states, resetter listing, the next step's window ----
-    lds_wait(&sh.sy_ready, (uint32_t)k + 1u, derr);
+    lds_wait(&sh.sx_ready, (uint32_t)k + 1u, derr);
     if (w == 0) WSTAMP(P, k, 2);
-    const u128 Sy = mk128(sh.sy_hi, sh.sy_lo);
-    const u128 Srw = mk128(sh.rw_hi, sh.rw_lo);
     {
-      const u128 cs = apply_jump(jcs, Sy);
-      reinterpret_cast<ulonglong2*>(L.CS)[lg] = ulonglong2{lo64(cs), hi64(cs)};
+      const u128 cs = apply_jump(jcs, mk128(sh.sx[k & 1][0], sh.sx[k & 1][1]));  // S(x + B + 32 lg + 1)
+      reinterpret_cast<ulonglong2*>(L.CS(k))[lg] = ulonglong2{lo64(cs), hi64(cs)};
     }
     lds_release();
     if (lane == 0) lds_add(&sh.cs_done, 1u);
     if (w == 0) WSTAMP(P, k, 3);
-    lds_wait(&sh.trans_done, (uint32_t)EW * (uint32_t)(k + 1), derr);
+    lds_wait(&sh.trans_done, (uint32_t)EW * (uint32_t)(k + 1), derr);  // every wave's masks; nobody reads the window now
     {
       const uint32_t c = lane < NS * EW ? (uint32_t)__builtin_popcountll(sh.mask[lane >> 3][lane & 7]) : 0u;
       const uint32_t ex = wave_incl_scan(c) - c;
@@ -659,23 +710,35 @@ __device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Ta
     if (lane == 0) lds_add(&sh.r2s_done, 1u);
     if (w == 0) WSTAMP(P, k, 4);
     if (k + 1 < K) {
-      fill_window(L.RW, jrw, j512, nw, Srw, lg);
+      lds_wait(&sh.sy_ready, (uint32_t)k + 1u, derr);
+      const u128 Srw = mk128(sh.rw[(k + 1) & 1][0], sh.rw[(k + 1) & 1][1]);
+      if (!(tmode & TM_NOFILL)) fill_window(L.RW, jrw, j512, nw, Srw, lg);
+      lds_release();
+      if (lane == 0) lds_add(&sh.fill_done, 1u);
+      fill_target += EW;
 #pragma unroll
       for (int s = 0; s < NS; ++s) arow[s] = action_row<NA>(anext[s], derr);
     }
     if (w == 0) WSTAMP(P, k, 5);
     if (w == EW - 1) WSTAMP(P, k, 15);
-    lds_barrier();  // B2: the block's resetter cells are staged (or the slow path is flagged)
+    // ---- the exchange's outcome: the resetters' cells ----
+    lds_wait(&sh.cells_done, (uint32_t)k + 1u, derr);
+    if (w == 0) WSTAMP(P, k, 11);
     const uint32_t fix = sh.fix[k & 1];
-    if (fix) {
-      if (fix & 1u) wg_env_slow<NS>(P, sh, tb, L, stg, dn, pre, bm, ae);
-      if ((fix & 2u) && k + 1 < K) fill_window(L.RW, jrw, j512, nw, mk128(sh.rw_hi, sh.rw_lo), lg);
-      lds_barrier();
-    }
-    if (!(fix & 1u)) {
+    if (fix & 1u) {
+      wg_env_slow<NS>(P, sh, tb, L.CS(k), k, stg, dn, pre, bm, ae);
+    } else {
 #pragma unroll
       for (int s = 0; s < NS; ++s)
         if ((dn >> s) & 1u) ae[s] = reinterpret_cast<const uint16_t*>(stg)[2 * (s * 512 + lg)];
+    }
+    lds_release();
+    if (lane == 0) lds_add(&sh.res_done, 1u);
+    if ((fix & 2u) && k + 1 < K) {  // the prediction missed the window: regenerate it exactly
+      fill_window(L.RW, jrw, j512, nw, mk128(sh.rw[(k + 1) & 1][0], sh.rw[(k + 1) & 1][1]), lg);
+      lds_release();
+      if (lane == 0) lds_add(&sh.fill_done, 1u);
+      fill_target += EW;
     }
   }
 #pragma unroll
@@ -689,59 +752,53 @@ __device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Ta
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void nt_store(void* p, u32x4 v) { __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p)); }
 
+// Step k's staging (final once every env wave has taken its resetters' cells) -> obs, reward, terminated,
+// truncated in HBM, 16 envs per lane and chunk, while the env waves run the next steps.
 template <int NS>
 __device__ __forceinline__ void wg_store(const WgParams& P, WgShared& sh, const Tabs& tb, const Lds& L, int K,
                                          int32_t* __restrict__ obs, float* __restrict__ rew, uint8_t* __restrict__ term,
                                          uint8_t* __restrict__ trunc) {
   const int sl = (int)threadIdx.x - (EW + 1) * 64;  // 0..127
+  const int lane = sl & 63;
   const int beta = (int)blockIdx.x, G = (int)gridDim.x;
   constexpr int E = NS * 512;
   const size_t B = (size_t)E * (size_t)G;
   const float rs = P.r_step, rwall = P.r_wall, rg = P.r_goal;
+  const int tmode = P.tmode;
+  uint32_t* derr = &P.ctl->err;
   lds_barrier();  // P1
-  lds_barrier();  // P2
   for (int k = 0; k < K; ++k) {
-    lds_barrier();  // B2
-    if (sh.fix[k & 1]) lds_barrier();
+    lds_wait(&sh.res_done, (uint32_t)EW * (uint32_t)(k + 1), derr);
     if (sl < 64) WSTAMP(P, k, 13);
     const uint32_t* st = reinterpret_cast<const uint32_t*>(L.stg(k, E));
     const size_t base = (size_t)k * B + (size_t)beta * E;
-    for (int c = sl; c < E / 16; c += SW * 64) {  // 16 envs per chunk
-      uint32_t v[16];
+    // Lane-contiguous: in every store instruction consecutive lanes write consecutive 16 B (obs, reward) or 4 B
+    // (terminated, truncated) of 4 envs each, whole cache lines per instruction (a lane-strided pattern left the
+    // lines to be merged from partial writes and ran the output stream at a fraction of the HBM rate).
+#pragma unroll 2
+    for (int c = sl; c < E / 4 && !(tmode & TM_NOSTORE); c += SW * 64) {  // 4 envs per lane and iteration
+      const uint4 x = reinterpret_cast<const uint4*>(st)[c];
+      const uint32_t v[4] = {x.x, x.y, x.z, x.w};
+      u32x4 o, r;
+      uint32_t tm = 0, tr = 0;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint4 x = reinterpret_cast<const uint4*>(st)[4 * c + q];
-        v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
+      for (int z = 0; z < 4; ++z) {
+        o[z] = (uint32_t)tb.ocell(v[z] & 0xFFFFu);
+        const float rr = (v[z] & 0x10000u) ? rg : ((v[z] & 0x40000u) ? rwall : rs);
+        r[z] = __builtin_bit_cast(uint32_t, rr);
+        tm |= ((v[z] >> 16) & 1u) << (8 * z);
+        tr |= ((v[z] >> 17) & 1u) << (8 * z);
       }
-      const size_t e = base + (size_t)c * 16;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        u32x4 o, r;
-#pragma unroll
-        for (int z = 0; z < 4; ++z) {
-          const uint32_t x = v[4 * q + z];
-          o[z] = (uint32_t)tb.ocell(x & 0xFFFFu);
-          const float rr = (x & 0x10000u) ? rg : ((x & 0x40000u) ? rwall : rs);
-          r[z] = __builtin_bit_cast(uint32_t, rr);
-        }
-        nt_store(obs + e + 4 * q, o);
-        nt_store(rew + e + 4 * q, r);
-      }
-      u32x4 tm, tr;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        uint32_t a = 0, b = 0;
-#pragma unroll
-        for (int z = 0; z < 4; ++z) {
-          a |= ((v[4 * q + z] >> 16) & 1u) << (8 * z);
-          b |= ((v[4 * q + z] >> 17) & 1u) << (8 * z);
-        }
-        tm[q] = a;
-        tr[q] = b;
-      }
-      nt_store(term + e, tm);
-      nt_store(trunc + e, tr);
+      const size_t e = base + (size_t)c * 4;
+      nt_store(obs + e, o);
+      nt_store(rew + e, r);
+      __builtin_nontemporal_store(tm, reinterpret_cast<uint32_t*>(term + e));
+      __builtin_nontemporal_store(tr, reinterpret_cast<uint32_t*>(trunc + e));
+      if (tmode & TM_THROTTLE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    // the staging buffer is free once its LDS reads are done (the stores' data left in registers)
+    lds_release();
+    if (lane == 0) lds_add(&sh.st_done, 1u);
     if (sl < 64) WSTAMP(P, k, 14);
   }
 }
@@ -776,7 +833,8 @@ __global__ __launch_bounds__(TPB) void wgrid_rollout(const WgParams* __restrict_
     }
   }
   if (tid == 0) {
-    sh.trans_done = sh.cs_done = sh.r2s_done = sh.sy_ready = sh.pro = 0;
+    sh.trans_done = sh.cs_done = sh.r2s_done = sh.fill_done = sh.res_done = sh.st_done = 0;
+    sh.sx_ready = sh.sy_ready = sh.cells_done = sh.pro = 0;
     sh.fix[0] = sh.fix[1] = 0;
   }
   const Tabs tb(dyn, P);

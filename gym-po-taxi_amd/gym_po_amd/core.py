@@ -132,7 +132,10 @@ class NativeVecEnv:
             raise IndexError(f"index {bad} is out of bounds for axis 0 with size {n}")
 
     def _post_obs(self, obs):
-        return obs
+        # obs_dtype="reference" (grid envs): the reference's own dtype, cast on the device after the kernel (the
+        # kernels and rollout_plan's buffers keep the compact native layout)
+        cast = getattr(self, "_obs_cast", None)
+        return obs if cast is None else obs.to(cast)
 
     # ------------------------------------------------------------------ seeding ----
     def _seed(self, seed, spawn_key=()):

@@ -47,8 +47,25 @@ class GridEnvBase(NativeVecEnv):
     """A GP_KIND_GRID env (ROOMS / multistory FourRooms)."""
     _ndim = 2
 
+    def _set_obs_dtype(self, obs_dtype, spec):
+        """obs_dtype: None / "native" (int32 scalars, uint8 vectors / windows: the compact layout the kernels
+        write), "reference" (the reference's own arrays: float64 for the scalar Hansen obs, whose goal multiplier
+        is a float array (msrooms.py:180-189, observations.py:62-71), int64 for every other obs), or an
+        explicit torch dtype / name. The cast runs on the device after the step."""
+        torch = _torch()
+        if obs_dtype is None or obs_dtype == "native":
+            self._obs_cast = None
+        elif obs_dtype == "reference":
+            self._obs_cast = torch.float64 if spec.kind == _lib.GP_OBS_HANSEN else torch.int64
+        elif isinstance(obs_dtype, torch.dtype):
+            self._obs_cast = obs_dtype
+        elif isinstance(obs_dtype, str) and isinstance(getattr(torch, obs_dtype, None), torch.dtype):
+            self._obs_cast = getattr(torch, obs_dtype)
+        else:
+            raise ValueError(f"obs_dtype must be None, 'native', 'reference' or a torch dtype, got {obs_dtype!r}")
+
     def _create_grid(self, flavor, cells, n_actions, p_fail, spec, fixed_goal, fixed_agent, time_limit, rewards,
-                     num_envs, device, rng_mode):
+                     num_envs, device, rng_mode, obs_dtype=None):
         cells = np.ascontiguousarray(cells, dtype=np.int32)
         shape = cells.shape if cells.ndim == 3 else (1,) + cells.shape
         self._cells_keep = cells
@@ -72,6 +89,7 @@ class GridEnvBase(NativeVecEnv):
         self._shape3 = shape
         self._create(_lib.GP_KIND_GRID, cfg, num_envs, device, rng_mode)
         self._obs_window = spec.n if spec.kind == _lib.GP_OBS_WINDOW else None
+        self._set_obs_dtype(obs_dtype, spec)
 
     def _obs_shape(self):
         if self._obs_window:

@@ -90,7 +90,7 @@ class MultistoryFourRoomsEnv(GridEnvBase):
     def __init__(self, num_envs, grid_z=1, floor_map=FR_MAP, time_limit=500, obs_type="mdp", obs_n=3,
                  action_failure_probability=1.0 / 3, action_type="cardinal", agent_xyz=None, goal_xyz=END_XYZ,
                  step_reward=0.0, wall_reward=0.0, goal_reward=1.0, render_mode=None, device=None,
-                 rng_mode="numpy", **kwargs):
+                 rng_mode="numpy", obs_dtype=None, **kwargs):
         self.grid, self.room_grid = rooms_map_to_multistory(floor_map, grid_z)
         self.metadata = dict(self.metadata)
         self.metadata["name"] += f"{grid_z}__{action_type}__{obs_type}"
@@ -130,7 +130,7 @@ class MultistoryFourRoomsEnv(GridEnvBase):
         self.action_matrix = create_action_probability_matrix(self.actions.shape[0], action_failure_probability)
         self._create_grid(_lib.GP_FLAVOR_MULTISTORY, self.grid, self.actions.shape[0], action_failure_probability,
                           spec, fixed_goal, fixed_agent, time_limit, (step_reward, wall_reward, goal_reward),
-                          num_envs, device, rng_mode)
+                          num_envs, device, rng_mode, obs_dtype)
 
     def reset(self, *, seed=None, options=None):
         """Reset all environments, set seed if given (msrooms.py:369-381). Returns (obs, {})."""

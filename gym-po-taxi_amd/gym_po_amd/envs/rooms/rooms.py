@@ -51,7 +51,8 @@ class RoomsEnv(GridEnvBase):
 
     def __init__(self, num_envs, layout="4", time_limit=500, obs_type="mdp", obs_n=3, action_failure_probability=0.2,
                  action_type="ordinal", agent_xy=None, goal_xy=(0, 0), step_reward=0.0, wall_reward=0.0,
-                 goal_reward=1.0, render_mode=None, device=None, rng_mode="numpy", **kwargs):
+                 goal_reward=1.0, render_mode=None, device=None, rng_mode="numpy", obs_dtype=None,
+                 **kwargs):
         assert layout in LAYOUTS
         self.metadata = dict(self.metadata)
         self.metadata["name"] += f"__{layout}__{action_type}__{obs_type}"
@@ -91,7 +92,7 @@ class RoomsEnv(GridEnvBase):
             pass  # coordinates of an off-grid goal are reported as-is (no indexing)
         self._create_grid(_lib.GP_FLAVOR_ROOMS, grid, self.actions.shape[0], action_failure_probability, spec,
                           fixed_goal, fixed_agent, time_limit, (step_reward, wall_reward, goal_reward), num_envs,
-                          device, rng_mode)
+                          device, rng_mode, obs_dtype)
         self._fixed_goal_yx = (goal_yx[0], goal_yx[1]) if goal_xy is not None else None
 
     def reset(self, *, seed=None, options=None):

@@ -332,3 +332,22 @@ def test_fused_multi_tile_per_block(B, gpu_device):
     """QPT > 1 (several 4096-env tiles per persistent block) vs the oracle, few steps."""
     meta, _ = load_case("fr_hansen_tl20")
     _run_vs_oracle(meta, B, 4, seed=17, action_seed=18)
+
+
+@pytest.mark.parametrize("name", ["fr_hansen_b256", "fr_mdp_z2", "rooms_10b_hansen", "fr_vector_hansen8_z2"])
+def test_obs_dtype_reference_matches_fixture_dtype_and_values(name, gpu_device):
+    """obs_dtype="reference": the reference's own obs arrays (float64 for the scalar Hansen obs, whose goal multiplier
+    is a float array (msrooms.py:180-189, observations.py:62-71); int64 otherwise), dtype and values, against the
+    reference fixtures (no cast in the comparison). The default stays the compact native layout (int32 / uint8)."""
+    meta, data = load_case(name)
+    env = make_env(meta, obs_dtype="reference")
+    native = make_env(meta)
+    o0 = np_obs(reset_obs(env, meta["seed"]))
+    assert np_obs(reset_obs(native, meta["seed"])).dtype in (np.int32, np.uint8)
+    assert o0.dtype == data["obs0"].dtype
+    np.testing.assert_array_equal(o0, data["obs0"])
+    acts = step_actions(meta)
+    for t in range(min(meta["steps"], 40)):
+        o = np_obs(env.step(acts[t])[0])
+        assert o.dtype == data["obs0"].dtype
+        assert digest(o) == data["digests"][t][0], f"t={t}"
