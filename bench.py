@@ -95,8 +95,8 @@ def lib_hash():
 
 # sources that determine each measured kernel's code (PMC traffic is reused only for the same sources)
 KERNEL_SOURCES = {"fourrooms": ("wgrid.hip", "grid.hip", "grid_shared.h", "gp_common.h", "gp_internal.h"),
-                  "taxi": ("taxi.hip", "gp_common.h", "gp_internal.h"),
-                  "crooms": ("crooms.hip", "gp_common.h", "gp_internal.h", "ziggurat_tables.h"),
+                  "taxi": ("taxi.hip", "gp_common.h", "gp_internal.h", "gp_libm.h"),
+                  "crooms": ("crooms.hip", "gp_common.h", "gp_internal.h", "ziggurat_tables.h", "gp_libm.h"),
                   "anttag": ("anttag.hip", "gp_common.h", "gp_internal.h")}
 
 

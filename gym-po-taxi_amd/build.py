@@ -1,6 +1,10 @@
 """Build libgympo_amd.so (HIP for gfx950) in-tree: gym_po_amd/libgympo_amd.so.
 
-    python gym-po-taxi_amd/build.py [--debug]
+    python gym-po-taxi_amd/build.py [--debug] [--stamps] [--asan]
+
+--asan: a host-sanitised copy, gym_po_amd/libgympo_amd_asan.so (AddressSanitizer + UndefinedBehaviorSanitizer on
+the host code only: -fsanitize follows -Xarch_host; device code is built as usual). tools/asan_cpu.sh runs the CPU
+test suite against it with the clang ASan runtime preloaded.
 
 hipcc cross-compiles without a GPU. Sources: csrc/*.hip (+ the C ABI header in include/).
 Rebuilds only when a source is newer than the library.
@@ -32,22 +36,27 @@ def up_to_date():
     return all(os.path.getmtime(d) <= t for d in deps())
 
 
-def build(force=False, debug=False, verbose=True, stamps=False):
+def build(force=False, debug=False, verbose=True, stamps=False, asan=False):
     """Compile each csrc/*.hip to an object in parallel (one hipcc per source), then link the .so."""
-    out = OUT.replace(".so", "_stamps.so") if stamps else OUT
-    if not force and not stamps and up_to_date():
+    out = OUT.replace(".so", "_stamps.so") if stamps else (OUT.replace(".so", "_asan.so") if asan else OUT)
+    if not force and not stamps and not asan and up_to_date():
         return OUT
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     flags = [f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-O1" if debug else "-O3", "-Wno-unused-result",
              "-I", os.path.join(ROOT, "include")]
     if stamps:  # diagnostic build: s_memtime phase stamps in the fused kernel (never benchmarked)
         flags.insert(0, "-DGP_STAMPS")
-    if debug:
+    if debug or asan:
         flags.append("-g")
+    san = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
+           "-Xarch_host", "-fno-omit-frame-pointer", "-Xarch_host", "-fno-sanitize-recover=undefined"]
+    if asan:
+        flags += san
     # objects are keyed on the compiler and every flag (arch included): a changed GP_OFFLOAD_ARCH / HIPCC never
     # links objects built for another target
     key = hashlib.sha1(" ".join([hipcc] + flags).encode()).hexdigest()[:10]
-    objdir = os.path.join(HERE, "build", ("stamps" if stamps else ("debug" if debug else "release")) + "-" + key)
+    kind = "stamps" if stamps else ("asan" if asan else ("debug" if debug else "release"))
+    objdir = os.path.join(HERE, "build", kind + "-" + key)
     os.makedirs(objdir, exist_ok=True)
 
     headers = [d for d in deps() if not d.endswith(".hip")]
@@ -66,7 +75,8 @@ def build(force=False, debug=False, verbose=True, stamps=False):
     from concurrent.futures import ThreadPoolExecutor
     with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
         objs = list(ex.map(compile_one, sources()))
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + ".tmp"] + objs
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC"] + (["-shared-libsan", "-fsanitize=address,undefined"]
+                                                                   if asan else []) + ["-o", out + ".tmp"] + objs
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
@@ -75,4 +85,5 @@ def build(force=False, debug=False, verbose=True, stamps=False):
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv, debug="--debug" in sys.argv, stamps="--stamps" in sys.argv)
+    build(force="--force" in sys.argv, debug="--debug" in sys.argv, stamps="--stamps" in sys.argv,
+          asan="--asan" in sys.argv)

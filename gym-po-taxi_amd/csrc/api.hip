@@ -34,6 +34,9 @@ const char* gp_derr_text(uint32_t flags) {
             sizeof(buf) - strlen(buf) - 1);
   if (flags & GP_DERR_OVERFLOW)
     strncat(buf, "more rejected choice() words in one step than the windowed kernel lists; ", sizeof(buf) - strlen(buf) - 1);
+  if (flags & GP_DERR_BTPE)
+    strncat(buf, "a Taxi numpy-mode reset needed numpy's BTPE binomial (not restated on the device); ",
+            sizeof(buf) - strlen(buf) - 1);
   if (flags & GP_DERR_STREAM)
     strncat(buf, "a numpy normal needed more words than one stream window holds; ", sizeof(buf) - strlen(buf) - 1);
   return buf;

@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "gp_internal.h"
+#include "gp_libm.h"
 #include "ziggurat_tables.h"
 
 #pragma clang fp contract(off)
@@ -108,35 +109,9 @@ __device__ __forceinline__ void stage_tables(const CrDev& p, uint8_t* lds) {
 // differs from libm in ~1% of last bits). zlog1p_neg restates glibc 2.35's log1p (sysdeps/ieee754/dbl-64/
 // s_log1p.c: fdlibm's reduction and its Lp1..Lp7 polynomial in the parallel R1 + z2 R2 + z4 R3 + z6 R4 order),
 // IEEE double ops without contraction, so tail values equal numpy's bit for bit; host copy gp_log1p_libm for
-// the CPU test against libm (tests/test_log1p_cpu.py). exp of the wedge test: a compact ~1-ulp version
-// (GP_ZIG_OCML=1: the device libm's) -- a wedge accept / reject can only differ from glibc's when both sides of
-// `(fi[i-1] - fi[i]) u + fi[i] < exp(-x^2 / 2)` agree to within an ulp (probability ~1e-16 per wedge draw).
-#ifndef GP_ZIG_OCML
-#define GP_ZIG_OCML 0
-#endif
-__device__ __forceinline__ double zexp(double y) {
-#if GP_ZIG_OCML
-  return exp(y);
-#else
-  const double k = rint(y * 1.4426950408889634);               // y = k ln2 + r, |r| <= ln2 / 2
-  const double r = fma(-k, 1.9082149292705877e-10, fma(-k, 0.6931471803691238, y));  // Cody-Waite ln2 hi / lo
-  double q = 1.6059043836821613e-10;                           // 1/13!, Horner to 1/0!
-  q = fma(q, r, 2.08767569878681e-09);
-  q = fma(q, r, 2.505210838544172e-08);
-  q = fma(q, r, 2.755731922398589e-07);
-  q = fma(q, r, 2.7557319223985893e-06);
-  q = fma(q, r, 2.48015873015873e-05);
-  q = fma(q, r, 0.0001984126984126984);
-  q = fma(q, r, 0.001388888888888889);
-  q = fma(q, r, 0.008333333333333333);
-  q = fma(q, r, 0.041666666666666664);
-  q = fma(q, r, 0.16666666666666666);
-  q = fma(q, r, 0.5);
-  q = fma(q, r, 1.0);
-  q = fma(q, r, 1.0);
-  return ldexp(q, (int)k);
-#endif
-}
+// the CPU test against libm (tests/test_log1p_cpu.py). exp of the wedge test: glibc 2.35's exp restated
+// (gp_libm.h, pinned against libm by tests/test_libm_cpu.py), so wedge accepts / rejects are numpy's exactly.
+__device__ __forceinline__ double zexp(double y) { return gp_libm::exp<true>(y); }
 GP_HD int32_t zhi(double x) { return (int32_t)(__builtin_bit_cast(uint64_t, x) >> 32); }
 GP_HD double zset_hi(double x, int32_t h) {
   return __builtin_bit_cast(double, (__builtin_bit_cast(uint64_t, x) & 0xFFFFFFFFull) | ((uint64_t)(uint32_t)h << 32));

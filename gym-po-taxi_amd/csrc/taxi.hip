@@ -30,6 +30,7 @@
 #include <vector>
 
 #include "gp_internal.h"
+#include "gp_libm.h"
 
 namespace {
 
@@ -237,9 +238,10 @@ __device__ __forceinline__ void write_onehot_wave(uint8_t* __restrict__ out, int
 }
 
 // Per-block metrics into the block's own slot (the grid is persistent: block b owns slot b).
+template <int NW = WAVES>
 __device__ void taxi_metrics(const TaxiDev& p, float rsum, uint32_t eps, uint32_t lens, uint32_t nst) {
-  __shared__ float s_r[WAVES];
-  __shared__ uint32_t s_e[WAVES], s_l[WAVES], s_n[WAVES];
+  __shared__ float s_r[NW];
+  __shared__ uint32_t s_e[NW], s_l[NW], s_n[NW];
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) {
     rsum += __shfl_xor(rsum, d, 64);
@@ -253,7 +255,7 @@ __device__ void taxi_metrics(const TaxiDev& p, float rsum, uint32_t eps, uint32_
   if (threadIdx.x == 0) {
     float r = 0.f;
     unsigned long long e = 0, l = 0, n = 0;
-    for (int w = 0; w < WAVES; ++w) { r += s_r[w]; e += s_e[w]; l += s_l[w]; n += s_n[w]; }
+    for (int w = 0; w < NW; ++w) { r += s_r[w]; e += s_e[w]; l += s_l[w]; n += s_n[w]; }
     TaxiSlot& m = p.mslot[blockIdx.x];
     m.return_sum += (double)r;
     m.episodes += e;
@@ -439,6 +441,354 @@ __global__ void resize_area_kernel(ResizeArea p, uint8_t* dst) {
   dst[(size_t)dy * p.dpitch + (size_t)dx * p.ch + k] = (uint8_t)min(max(v, 0), 255);
 }
 
+// ------------------------------------------------------------------ numpy mode ----
+// rng_mode "numpy": the reference's own stream (extended_taxi.py:281-286, 344-364), draw for draw, so that a seeded
+// run reproduces TaxiVecEnv's obs / rewards / dones and its final PCG64 state. One workgroup of NP_TPB threads
+// runs K steps per launch:
+//  1. transitions of every env (coalesced 1024-env tiles), each tile's task completions (tc) and resets (rs)
+//     ranked in env order by a workgroup scan;
+//  2. _reset_passenger_and_destination: integers(L, b1) for p, then for d, then the `while d == p` redraws,
+//     numpy's buffered 32-bit Lemire draws (distributions.c random_bounded_uint64_fill -> buffered_bounded_lemire_
+//     uint32 on next_uint32) -- serial on one lane (a handful per step);
+//  3. _reset_mask: multinomial(ns, state_distribution, b2).argmax(-1), numpy's random_multinomial: per valid
+//     category in order a random_binomial(p_j / remaining_p, dn) by inversion (random_binomial_inversion, one
+//     next_double per try, q^n = exp(n log q) with glibc's exp restated in gp_libm.h), stopping when dn hits 0.
+//     A row draws C0 doubles (one per drawn category) unless it stops early or an inversion restarts, so rows are
+//     walked SPECULATIVELY: lane (l, delta) walks row r0 + l from stream offset C0 l - delta; lane 0 then chains
+//     the rows whose guessed offset was right (delta = the deficit of the rows before) and the next round starts
+//     after them. 64 rows x 16 deficits per round; the deficit grows ~0.25 per row.
+//  4. the task / episode resets applied, observations written.
+// Host tables per category (p_j, q_j = 1 - p_j, log q_j with the C library's log, flipped when p_j > 0.5 as
+// random_binomial does) keep every dn-independent value identical to numpy's.
+constexpr int NP_TPB = 1024;
+constexpr int NP_WAVES = NP_TPB / 64;
+constexpr int SPEC_DEF = 16;                   // deficits per speculative row
+constexpr int SPEC_ROWS = NP_TPB / SPEC_DEF;   // rows per round
+constexpr uint32_t NP_INV_CAP = 1u << 20;      // inversion tries before a row is flagged (numpy would loop on)
+
+struct TaxiNpDev {
+  uint64_t* rng;          // [6] state hi, lo, inc hi, lo, has_uint32, uinteger
+  const uint8_t* mtab;    // category tables (staged into LDS): pp f64 | q f64 | lq f64 | cat u16 | flip u8
+  int32_t off_pp, off_q, off_lq, off_cat, off_flip, mtab_bytes;
+  int32_t C0;             // categories a row draws when it neither stops early nor restarts
+  int32_t n;              // balls per row (= ns)
+  int32_t last;           // the last category (ns - 1): count dn if the row ends with dn > 0
+  const PcgJump* jrow;    // [NP_TPB]: jump by C0 l - delta (lane l * SPEC_DEF + delta)
+  const PcgJump* jt;      // radix-64 general jump tables
+  int32_t* rk;            // [B] this step's rank: -1, tc rank, or rs rank | 1 << 30
+  int32_t* vtc;           // [B] tc rank -> p << 16 | d
+  uint16_t* vrs;          // [B] rs rank -> start state
+};
+
+struct NpRng {
+  u128 s, inc;
+  uint32_t has, uval;
+};
+// pcg64_next32: the buffered high half first
+__device__ __forceinline__ uint32_t np_next32(NpRng& g) {
+  if (g.has) {
+    g.has = 0;
+    return g.uval;
+  }
+  g.s = pcg_step(g.s, g.inc);
+  const uint64_t x = pcg_output(g.s);
+  g.has = 1;
+  g.uval = (uint32_t)(x >> 32);
+  return (uint32_t)x;
+}
+// integers(n) with int64 output: random_bounded_uint64_fill(rng = n - 1) -> buffered_bounded_lemire_uint32
+__device__ __forceinline__ uint32_t np_integers(NpRng& g, uint32_t n) {
+  if (n <= 1) return 0;  // rng == 0: no draw
+  uint64_t m = (uint64_t)np_next32(g) * n;
+  uint32_t left = (uint32_t)m;
+  if (left < n) {
+    const uint32_t thr = (0xFFFFFFFFu - (n - 1)) % n;
+    while (left < thr) {
+      m = (uint64_t)np_next32(g) * n;
+      left = (uint32_t)m;
+    }
+  }
+  return (uint32_t)(m >> 32);
+}
+__device__ __forceinline__ double np_next_double(u128& s, u128 inc) {
+  s = pcg_step(s, inc);
+  return (double)(pcg_output(s) >> 11) * (1.0 / 9007199254740992.0);
+}
+
+struct NpCats {
+  const double *pp, *q, *lq;
+  const uint16_t* cat;
+  const uint8_t* flip;
+  const uint64_t* etab;  // exp table (LDS copy)
+};
+
+// One multinomial row from state s: the argmax category; `used` = doubles drawn.
+__device__ __forceinline__ uint32_t np_row(const TaxiNpDev& q, const NpCats& c, u128 s, u128 inc, uint32_t& used,
+                                           uint32_t& flags) {
+#pragma clang fp contract(off)
+  int64_t dn = q.n, best = -1;
+  uint32_t arg = 0, u = 0;
+  for (int k = 0; k < q.C0; ++k) {
+    const double pp = c.pp[k];
+    int64_t X = 0;
+    if (pp * (double)dn <= 30.0) {  // random_binomial -> random_binomial_inversion(dn, pp)
+      const double qq = c.q[k];
+      const double qn = gp_libm::exp<true>((double)dn * c.lq[k], c.etab);
+      const double np = (double)dn * pp;
+      const double bnd = np + 10.0 * __builtin_sqrt(np * qq + 1.0);
+      const int64_t bound = (int64_t)((double)dn < bnd ? (double)dn : bnd);
+      double px = qn, U = np_next_double(s, inc);
+      ++u;
+      uint32_t tries = 0;
+      while (U > px) {
+        ++X;
+        if (X > bound) {
+          X = 0;
+          px = qn;
+          U = np_next_double(s, inc);
+          ++u;
+        } else {
+          U -= px;
+          px = ((double)(dn - X + 1) * pp * px) / ((double)X * qq);
+        }
+        if (++tries > NP_INV_CAP) {
+          flags |= GP_DERR_BTPE;
+          break;
+        }
+      }
+    } else {
+      flags |= GP_DERR_BTPE;  // numpy's BTPE: not restated
+    }
+    if (c.flip[k]) X = dn - X;
+    if (X > best) {
+      best = X;
+      arg = c.cat[k];
+    }
+    dn -= X;
+    if (dn <= 0) break;
+  }
+  if (dn > 0 && dn > best) arg = (uint32_t)q.last;
+  used = u;
+  return arg;
+}
+
+// Workgroup scan of two flags over one 1024-env tile: ranks below this thread (env order) and the tile totals.
+__device__ __forceinline__ void np_tile_scan(bool ftc, bool frs, uint32_t* wcnt, uint32_t& rtc, uint32_t& rrs,
+                                             uint32_t& ttc, uint32_t& trs) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t btc = __ballot((int)ftc), brs = __ballot((int)frs);
+  if (lane == 0) wcnt[w] = (uint32_t)__builtin_popcountll(btc) | ((uint32_t)__builtin_popcountll(brs) << 16);
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
+  for (int i = 0; i < NP_WAVES; ++i) {
+    const uint32_t v = wcnt[i];
+    pre += i < w ? v : 0u;
+    tot += v;
+  }
+  const uint32_t mtc = __builtin_amdgcn_mbcnt_hi((uint32_t)(btc >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)btc, 0u));
+  const uint32_t mrs = __builtin_amdgcn_mbcnt_hi((uint32_t)(brs >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)brs, 0u));
+  rtc = (pre & 0xFFFFu) + mtc;
+  rrs = (pre >> 16) + mrs;
+  ttc = tot & 0xFFFFu;
+  trs = tot >> 16;
+  __syncthreads();  // wcnt is reused by the next tile
+}
+
+struct NpShared {
+  uint32_t wcnt[NP_WAVES];
+  uint32_t b1, b2, r0, flags;
+  uint64_t S[2];                // the stream state between phases (hi, lo)
+  uint32_t has, uval;
+  uint16_t res_arg[NP_TPB];
+  uint16_t res_used[NP_TPB];
+};
+
+// The rows of this step's b2 resets (ranks 0..b2-1 -> q.vrs), all threads.
+__device__ void np_reset_rows(const TaxiDev& p, const TaxiNpDev& q, const NpCats& c, NpShared& sh, uint32_t b2) {
+  const int t = threadIdx.x;
+  const int l = t / SPEC_DEF, del = t % SPEC_DEF;
+  const PcgJump jl = q.jrow[t];
+  const u128 inc = mk128(q.rng[2], q.rng[3]);
+  uint32_t r0 = 0;
+  uint32_t flags = 0;
+  while (r0 < b2) {
+    const u128 S = mk128(sh.S[0], sh.S[1]);
+    if (r0 + (uint32_t)l < b2 && !(l == 0 && del > 0)) {
+      uint32_t used = 0;
+      const uint32_t a = np_row(q, c, apply_jump(jl, S), inc, used, flags);
+      sh.res_arg[t] = (uint16_t)a;
+      sh.res_used[t] = (uint16_t)min(used, 65535u);
+    }
+    __syncthreads();
+    if (t == 0) {  // chain the rows whose guessed offset was right
+      int32_t D = 0;
+      uint32_t n = 0;
+      while (r0 + n < b2 && n < (uint32_t)SPEC_ROWS && D >= 0 && D < SPEC_DEF) {
+        const int u = (int)n * SPEC_DEF + D;
+        q.vrs[r0 + n] = sh.res_arg[u];
+        D += q.C0 - (int32_t)sh.res_used[u];
+        ++n;
+      }
+      const u128 S2 = pcg_jump(q.jt, S, (uint32_t)((int64_t)q.C0 * n - D));
+      sh.S[0] = hi64(S2);
+      sh.S[1] = lo64(S2);
+      sh.r0 = r0 + n;
+    }
+    __syncthreads();
+    r0 = sh.r0;
+  }
+  if (flags) atomicOr(p.derr, flags);
+}
+
+// The draws of one step (or of reset(): b1 = 0, every env a reset), between the two env passes.
+__device__ void np_draws(const TaxiDev& p, const TaxiNpDev& q, const NpCats& c, NpShared& sh) {
+  const uint32_t b1 = sh.b1, b2 = sh.b2;
+  if (threadIdx.x == 0) {
+    NpRng g{mk128(sh.S[0], sh.S[1]), mk128(q.rng[2], q.rng[3]), sh.has, sh.uval};
+    if (b1) {  // extended_taxi.py:360-363
+      const uint32_t L = (uint32_t)p.nlocs;
+      for (uint32_t i = 0; i < b1; ++i) q.vtc[i] = (int32_t)(np_integers(g, L) << 16);
+      for (uint32_t i = 0; i < b1; ++i) q.vtc[i] |= (int32_t)np_integers(g, L);
+      bool any = true;
+      for (uint32_t it = 0; any && it < (1u << 20); ++it) {
+        any = false;
+        for (uint32_t i = 0; i < b1; ++i) {
+          const int32_t v = q.vtc[i];
+          if ((v >> 16) == (v & 0xFFFF)) {
+            q.vtc[i] = (v & ~0xFFFF) | (int32_t)np_integers(g, L);
+            any = true;
+          }
+        }
+      }
+    }
+    sh.S[0] = hi64(g.s);
+    sh.S[1] = lo64(g.s);
+    sh.has = g.has;
+    sh.uval = g.uval;
+  }
+  __syncthreads();
+  if (b2) np_reset_rows(p, q, c, sh, b2);
+}
+
+// The numpy-mode rollout / reset: one workgroup, K steps (K = 0: reset(), every env draws a start state).
+template <bool ONEHOT>
+__global__ __launch_bounds__(NP_TPB) void taxi_np_kernel(TaxiDev p, TaxiNpDev q, int K, const int32_t* __restrict__ act,
+                                                         void* __restrict__ obs, float* __restrict__ rew,
+                                                         uint8_t* __restrict__ term, uint8_t* __restrict__ trunc) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  __shared__ NpShared sh;
+  __shared__ uint64_t etab[256];
+  const int t = threadIdx.x;
+  {  // tables: the env tables, then the category tables behind them, the exp table
+    const uint4* s1 = (const uint4*)p.tabs;
+    uint4* d1 = (uint4*)lds;
+    for (int i = t; i < p.tab_bytes / 16; i += NP_TPB) d1[i] = s1[i];
+    const uint4* s2 = (const uint4*)q.mtab;
+    uint4* d2 = (uint4*)(lds + p.tab_bytes);
+    for (int i = t; i < q.mtab_bytes / 16; i += NP_TPB) d2[i] = s2[i];
+    for (int i = t; i < 256; i += NP_TPB) etab[i] = gp_libm::kExpTab[i];
+    if (t == 0) {
+      sh.S[0] = q.rng[0];
+      sh.S[1] = q.rng[1];
+      sh.has = (uint32_t)q.rng[4];
+      sh.uval = (uint32_t)q.rng[5];
+    }
+  }
+  __syncthreads();
+  const uint8_t* mt = lds + p.tab_bytes;
+  const NpCats c{(const double*)(mt + q.off_pp), (const double*)(mt + q.off_q), (const double*)(mt + q.off_lq),
+                 (const uint16_t*)(mt + q.off_cat), mt + q.off_flip, etab};
+  const uint16_t* obs_of = l_obs(lds, p);
+  const int B = p.B, ntile = (B + NP_TPB - 1) / NP_TPB;
+  float rsum = 0.f;
+  uint32_t eps = 0, lens = 0, nst = 0;
+  const int steps = K > 0 ? K : 1;
+  for (int k = 0; k < steps; ++k) {
+    const size_t off = (size_t)k * B;
+    // ---- pass 1: transitions (steps) or every env a reset (reset()), ranked in env order ----
+    uint32_t ntc = 0, nrs = 0;
+    for (int tile = 0; tile < ntile; ++tile) {
+      const int env = tile * NP_TPB + t;
+      const bool live = env < B;
+      bool ftc = false, frs = false;
+      if (K == 0) {
+        frs = live;
+      } else if (live) {
+        uint32_t u = p.st[env];
+        uint32_t s = u & 0xFFFu, nd = (u >> 12) & 0xFu, el = (u >> 16) + 1u;
+        int a = act[off + env];
+        if (action_out_of_range(a, NACT)) flag_bad_action(p.derr);
+        a = a < 0 ? (a == -1 ? NACT : max(a + NACT, 0)) : min(a, NACT - 1);
+        const uint32_t tr = l_trans(lds, p)[s * TCOL + (uint32_t)a];
+        s = tr & 0xFFFu;
+        const uint32_t goal = (tr >> 12) & 1u, bad = (tr >> 13) & 1u;
+        nd += goal;
+        const float r = goal ? p.r_goal : (bad ? p.r_bad : p.r_any);
+        const bool dterm = nd == (uint32_t)p.num_passengers, dtrunc = el > (uint32_t)p.time_limit;
+        rew[off + env] = r;
+        term[off + env] = dterm ? 1 : 0;
+        trunc[off + env] = dtrunc ? 1 : 0;
+        rsum += r;
+        nst += 1u;
+        ftc = goal && !(dterm || dtrunc);
+        frs = dterm || dtrunc;
+        if (frs) {
+          eps += 1u;
+          lens += el;
+        }
+        p.st[env] = s | (nd << 12) | (min(el, 0xFFFFu) << 16);
+      }
+      uint32_t rtc, rrs, ttc, trs;
+      np_tile_scan(ftc, frs, sh.wcnt, rtc, rrs, ttc, trs);
+      if (live) q.rk[env] = ftc ? (int32_t)(ntc + rtc) : (frs ? (int32_t)((nrs + rrs) | (1u << 30)) : -1);
+      ntc += ttc;
+      nrs += trs;
+    }
+    if (t == 0) {
+      sh.b1 = ntc;
+      sh.b2 = nrs;
+    }
+    __syncthreads();
+    // ---- the draws, in the reference's order ----
+    np_draws(p, q, c, sh);
+    __syncthreads();
+    // ---- pass 2: task / episode resets applied, observations ----
+    for (int tile = 0; tile < ntile; ++tile) {
+      const int env = tile * NP_TPB + t;
+      if (env >= B) continue;
+      uint32_t u = p.st[env];
+      const int32_t r = q.rk[env];
+      if (r >= 0) {
+        if (r & (1 << 30)) {
+          u = q.vrs[r & ~(1 << 30)];  // _reset_mask: new start state, elapsed 0, dropoffs 0
+        } else {
+          const int32_t v = q.vtc[r];  // encode(r, c, p, d): taxi cell kept
+          const uint32_t s = u & 0xFFFu;
+          const uint32_t s2 = (s / (uint32_t)p.lpl) * (uint32_t)p.lpl + (uint32_t)(v >> 16) * (uint32_t)p.nlocs +
+                              (uint32_t)(v & 0xFFFF);
+          u = (u & ~0xFFFu) | s2;
+        }
+        p.st[env] = u;
+      }
+      const uint32_t h = obs_of[u & 0xFFFu];
+      if constexpr (!ONEHOT) {
+        reinterpret_cast<int32_t*>(obs)[off + env] = (int32_t)h;
+      } else {
+        uint8_t* row = (uint8_t*)obs + (off + env) * (size_t)p.n_obs;
+        for (int i = 0; i < p.n_obs; ++i) row[i] = (uint32_t)i == h ? 1 : 0;
+      }
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    q.rng[0] = sh.S[0];
+    q.rng[1] = sh.S[1];
+    q.rng[4] = sh.has;
+    q.rng[5] = sh.uval;
+  }
+  if (K > 0) taxi_metrics<NP_WAVES>(p, rsum, eps, lens, nst);
+}
+
 // ------------------------------------------------------------------ host backend ----
 struct TaxiBackend : EnvBackend {
   TaxiDev d{};
@@ -451,6 +801,25 @@ struct TaxiBackend : EnvBackend {
   const int32_t* rp_state = nullptr;
   const int32_t* rp_pd = nullptr;
 
+  // numpy mode (rng_mode GP_RNG_NUMPY): the reference's stream on the device
+  TaxiNpDev np{};
+  DevBuf b_rng, b_mtab, b_jrow, b_jt, b_rk, b_vtc, b_vrs;
+  int np_build(const std::vector<uint16_t>& valid);
+  int np_upload_rng() {
+    GP_HIP_CHECK(hipDeviceSynchronize());
+    const uint64_t r6[6] = {hi64(rng.state), lo64(rng.state), hi64(rng.inc), lo64(rng.inc), rng.has_u32, rng.uinteger};
+    GP_HIP_CHECK(hipMemcpy(b_rng.p, r6, sizeof(r6), hipMemcpyHostToDevice));
+    const std::vector<PcgJump> jt = build_jump_tables(rng.inc);
+    GP_HIP_CHECK(hipMemcpy(b_jt.p, jt.data(), jt.size() * sizeof(PcgJump), hipMemcpyHostToDevice));
+    std::vector<PcgJump> jr(NP_TPB);
+    for (int t = 0; t < NP_TPB; ++t) {
+      const int64_t delta = (int64_t)np.C0 * (t / SPEC_DEF) - t % SPEC_DEF;  // negative: never chained
+      jr[t] = pcg_jump_params((u128)(delta > 0 ? delta : 0), rng.inc);
+    }
+    GP_HIP_CHECK(hipMemcpy(b_jrow.p, jr.data(), jr.size() * sizeof(PcgJump), hipMemcpyHostToDevice));
+    return GP_OK;
+  }
+
   int build(const gp_taxi_config* cfg);
   int seed(const RngHost& r, const uint32_t key[2]) override {
     rng = r;
@@ -459,16 +828,41 @@ struct TaxiBackend : EnvBackend {
     d.key0 = key[0];
     d.key1 = key[1];
     philox_step = 0;
+    if (rng_mode == GP_RNG_NUMPY)
+      if (int e = np_upload_rng()) return e;
     return derr.clear();
   }
   int check() override { return derr.check("taxi"); }
   int set_rng_state(const RngHost& r) override {
-    gp_set_error("taxi: the PCG64 stream is not used on the device (philox / replay modes)");
-    return GP_E_UNSUPPORTED;
+    if (rng_mode != GP_RNG_NUMPY) {
+      gp_set_error("taxi: the PCG64 stream is used on the device only with rng_mode numpy");
+      return GP_E_UNSUPPORTED;
+    }
+    rng = r;
+    return np_upload_rng();
   }
   int get_rng_state(RngHost* r) override {
-    gp_set_error("taxi: the PCG64 stream is not used on the device (philox / replay modes)");
-    return GP_E_UNSUPPORTED;
+    if (rng_mode != GP_RNG_NUMPY) {
+      gp_set_error("taxi: the PCG64 stream is used on the device only with rng_mode numpy");
+      return GP_E_UNSUPPORTED;
+    }
+    GP_HIP_CHECK(hipDeviceSynchronize());
+    uint64_t r6[6];
+    GP_HIP_CHECK(hipMemcpy(r6, b_rng.p, sizeof(r6), hipMemcpyDeviceToHost));
+    r->state = mk128(r6[0], r6[1]);
+    r->inc = mk128(r6[2], r6[3]);
+    r->has_u32 = (uint32_t)r6[4];
+    r->uinteger = (uint32_t)r6[5];
+    return check();
+  }
+  void launch_np(int K, const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc, hipStream_t s) {
+    const size_t lds = (size_t)d.tab_bytes + (size_t)np.mtab_bytes;
+    if (one_hot)
+      hipLaunchKernelGGL((taxi_np_kernel<true>), dim3(1), dim3(NP_TPB), lds, s, d, np, K, (const int32_t*)act, obs,
+                         rew, term, trunc);
+    else
+      hipLaunchKernelGGL((taxi_np_kernel<false>), dim3(1), dim3(NP_TPB), lds, s, d, np, K, (const int32_t*)act, obs,
+                         rew, term, trunc);
   }
   // Largest chunk size the one-hot stream may use for these buffers.
   int chunk_size(const void* obs, int K) const {
@@ -515,7 +909,9 @@ struct TaxiBackend : EnvBackend {
   int reset(void* obs, hipStream_t s) override {
     GP_HIP_CHECK(hipMemsetAsync(d.mslot, 0, sizeof(TaxiSlot) * grid, s));
     const int cs = chunk_size(obs, 1);
-    if (rng_mode == GP_RNG_REPLAY) {
+    if (rng_mode == GP_RNG_NUMPY) {
+      launch_np(0, nullptr, obs, nullptr, nullptr, nullptr, s);
+    } else if (rng_mode == GP_RNG_REPLAY) {
       if (!rp_state) {
         gp_set_error("taxi replay reset needs reset states (gp_set_replay i0)");
         return GP_E_STATE;
@@ -543,7 +939,8 @@ struct TaxiBackend : EnvBackend {
     }
     const int cs = chunk_size(obs, K);
     timer.begin(s);
-    if (rng_mode == GP_RNG_REPLAY) launch_rollout<true>(cs, K, 0, act, obs, rew, term, trunc, s);
+    if (rng_mode == GP_RNG_NUMPY) launch_np(K, act, obs, rew, term, trunc, s);
+    else if (rng_mode == GP_RNG_REPLAY) launch_rollout<true>(cs, K, 0, act, obs, rew, term, trunc, s);
     else launch_rollout<false>(cs, K, philox_step, act, obs, rew, term, trunc, s);
     timer.end(s);
     GP_HIP_CHECK(hipGetLastError());
@@ -782,19 +1179,84 @@ int TaxiBackend::build(const gp_taxi_config* cfg) {
     gp_set_error("taxi: tables (%d B) exceed the LDS budget", d.tab_bytes);
     return GP_E_INVALID;
   }
+  if (rng_mode == GP_RNG_NUMPY)
+    if (int e = np_build(valid)) return e;
   return GP_OK;
+}
+
+// numpy mode: random_multinomial's per-category constants for pvals = state_distribution (1/V on the valid states,
+// extended_taxi.py:205-218). Category j < ns - 1 with pix_j > 0 draws random_binomial(pix_j / remaining_p, dn);
+// remaining_p -= pix_j after each (zeros change nothing). The flip and q = 1 - p are random_binomial's, log q is
+// the C library's (random_binomial_inversion: qn = exp(n * log(q))).
+int TaxiBackend::np_build(const std::vector<uint16_t>& valid) {
+  const int ns = d.ns, V = (int)valid.size();
+  const double pix = 1.0 / (double)V;  // state_distribution[valid] += 1; /= sum (exactly V)
+  std::vector<double> pp, qv, lq;
+  std::vector<uint16_t> cat;
+  std::vector<uint8_t> flip;
+  double rem = 1.0;
+  size_t vi = 0;
+  for (int j = 0; j + 1 < ns; ++j) {
+    const bool isv = vi < valid.size() && valid[vi] == j;
+    if (isv) {
+      ++vi;
+      const double p = pix / rem;
+      const bool fl = p > 0.5;
+      const double pb = fl ? 1.0 - p : p;
+      pp.push_back(pb);
+      qv.push_back(1.0 - pb);
+      lq.push_back(std::log(1.0 - pb));
+      cat.push_back((uint16_t)j);
+      flip.push_back(fl ? 1 : 0);
+      rem -= pix;
+    }
+  }
+  const int C0 = (int)pp.size();
+  if (C0 < 1) {
+    gp_set_error("taxi numpy mode: no category to draw");
+    return GP_E_INVALID;
+  }
+  auto al16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+  const size_t o_pp = 0, o_q = al16(o_pp + 8 * (size_t)C0), o_lq = al16(o_q + 8 * (size_t)C0),
+               o_cat = al16(o_lq + 8 * (size_t)C0), o_flip = al16(o_cat + 2 * (size_t)C0), tot = al16(o_flip + C0);
+  if ((size_t)d.tab_bytes + tot > 96 * 1024) {
+    gp_set_error("taxi numpy mode: tables (%zu B) exceed the LDS budget", (size_t)d.tab_bytes + tot);
+    return GP_E_INVALID;
+  }
+  std::vector<uint8_t> blob(tot, 0);
+  memcpy(blob.data() + o_pp, pp.data(), 8 * (size_t)C0);
+  memcpy(blob.data() + o_q, qv.data(), 8 * (size_t)C0);
+  memcpy(blob.data() + o_lq, lq.data(), 8 * (size_t)C0);
+  memcpy(blob.data() + o_cat, cat.data(), 2 * (size_t)C0);
+  memcpy(blob.data() + o_flip, flip.data(), (size_t)C0);
+  int e;
+  if ((e = b_mtab.upload(blob)) || (e = b_rng.alloc(64)) || (e = b_jrow.alloc(sizeof(PcgJump) * NP_TPB)) ||
+      (e = b_jt.alloc(sizeof(PcgJump) * JT_LEVELS * JT_RADIX)) || (e = b_rk.alloc((size_t)B * 4 + 16)) ||
+      (e = b_vtc.alloc((size_t)B * 4 + 16)) || (e = b_vrs.alloc((size_t)B * 2 + 16)))
+    return e;
+  np.rng = b_rng.as<uint64_t>();
+  np.mtab = b_mtab.as<uint8_t>();
+  np.off_pp = (int)o_pp;
+  np.off_q = (int)o_q;
+  np.off_lq = (int)o_lq;
+  np.off_cat = (int)o_cat;
+  np.off_flip = (int)o_flip;
+  np.mtab_bytes = (int)tot;
+  np.C0 = C0;
+  np.n = ns;
+  np.last = ns - 1;
+  np.jrow = b_jrow.as<PcgJump>();
+  np.jt = b_jt.as<PcgJump>();
+  np.rk = b_rk.as<int32_t>();
+  np.vtc = b_vtc.as<int32_t>();
+  np.vrs = b_vrs.as<uint16_t>();
+  return np_upload_rng();
 }
 
 }  // namespace
 
 std::unique_ptr<EnvBackend> make_taxi_backend(const gp_taxi_config* cfg, int64_t B, int device, int rng_mode,
                                               int* err) {
-  if (rng_mode == GP_RNG_NUMPY) {
-    gp_set_error("taxi: rng_mode numpy is not available on the device (the reference's multinomial reset draws "
-                 "~300 data-dependent binomials per env from one stream); use philox (same law) or replay");
-    *err = GP_E_UNSUPPORTED;
-    return nullptr;
-  }
   if (B < 1 || B > (int64_t)1 << 30) {
     gp_set_error("taxi: num_envs %lld out of range", (long long)B);
     *err = GP_E_INVALID;

@@ -103,6 +103,8 @@ SIGNATURES = {
                                                           ctypes.POINTER(ctypes.c_double)]),
     "gp_standard_normal_words": (ctypes.c_int, [_vp, ctypes.c_int64, _vp, ctypes.c_int64,
                                                 ctypes.POINTER(ctypes.c_int64), _vp]),
+    "gp_exp_libm": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                   ctypes.c_int64, ctypes.c_int]),
     "gp_zig_log1p_neg": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                         ctypes.c_int64]),
     "gp_debug_set": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int64]),

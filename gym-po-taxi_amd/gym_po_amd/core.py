@@ -207,7 +207,8 @@ class NativeVecEnv:
 
         Philox mode, and numpy mode on the grid envs (persistent kernel with a per-step grid
         exchange), run the K steps in ONE fused launch with the env state in registers; C-ROOMS
-        numpy mode runs them in one single-workgroup launch (the stream walk); replay mode issues
+        numpy mode runs a few multi-workgroup stream kernels per step (csrc/crooms.hip xg_*), Taxi
+        numpy mode one single-workgroup launch for the K steps (the stream walk); replay mode issues
         K step launches on the stream. `out` may supply preallocated buffers
         (obs, rew, term(uint8), trunc(uint8)) shaped like `_alloc_outputs(K)`: they are checked
         for shape, dtype, device and contiguity (ValueError otherwise)."""

@@ -4,12 +4,14 @@ Same constructor, attributes, spaces and reset/step semantics as `TaxiVecEnv`; t
 the task/episode resets and the observation builder run in the HIP kernels of libgympo_amd.so
 (csrc/taxi.hip) and return torch-ROCm tensors.
 
-RNG: the reference's reset (`multinomial(ns, p, b).argmax(-1)`, :344-352) consumes a data-dependent
-run of ~300 binomial draws per env from one numpy stream, which no parallel kernel can follow, so
-`rng_mode="numpy"` is not offered for Taxi. `"philox"` (default) draws from the *exact* law of
-that reset (`reset_distribution`, computed in closed form) and from the exact passenger/destination
-law of :354-364; `"replay"` takes caller-decided draws and reproduces the reference's trajectories
-bit-for-bit (how parity is tested). The step itself uses no randomness.
+RNG: `"philox"` (default, the fast path) draws from the *exact* law of the reference's reset
+(`multinomial(ns, p, b).argmax(-1)`, :344-352; `reset_distribution`, computed in closed form) and from the
+exact passenger/destination law of :354-364, counter-based per (env, step). `"numpy"` follows the
+reference's own PCG64 stream draw for draw (one workgroup walks numpy's random_multinomial /
+random_binomial_inversion and the buffered Lemire `integers` calls, csrc/taxi.hip), so a seeded run
+reproduces the reference's trajectories and final `np_random` state; it is a parity mode (a reset
+costs ~300 sequential binomials per env). `"replay"` takes caller-decided draws. The step itself
+uses no randomness.
 
 Extra keyword arguments beyond the reference: `device`, `rng_mode`, `one_hot` (emit the observation
 index one-hot as uint8 [B, n_obs], a build-side encoding).
@@ -133,9 +135,6 @@ class TaxiVecEnv(NativeVecEnv):
         cfg.obs_kind = _lib.GP_OBS_HANSEN if self.hansen else _lib.GP_OBS_TABLE
         cfg.one_hot = int(self.one_hot)
         cfg.reward_goal, cfg.reward_bad, cfg.reward_any = float(reward_goal), float(reward_bad), float(reward_any)
-        if rng_mode == "numpy":
-            raise _lib.GymPoError("TaxiVecEnv: rng_mode='numpy' is not available on the device (the multinomial "
-                                  "reset stream is sequential); use 'philox' (same reset law) or 'replay'")
         self._create(_lib.GP_KIND_TAXI, cfg, num_envs, device, rng_mode)
 
     # ---- reference surface ----

@@ -56,7 +56,7 @@ extern "C" {
 #define GP_KIND_ANTTAG 4
 
 /* ---- RNG modes ---- */
-#define GP_RNG_NUMPY 0   /* seed-identical to numpy Generator(PCG64(SeedSequence(seed))) (GRID only) */
+#define GP_RNG_NUMPY 0   /* seed-identical to numpy Generator(PCG64(SeedSequence(seed))): GRID, CROOMS, TAXI */
 #define GP_RNG_PHILOX 1  /* counter-based Philox4x32-10 keyed by (seed, env, step): fusable rollouts */
 #define GP_RNG_REPLAY 2  /* pre-decided per-env draws supplied by gp_set_replay each step       */
 
@@ -266,8 +266,11 @@ int gp_profile_read_resolver(gp_env* env, double* total_ms, int64_t* n_launches)
  *   env waves store outputs directly), "xmode" (fused exchange variant, default 1), "spin_limit" (polls
  *   before a cross-block wait gives up, 0 = default), "fault_block" (this block never publishes: forces
  *   the timeout path; -1 = off), "fused_tile" (GRID fused kernel envs per tile: 512, 1024 or 2048; 0 = by
- *   size), "no_spw" (GRID fused kernel: 1 = no speculative word windows), "generic_kernels" (CROOMS: 1 = the generic philox rollout even where a compile-time-specialised one
- *   exists). gp_debug_reset restores the defaults. Unknown key: GP_E_INVALID. */
+ *   size), "no_spw" (GRID fused kernel: 1 = no speculative word windows), "generic_kernels" (CROOMS: 1 = the
+ *   generic philox rollout even where a compile-time-specialised one exists), "no_wgrid" (GRID numpy mode: 1 =
+ *   never the windowed kernel csrc/wgrid.hip), "wg_halo" (its window halo: 256 or 512 draws), "wg_bias" (added
+ *   to its predicted reset count: forces window regenerations), "wg_tmode" (its timing-study variants, TM_* in
+ *   csrc/wgrid.hip; results invalid for some). gp_debug_reset restores the defaults. Unknown key: GP_E_INVALID. */
 int gp_debug_set(const char* key, int64_t value);
 void gp_debug_reset(void);
 
@@ -280,6 +283,11 @@ int gp_pcg64_seed_state(const uint32_t* entropy, int n_entropy, const uint32_t* 
  * the C-ROOMS exact mode's ziggurat tail uses on the device: numpy's random_standard_normal calls npy_log1p ->
  * libm, distributions.c). Host-only check entry for the CPU tests. */
 int gp_zig_log1p_neg(const double* u, double* out, int64_t n);
+/* exp(x[i]) exactly as the C library computes it (glibc 2.35 __exp restated, csrc/gp_libm.h: the device copy the
+ * exact-stream paths use where numpy calls libm's exp, e.g. random_binomial_inversion's q^n = exp(n log q),
+ * distributions.c). fma != 0: the -mfma build glibc selects on CPUs with FMA (x86-64 ifunc), else the plain one.
+ * Host-only check entry for the CPU tests. */
+int gp_exp_libm(const double* x, double* out, int64_t n, int fma);
 /* P(argmax = k), k < m, for Multinomial(n, uniform over m) counts, ties to the first index:
  * the law of TaxiVecEnv._reset_mask (extended_taxi.py:344-352). Returns m. */
 int gp_argmax_multinomial_distribution(int m, int n, double* out);

@@ -276,6 +276,23 @@ def test_device_ziggurat_tail_heavy_stream_exact(gpu_device):
     np.testing.assert_array_equal(got.view(np.uint64), want.view(np.uint64))
 
 
+def test_device_ziggurat_wedge_heavy_stream_exact(gpu_device):
+    """A word stream that sends most normals to the wedge test (the top 7 bits of the 52-bit magnitude set, so
+    rabs >= ki[idx] on nearly every layer): ~2e5 accept tests (fi[i-1] - fi[i]) u + fi[i] < exp(-x^2 / 2) over
+    random x in each layer's wedge. The device's exp is glibc's restated (csrc/gp_libm.h); device == the oracle
+    (math.exp = the C library's, as numpy) bit for bit and the same word count."""
+    from oracle.ziggurat import standard_normals
+    n = 300000
+    words = np.random.PCG64(123).random_raw(4 * n)
+    words[::2] |= np.uint64(0x7F) << np.uint64(54)  # bits 54..60: the top 7 of rabs = word bits 9..60
+    want, used_want = standard_normals(words, n)
+    want = np.asarray(want, np.float64)
+    got, used = _device_normals(words, n, gpu_device)
+    assert used == used_want
+    assert used_want > 1.3 * n  # the wedge test drew a second word for a large share of the normals
+    np.testing.assert_array_equal(got.view(np.uint64), want.view(np.uint64))
+
+
 def test_device_ziggurat_words_run_out_mid_normal(gpu_device):
     """A normal whose wedge / tail draws run past the caller's words is NaN, not a value built from
     zero words; with every word it needs it is numpy's value."""
