@@ -2959,31 +2959,7 @@ int GridBackend::build_wgrid(const std::vector<uint16_t>& move, const std::vecto
     if (c < INT32_MIN / 2 || c > INT32_MAX / 2) return GP_OK;
   const int H = dbg.wg_halo == 512 ? 512 : 256;
   const int nc = d.ncells, na = d.nact;
-  // action-failure buckets: the distinct thresholds x > t of the first na - 1 cumulative probabilities of every
-  // row (the last one is never compared: an effective action is at most na - 1), and each row's effective action
-  // per bucket (wg_nthr: at most 2 na - 1 thresholds, else the older fused kernel serves this env)
-  std::vector<uint64_t> ut;
-  for (int a = 0; a < na; ++a)
-    for (int j = 0; j + 1 < na; ++j)
-      if (thr_on_u64(thr[(size_t)a * na + j]) != ~0ull) ut.push_back(thr_on_u64(thr[(size_t)a * na + j]));
-  std::sort(ut.begin(), ut.end());
-  ut.erase(std::unique(ut.begin(), ut.end()), ut.end());
-  const int nt = wg_nthr(na);
-  if ((int)ut.size() > nt) return GP_OK;
-  std::vector<uint64_t> ep((size_t)na, 0);
-  for (int a = 0; a < na; ++a)
-    for (int b = 0; b <= nt; ++b) {  // bucket b: x > ut[i] exactly for i < b
-      uint64_t eff = 0;
-      for (int j = 0; j + 1 < na; ++j) {
-        const uint64_t t = thr_on_u64(thr[(size_t)a * na + j]);
-        if (t == ~0ull) continue;
-        const int i = (int)(std::lower_bound(ut.begin(), ut.end(), t) - ut.begin());
-        eff += i < b ? 1u : 0u;
-      }
-      ep[a] |= eff << (4 * b);
-    }
-  ut.resize((size_t)nt, ~0ull);
-  // LDS image: j32 | jt8 | move | uthr | ep | ocell | avalid, 16-B aligned pieces
+  // LDS image: j32 | jt8 | move | thr | ocell | avalid, 16-B aligned pieces
   WgLds L{};
   int off = 0;
   auto put = [&](int32_t& o, size_t bytes) {
@@ -2993,8 +2969,7 @@ int GridBackend::build_wgrid(const std::vector<uint16_t>& move, const std::vecto
   put(L.j32, sizeof(PcgJump) * 32);
   put(L.jt8, sizeof(PcgJump) * 512);
   put(L.move, (size_t)nc * na * 2);
-  put(L.uthr, (size_t)nt * 8);
-  put(L.ep, (size_t)na * 8);
+  put(L.thr, (size_t)na * na * 8);
   put(L.ocell, (size_t)nc * 4);
   put(L.avalid, agent_valid_h.size() * 2);
   L.total = off;
@@ -3002,8 +2977,9 @@ int GridBackend::build_wgrid(const std::vector<uint16_t>& move, const std::vecto
   if (!wgrid_fits(E / 512, na, lds)) return GP_OK;
   wg_img.assign((size_t)L.total, 0);
   memcpy(wg_img.data() + L.move, move.data(), move.size() * 2);
-  memcpy(wg_img.data() + L.uthr, ut.data(), ut.size() * 8);
-  memcpy(wg_img.data() + L.ep, ep.data(), ep.size() * 8);
+  std::vector<uint64_t> th(thr.size());
+  for (size_t i = 0; i < thr.size(); ++i) th[i] = thr_on_u64(thr[i]);
+  memcpy(wg_img.data() + L.thr, th.data(), th.size() * 8);
   memcpy(wg_img.data() + L.ocell, ocell.data(), ocell.size() * 4);
   memcpy(wg_img.data() + L.avalid, agent_valid_h.data(), agent_valid_h.size() * 2);
   wg_G = (int)(B / E);

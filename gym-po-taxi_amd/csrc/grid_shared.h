@@ -28,12 +28,8 @@ struct alignas(32) MetricSlot {
 constexpr int WG_HMAX = 512;  // largest halo (u64 draws on each side of a predicted window)
 
 struct WgLds {  // byte offsets of the tables in the LDS image (WgParams::limg, copied verbatim into LDS)
-  int32_t j32, jt8, move, uthr, ep, ocell, avalid, total;
+  int32_t j32, jt8, move, thr, ocell, avalid, total;
 };
-// Action failures as buckets: the distinct u64 thresholds of the first NA-1 cumulative probabilities of every
-// action row, ascending (uthr, padded to NT = 2 NA - 1 entries with ~0), bucket(x) = #{i : x > uthr[i]}, and per
-// action a the effective action of every bucket, 4 bits each (ep[a] >> 4 b & 15).
-__host__ __device__ constexpr int wg_nthr(int NA) { return 2 * NA - 1; }
 
 struct WgParams {
   int32_t B, G, E, NS;          // envs, blocks, envs per block, env slots per env lane (E / 512)
@@ -72,11 +68,12 @@ struct WgArgs {  // one launch: K steps, caller-owned action [K][B] and output [
   uint8_t* trunc;
 };
 
-// Dynamic LDS bytes of a launch (tables + windows + coarse states + staging).
-// The window is one byte per draw (its action-failure bucket), double-buffered by step parity.
-__host__ __device__ constexpr int wg_rb_bytes(int E, int H) { return (E + 2 * H + 15) / 16 * 16; }
+// Dynamic LDS bytes of a launch (tables + window + coarse states + staging).
 __host__ __device__ constexpr int wg_dyn_bytes(int tables, int E, int H) {
-  return tables + 2 * wg_rb_bytes(E, H) + 2 * 512 * 16 + 3 * E * 4;
+#ifndef WG_NSTG
+#define WG_NSTG 3
+#endif
+  return tables + (E + 2 * H) * 8 + 2 * 512 * 16 + WG_NSTG * E * 4;
 }
 // Launch on `s` (host; csrc/wgrid.hip). Returns hipError_t as int.
 int wgrid_launch(const WgArgs& a, int NS, int NA, int G, size_t dyn_lds, hipStream_t s);

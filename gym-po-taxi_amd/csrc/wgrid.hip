@@ -9,29 +9,26 @@
 // Design (one workgroup of 11 waves per CU, block beta owns the E = 512 * NS consecutive envs [E beta, E beta + E);
 // env slot i = k * 512 + 64 w + l of env wave w, lane l, slot k):
 //  * The random(B) words a block needs at step t+1 depend on the stream only through the position x_{t+1} =
-//    y_t + used_t (y_t = x_t + B). The words can be computed before used_t is known: during step t the 8 env waves
-//    fill a WINDOW of E + 2H consecutive draws around the predicted position (used predicted from the previous
-//    step's b), one BYTE per draw: its action-failure bucket (#{i : x > uthr[i]} over the distinct thresholds of
-//    the action rows, action_utils.py:84-90 in integer form). After the exchange env i reads window byte
+//    y_t + used_t (y_t = x_t + B). The words themselves can be computed before used_t is known: while step t's
+//    exchange is in flight, the 8 env waves fill a WINDOW of E + 2H consecutive u64 draws around the predicted
+//    position (used predicted from the previous step's b). After the exchange env i reads window word
 //    i + rw_off, rw_off = H + used_t - used_pred; a prediction more than H off regenerates the window exactly
-//    (measured miss rate: tools/window_stats.py). A step's critical path is only
-//      resetter cells of the last step (one jump from a coarse state) -> transitions (window byte -> effective
-//      action from a per-action 4-bit table in registers -> LDS move table) -> granule publish -> all-gather of
-//      the G granules -> block prefix R, next window offset
-//    and the PCG64 work (~40 VALU per draw) runs on the otherwise idle SIMDs during the exchange.
+//    (measured miss rate: tools/window_stats.py). So the step's critical path is only
+//      transitions (window word -> integer threshold compares -> LDS move table) -> granule publish ->
+//      all-gather of the G granules -> the block's resetter cells -> barrier,
+//    and the PCG64 work (~40 VALU per word) runs on the otherwise idle SIMDs during the exchange.
 //  * choice() words: 512 COARSE STATES S(y + 1 + 32 j) (one per env lane, a per-lane constant jump) cover the
-//    first 16384 draws after random(B); a resetter's word is one jump (<= 31 steps, LDS table) from a coarse
-//    state, taken by the resetting env's own lane.
+//    first 16384 draws after random(B); a resetter's word is one jump (<= 31 steps, LDS table) from a coarse state.
 //  * Lemire rejections (p ~ 2.4e-8 per word for 104 cells): each block checks a 62-draw slice of the choice
 //    stream before publishing (slices of all blocks cover 124 G half-words); the granule carries the count.
 //    Any rejection, or more resets than the slices cover, takes the exact slow path: coverage rounds (one more
-//    granule exchange each), the rejected positions listed, and every resetter's word placed past them.
+//    granule exchange each), the rejected positions listed, and every resetter's word placed exactly.
 //  * Outputs: the env waves stage {cell, term, trunc, wall-bump} per env (4 B) in LDS; two store waves turn a
 //    step's staging into obs (per-cell obs table), reward, terminated and truncated with 16-B non-temporal
-//    stores while the next steps run (triple-buffered staging).
-// Synchronisation: no workgroup barrier inside the step loop, only monotone LDS counters and parity-buffered
-// shared fields; cross-block only the tagged 8-B granules (agent-scope relaxed stores / polls,
-// MI355X_MICROARCH.md "handoff" rows), each wait bounded (GridCtl::err flags a grid that cannot make progress).
+//    stores while the next step runs (double-buffered staging).
+// Synchronisation: one workgroup barrier per step (B2, after the exchange) plus LDS counters; cross-block only
+// the tagged 8-B granules (agent-scope relaxed stores / polls, MI355X_MICROARCH.md "handoff" rows), each wait
+// bounded by spin_limit (GridCtl::err flags a grid that cannot make progress).
 #include <stdint.h>
 
 #include "gp_internal.h"
@@ -70,10 +67,11 @@ namespace {
 // drop work (results invalid: measurement only); the others are alternative schedules with exact results.
 constexpr int TM_NOSTORE = 1;   // store waves skip the output copy
 constexpr int TM_NOFILL = 2;    // env waves skip the window fill (stale words)
-constexpr int TM_NOPRIO = 4;    // env waves keep priority 0 on the critical path (default: 2, above the stores)
+constexpr int TM_LATEACT = 4;   // env waves load the next step's actions after the transitions (default: before)
 constexpr int TM_THROTTLE = 8;  // store waves drain their stores after every 16-env chunk (vmcnt(0))
 constexpr int TM_BUSYPOLL = 16; // the all-gather polls without s_sleep
-constexpr int TM_FILLPRIO = 32; // env waves keep priority 2 through the window fill (default: 1)
+constexpr int TM_NOPRIO = 32;   // env waves keep priority 0 through their transitions (default: 2, above the store waves)
+constexpr int TM_EAGERSTORE = 64; // store waves copy a step as soon as it is final (default: after the next transitions)
 
 constexpr int EW = 8;                 // env waves
 constexpr int SW = 2;                 // store waves
@@ -85,26 +83,26 @@ constexpr int SLICE = 62;             // u64 draws per rejection-check slice (12
 constexpr int MAXRP = 512;            // rejected half-word positions the slow path lists
 
 struct WgShared {
-  uint64_t mask[2][8][EW];   // by step parity: the resetter ballots by (slot k, env wave w)
+  uint64_t mask[8][EW];      // this step's resetter ballots by (slot k, env wave w)
   // monotone LDS counters: the waves never meet at a workgroup barrier inside the step loop
   uint32_t trans_done;       // env waves done with a step's transitions (EW per step)
   uint32_t cs_done;          // env waves done with a step's coarse states
+  uint32_t r2s_done;         // env waves done listing a step's resetters in r2s
   uint32_t fill_done;        // env-wave window fills (and exact regenerations) completed
   uint32_t res_done;         // env waves done taking a step's resetter cells (the staging is final)
   uint32_t st_done;          // store-wave step copies completed (SW per step)
   uint32_t sx_ready;         // control wave: step k's S(x) published (k + 1)
-  uint32_t sy_ready;         // control wave: step k's S(y) and step k+1's predicted window base published (k + 1)
-  uint32_t cells_done;       // control wave: step k's exchange finished: R, h, u, fix, next offset (k + 1)
+  uint32_t sy_ready;         // control wave: step k's S(y) and step k+1's window base published (k + 1)
+  uint32_t cells_done;       // control wave: step k's exchange finished, its resetters' cells staged (k + 1)
   uint32_t pro;              // prologue: the first window's base is published
   uint64_t sx[2][2];         // by step parity: S(x_t) (hi, lo), the state at the step's start
   uint64_t sy[2][2];         // by step parity: S(y_t) (hi, lo), the state after the step's random(B)
   uint64_t rw[2][2];         // by parity of the step a window serves: its base state (hi, lo)
-  int32_t rw_off[2];         // by step parity: env i of that step reads window byte i + rw_off
-  uint32_t fix;              // the last exchange: bit 0 slow path, bit 1 window regeneration
-  uint32_t R, h, u, nrp;     // the last exchange: block prefix (half-words), has_uint32 / uinteger at its step's
-                             // start, # rejected positions (slow path)
+  int32_t rw_off[2];         // by step parity: env i of that step reads window word i + rw_off
+  uint32_t fix[2];           // by step parity: bit 0 slow path, bit 1 window regeneration
+  uint32_t R, h, u, nrp;     // slow path: block prefix, has_uint32 / uinteger at the step start, # positions
   uint32_t rp[MAXRP];        // slow path: rejected half-word positions, ascending
-  uint16_t wl[EW][8 * 64];   // per env wave: its resetters (slot << 6 | lane), compacted for the cell draws
+  uint16_t r2s[4096];        // resetter rank in the block -> env slot
 };
 
 // ------------------------------------------------------------------ small helpers ----
@@ -166,6 +164,15 @@ __device__ __forceinline__ void words_to_draws(uint32_t wtot, uint32_t h0, uint3
 // A 53-bit threshold t as a threshold on the full 64-bit draw x: (x >> 11) > t  <=>  x > (t << 11) | 0x7FF.
 __host__ __device__ __forceinline__ uint64_t thr_on_u64(uint64_t t) {
   return t >= (1ull << 53) ? ~0ull : ((t << 11) | 0x7FFull);
+}
+
+// Action -> byte offset of its threshold row (numpy negative indexing; out-of-range actions, an IndexError in
+// the reference (msrooms.py:400 action_matrix[action]), set GP_DERR_ACTION and are clamped).
+template <int NA>
+__device__ __forceinline__ int32_t action_row(int32_t a, uint32_t* derr) {
+  if (action_out_of_range(a, NA)) flag_bad_action(derr);
+  if (a < 0) a += NA;
+  return min(max(a, 0), NA - 1) * NA * 8;
 }
 
 struct Tabs {  // the LDS copy of the tables (pointers resolved once per role)
@@ -277,17 +284,24 @@ __device__ __forceinline__ uint32_t gcnt(uint64_t g) { return (uint32_t)g & 0xFF
 __device__ __forceinline__ uint32_t grej(uint64_t g) { return (uint32_t)(g >> 24) & 0xFFu; }
 
 // Per-launch view of the dynamic LDS (pointers resolved once) and the block geometry.
-constexpr int NSTG = 3;  // staging buffers: the store waves may trail the env waves by up to two steps
+#ifndef WG_NSTG
+#define WG_NSTG 3
+#endif
+#ifndef WG_EAGER_TAIL
+#define WG_EAGER_TAIL 4
+#endif
+#ifndef WG_SUNROLL
+#define WG_SUNROLL 2
+#endif
+constexpr int NSTG = WG_NSTG;  // staging buffers: the store waves may trail the env waves by up to NSTG - 1 steps
 struct Lds {
-  uint8_t* RB0;   // [2 step parities][wg_rb_bytes] window buckets
-  int rbs;        // bytes per window
+  uint64_t* RW;   // [E + 2H] window words
   uint64_t* CS0;  // [2 step parities][512][2] coarse states (lo, hi)
   char* stg0;     // [NSTG][E] staged u32 per env: cell | term << 16 | trunc << 17 | wall bump << 18
   __device__ __forceinline__ Lds(char* dyn, const WgParams& P, int E)
-      : RB0(reinterpret_cast<uint8_t*>(dyn + P.lds.total)), rbs(wg_rb_bytes(E, P.halo)),
-        CS0(reinterpret_cast<uint64_t*>(dyn + P.lds.total + 2 * (size_t)wg_rb_bytes(E, P.halo))),
-        stg0(dyn + P.lds.total + 2 * (size_t)wg_rb_bytes(E, P.halo) + 2 * 512 * 16) {}
-  __device__ __forceinline__ uint8_t* RB(int k) const { return RB0 + (size_t)(k & 1) * rbs; }
+      : RW(reinterpret_cast<uint64_t*>(dyn + P.lds.total)),
+        CS0(reinterpret_cast<uint64_t*>(dyn + P.lds.total + (size_t)(E + 2 * P.halo) * 8)),
+        stg0(dyn + P.lds.total + (size_t)(E + 2 * P.halo) * 8 + 2 * 512 * 16) {}
   __device__ __forceinline__ char* stg(int k, int E) const { return stg0 + (size_t)(k % NSTG) * E * 4; }
   __device__ __forceinline__ uint64_t* CS(int k) const { return CS0 + (size_t)(k & 1) * 1024; }
 };
@@ -384,15 +398,15 @@ __device__ __forceinline__ uint32_t ctrl_slow(const WgParams& P, WgShared& sh, c
 }
 
 // ------------------------------------------------------------------ the control wave ----
-// Per step: S(x) published (sx_ready), the rejection check of its slice, S(y) and the next step's predicted window
-// base (sy_ready), the block's reset count once the env waves' transitions are in, the granule published, the
-// all-gather, the block prefix R and the next window's offset (cells_done), and the next step's
-// S(x) = S(y + used), one jump from a coarse state. Every constant part of a jump (random(B), the block and lane
-// offsets) is folded into per-lane / per-block tables, so only two jumps sit between an exchange and the next
-// granule.
+// Per step: S(x) published (sx_ready: the env waves' coarse states), the rejection check of its slice, the block's
+// reset count once the env waves' transitions are in, the granule published, S(y) and the next window's base
+// (sy_ready), the all-gather, the resetters' cells (cells_done), then the next step's S(x) = J_used(S(y)). Every
+// constant part of a jump (random(B), the block and lane offsets) is folded into per-lane / per-block tables, so
+// the chain from one exchange to the next publish is two table jumps and one per-lane jump.
 template <int NS, int NA>
 __device__ __forceinline__ void wg_ctrl(const WgParams& P, WgShared& sh, const Tabs& tb, const Lds& L, int K) {
   const int lane = threadIdx.x & 63, beta = (int)blockIdx.x, G = (int)gridDim.x;
+  constexpr int E = NS * 512;
   GridCtl* C = P.ctl;
   u128 Sx = mk128(C->s_hi, C->s_lo);
   uint32_t h = C->has_u32, u = C->uinteger;
@@ -418,13 +432,12 @@ __device__ __forceinline__ void wg_ctrl(const WgParams& P, WgShared& sh, const T
   LSTAMP(P, 1);
   for (int k = 0; k < K; ++k) {
     const uint32_t ts = ts0 + (uint32_t)k;
-    if (lane == 0) {  // S(x): the env waves' coarse states
+    if (lane == 0) {
       sh.sx[k & 1][0] = hi64(Sx);
       sh.sx[k & 1][1] = lo64(Sx);
       lds_release();
       __hip_atomic_store(&sh.sx_ready, (uint32_t)k + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    WSTAMP(P, k, 6);
     // Lemire check of this block's slice of the choice() stream (u64 draws 62 beta + 1 .. + 62 after random(B))
     uint32_t rj = 0;
     if (lane < SLICE) {
@@ -434,8 +447,15 @@ __device__ __forceinline__ void wg_ctrl(const WgParams& P, WgShared& sh, const T
       rj = lemire_rejected(u, nag, thra) ? 1u : 0u;  // the buffered half is hw 0
     }
     const uint32_t rejc = wave_sum(rj);
-    // S(y) and the next step's window, around the used predicted from the last b (the env waves fill it right
-    // after their transitions)
+    WSTAMP(P, k, 6);
+    // this block's reset count, published
+    lds_wait(&sh.trans_done, (uint32_t)EW * (uint32_t)(k + 1), derr);
+    WSTAMP(P, k, 7);
+    const uint32_t cb = wave_sum(lane < NS * EW ? (uint32_t)__builtin_popcountll(sh.mask[lane >> 3][lane & 7]) : 0u);
+    uint64_t* slots = P.slots + (size_t)(ts & 1u) * 2 * G;
+    publish(P, slots, ts << 6, rejc, cb);
+    WSTAMP(P, k, 8);
+    // while the granules travel: S(y) and the next step's window, around the used predicted from the last b
     const u128 Sy = apply_jump(jB, Sx);
     uint32_t used_p, hp;
     words_to_draws(bprev + bias, h, used_p, hp);
@@ -449,14 +469,6 @@ __device__ __forceinline__ void wg_ctrl(const WgParams& P, WgShared& sh, const T
       lds_release();
       __hip_atomic_store(&sh.sy_ready, (uint32_t)k + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    // this block's reset count, published
-    lds_wait(&sh.trans_done, (uint32_t)EW * (uint32_t)(k + 1), derr);
-    WSTAMP(P, k, 7);
-    const uint32_t cb =
-        wave_sum(lane < NS * EW ? (uint32_t)__builtin_popcountll(sh.mask[k & 1][lane >> 3][lane & 7]) : 0u);
-    uint64_t* slots = P.slots + (size_t)(ts & 1u) * 2 * G;
-    publish(P, slots, ts << 6, rejc, cb);
-    WSTAMP(P, k, 8);
     uint64_t g[4];
     gather(P, slots, ts << 6, g);
     WSTAMP(P, k, 9);
@@ -474,13 +486,36 @@ __device__ __forceinline__ void wg_ctrl(const WgParams& P, WgShared& sh, const T
     const uint32_t rtot = wave_sum(grej(g[0]) + grej(g[1]) + grej(g[2]) + grej(g[3]));
     const bool slow = rtot != 0 || b > 124u * (uint32_t)G;
     uint32_t used, h2;
-    // the env waves take their resetters' words from this step's coarse states (and so does the slow path)
+    const uint64_t* CS = L.CS(k);
     lds_wait(&sh.cs_done, (uint32_t)EW * (uint32_t)(k + 1), derr);
+    // (also before cells_done when nothing is drawn: every env wave has read this step's masks)
+    lds_wait(&sh.r2s_done, (uint32_t)EW * (uint32_t)(k + 1), derr);
     if (!slow) {
       words_to_draws(b, h, used, h2);
+      if (cb) {  // this block's resetters' cells: rank q takes half-word R + q
+        uint16_t* st = reinterpret_cast<uint16_t*>(L.stg(k, E));
+        for (uint32_t q = (uint32_t)lane; q < cb; q += 64u) {
+          const uint32_t hw = R + q;
+          const uint32_t slot = sh.r2s[q];
+          uint32_t word;
+          if (h && hw == 0) {
+            word = u;
+          } else {
+            const uint32_t hh = hw - h;
+            const uint64_t x = pcg_output(draw_state(tb, CS, hh >> 1));
+            word = (hh & 1u) ? (uint32_t)(x >> 32) : (uint32_t)x;
+          }
+          st[2 * slot] = (uint16_t)tb.avalid(lemire_value(word, nag));  // the low half of the staged word
+        }
+      }
     } else {
-      const uint32_t wtot = ctrl_slow(P, sh, tb, L.CS(k), Sy, h, u, b, ts, g);
+      const uint32_t wtot = ctrl_slow(P, sh, tb, CS, Sy, h, u, b, ts, g);
       words_to_draws(wtot, h, used, h2);
+      if (lane == 0) {
+        sh.R = R;
+        sh.h = h;
+        sh.u = u;
+      }
     }
     // the next step's window offset; a window more than H off is regenerated exactly by the env waves
     int32_t off = heff_p + (int32_t)used - (int32_t)used_p;
@@ -496,19 +531,14 @@ __device__ __forceinline__ void wg_ctrl(const WgParams& P, WgShared& sh, const T
       }
     }
     if (lane == 0) {
-      sh.R = R;
-      sh.h = h;
-      sh.u = u;
       sh.rw_off[(k + 1) & 1] = off;
-      sh.fix = fix;
+      sh.fix[k & 1] = fix;
       lds_release();
       __hip_atomic_store(&sh.cells_done, (uint32_t)k + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     WSTAMP(P, k, 10);
-    // the next step's state S(x_{t+1}) = S(y_t + used): one jump from this step's coarse states
-    if (used == 0) Sx = Sy;
-    else if (used <= 16384u) Sx = draw_state(tb, L.CS(k), used - 1u);
-    else Sx = jump_any(tb, Sy, used);
+    // the next step's state S(x_{t+1}) = S(y_t + used)
+    Sx = jump_any(tb, Sy, used);
     if (used) u = (uint32_t)(pcg_output(Sx) >> 32);  // numpy keeps the last drawn high half in uinteger
     h = h2;
     bprev = b;
@@ -531,103 +561,55 @@ struct Acc {
   uint32_t eps = 0, ngoal = 0, nwall = 0, lens = 0;
 };
 
-// The resetters of step k (dn bits, ballots bm) take their choice() cells: rank in the block (prefix of the step's
-// ballots) -> half-word position R + rank (past the listed rejections on the slow path) -> one jump from a coarse
-// state -> Lemire -> valid cell. A wave's resetters (any slots) are first compacted onto its lanes so that one pass
-// draws them all; the cells go to the staging (low half) and back to their owners' registers.
+// Slow path: place this lane's resetters exactly (ranks -> positions past the listed rejections -> words).
 template <int NS>
-__device__ __forceinline__ void take_cells(const WgParams& P, WgShared& sh, const Tabs& tb, const uint64_t* CS, int k,
-                                           char* stg, uint32_t dn, const uint64_t (&bm)[NS], uint32_t (&ae)[NS],
-                                           bool slow) {
-  const int lg = threadIdx.x, lane = lg & 63, w = lg >> 6;
-  const uint32_t c = lane < NS * EW ? (uint32_t)__builtin_popcountll(sh.mask[k & 1][lane >> 3][lane & 7]) : 0u;
-  const uint32_t ex = wave_incl_scan(c) - c;
-  uint32_t pre[NS];
-  uint16_t* wl = sh.wl[w];
-  uint32_t nw = 0;  // this wave's resetters
+__device__ __forceinline__ void wg_env_slow(const WgParams& P, WgShared& sh, const Tabs& tb, const uint64_t* CS,
+                                            int k, char* stg, uint32_t dn, const uint32_t (&pre)[NS],
+                                            const uint64_t (&bm)[NS], uint32_t (&ae)[NS]) {
+  const int lg = threadIdx.x;
+  const u128 Sy = mk128(sh.sy[k & 1][0], sh.sy[k & 1][1]);
+  const uint32_t R = sh.R, h = sh.h, u = sh.u, n = sh.nrp;
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
-    pre[s] = (uint32_t)__builtin_amdgcn_readlane((int)ex, s * EW + w);
-    if ((dn >> s) & 1u) wl[nw + mbcnt(bm[s])] = (uint16_t)((s << 6) | lane);
-    nw += (uint32_t)__builtin_popcountll(bm[s]);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-  const uint32_t R = sh.R, h = sh.h, u = sh.u, n = slow ? sh.nrp : 0u;
-  uint16_t* st16 = reinterpret_cast<uint16_t*>(stg);
-  for (uint32_t i = (uint32_t)lane; i < nw; i += 64u) {
-    const uint32_t e = wl[i], s = e >> 6, l = e & 63u;
-    uint32_t ps = 0;
-    uint64_t bs = 0;
-#pragma unroll
-    for (int ss = 0; ss < NS; ++ss)
-      if ((uint32_t)ss == s) {
-        ps = pre[ss];
-        bs = bm[ss];
-      }
-    uint32_t p = R + ps + (uint32_t)__builtin_popcountll(bs & ((1ull << l) - 1ull));
+    if (!((dn >> s) & 1u)) continue;
+    uint32_t p = R + pre[s] + mbcnt(bm[s]);
     for (uint32_t q = 0; q < n; ++q) p += sh.rp[q] <= p ? 1u : 0u;
     uint32_t word;
     if (h && p == 0) {
       word = u;
     } else {
       const uint32_t hh = p - h, d = hh >> 1;
-      const u128 st = d < 16384u ? draw_state(tb, CS, d)
-                                 : pcg_jump(tb.jt64, mk128(sh.sy[k & 1][0], sh.sy[k & 1][1]), d + 1u);
+      const u128 st = d < 16384u ? draw_state(tb, CS, d) : pcg_jump(tb.jt64, Sy, d + 1u);
       const uint64_t x = pcg_output(st);
       word = (hh & 1u) ? (uint32_t)(x >> 32) : (uint32_t)x;
     }
-    st16[2 * (s * 512 + (uint32_t)w * 64 + l)] = (uint16_t)tb.avalid(lemire_value(word, (uint32_t)P.n_agent));
+    const uint32_t cell = tb.avalid(lemire_value(word, (uint32_t)P.n_agent));
+    reinterpret_cast<uint16_t*>(stg)[2 * (s * 512 + lg)] = (uint16_t)cell;
+    ae[s] = cell;
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-#pragma unroll
-  for (int s = 0; s < NS; ++s)
-    if ((dn >> s) & 1u) ae[s] = st16[2 * (s * 512 + lg)];
 }
 
-// The action-failure bucket of a draw: #{i : x > uthr[i]} (uthr padded with ~0, which no draw exceeds).
-template <int NT>
-__device__ __forceinline__ uint32_t bucket_of(uint64_t x, const uint64_t (&U)[NT]) {
-  uint32_t b = 0;
-#pragma unroll
-  for (int i = 0; i < NT; ++i) b += x > U[i] ? 1u : 0u;
-  return b;
-}
-
-// Fill a window: draw j = m * 512 + lg is the base state advanced by j (this lane: jump by lg, then by 512).
-template <int NT>
-__device__ __forceinline__ void fill_window(uint8_t* RB, const PcgJump& jl, const PcgJump& j512, int nw, u128 base,
-                                            int lg, const uint64_t (&U)[NT]) {
+// Fill the window: word j = m * 512 + lg is the base state advanced by j (this lane: jump by lg, then by 512).
+__device__ __forceinline__ void fill_window(uint64_t* RW, const PcgJump& jl, const PcgJump& j512, int nw, u128 base, int lg) {
   u128 s = apply_jump(jl, base);
   for (int m = 0; m < nw; ++m) {
-    RB[m * 512 + lg] = (uint8_t)bucket_of<NT>(pcg_output(s), U);
+    RW[m * 512 + lg] = pcg_output(s);
     s = apply_jump(j512, s);
   }
 }
 
-// Action -> its row of effective actions by bucket (numpy negative indexing; out-of-range actions, an IndexError
-// in the reference (msrooms.py:400 action_matrix[action]), set GP_DERR_ACTION and are clamped).
-template <int NA>
-__device__ __forceinline__ uint64_t action_eff(const uint64_t* ept, int32_t a, uint32_t* derr) {
-  if (action_out_of_range(a, NA)) flag_bad_action(derr);
-  if (a < 0) a += NA;
-  return ept[min(max(a, 0), NA - 1)];
-}
-
 template <int NS, int NA>
 __device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Tabs& tb, const Lds& L, const char* dyn,
-                                       const int32_t* __restrict__ act, int K, Acc& acc) {
-  constexpr int NT = wg_nthr(NA);
+                                       const int32_t* __restrict__ act, int K, Acc& acc, int32_t* __restrict__ obs,
+                                       float* __restrict__ rew, uint8_t* __restrict__ term,
+                                       uint8_t* __restrict__ trunc) {
   const int lg = threadIdx.x, lane = lg & 63, w = lg >> 6;
   const int beta = (int)blockIdx.x, G = (int)gridDim.x;
   constexpr int E = NS * 512;
   const size_t B = (size_t)E * (size_t)G;
   const size_t e0 = (size_t)beta * E;
-  const uint16_t* mv = reinterpret_cast<const uint16_t*>(dyn + P.lds.move);
-  const uint64_t* ept = reinterpret_cast<const uint64_t*>(dyn + P.lds.ep);
+  const char* thr = dyn + P.lds.thr;
+  const char* mv = dyn + P.lds.move;
   const uint32_t goal = (uint32_t)P.goal, tlim = (uint32_t)P.time_limit;
   uint32_t* derr = &P.ctl->err;
   uint32_t* aeg = P.ae;
@@ -637,126 +619,159 @@ __device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Ta
   // per-lane constant jumps: by lg (window fill) and by 32 lg + 1 (coarse state)
   const PcgJump jrw = P.jlane[2 * lg], jcs = P.jlane[2 * lg + 1];
   uint32_t ae[NS];
-  int32_t anext[NS];
-  uint64_t ep[NS];
+  int32_t arow[NS], anext[NS];
 #pragma unroll
   for (int k = 0; k < NS; ++k) {
     ae[k] = aeg[e0 + (size_t)k * 512 + lg];
     anext[k] = act[e0 + (size_t)k * 512 + lg];
   }
-  lds_barrier();  // P1
-  uint64_t U[NT];
+  // the first window, exact (word 0 = S(x_0 + 1 + E beta - heff)), filled from global data while the other waves
+  // stage the tables (it lies behind them in LDS)
   {
-    const uint64_t* up = reinterpret_cast<const uint64_t*>(dyn + P.lds.uthr);
-#pragma unroll
-    for (int i = 0; i < NT; ++i) {  // wave-uniform: kept in scalar registers
-      const uint64_t v = up[i];
-      U[i] = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32)) << 32) |
-             (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
-    }
+    const GridCtl* C = P.ctl;
+    fill_window(L.RW, jrw, j512, nw, apply_jump(P.jblk[2 * beta + 1], mk128(C->s_hi, C->s_lo)), lg);
   }
+  lds_barrier();  // P1
 #pragma unroll
   for (int k = 0; k < NS; ++k) {
-    ep[k] = action_eff<NA>(ept, anext[k], derr);
+    arow[k] = action_row<NA>(anext[k], derr);
     acc.lens += ae[k] >> 16;  // episode lengths: + elapsed at the start - elapsed at the end + steps
   }
-  lds_wait(&sh.pro, 1u, derr);
-  fill_window<NT>(L.RB(0), jrw, j512, nw, mk128(sh.rw[0][0], sh.rw[0][1]), lg, U);
-  lds_release();
+  lds_wait(&sh.pro, 1u, derr);  // the first window's offset
   if (lane == 0) lds_add(&sh.fill_done, 1u);
   uint32_t fill_target = EW;
   uint64_t bm[NS];
-  uint32_t dn = 0;
-  for (int k = 0; k <= K; ++k) {
-    // ---- the last exchange's outcome: step k-1's resetters take their cells (critical path) ----
-    if (k > 0) {
-      if (w == 0) WSTAMP(P, k, 0);
-      if (!(tmode & TM_NOPRIO)) __builtin_amdgcn_s_setprio(2);
-      lds_wait(&sh.cells_done, (uint32_t)k, derr);
-      if (w == 0) WSTAMP(P, k, 1);
-      const uint32_t fix = sh.fix;
-      uint64_t anyr = 0;
-#pragma unroll
-      for (int s = 0; s < NS; ++s) anyr |= bm[s];
-      if (anyr) take_cells<NS>(P, sh, tb, L.CS(k - 1), k - 1, L.stg(k - 1, E), dn, bm, ae, (fix & 1u) != 0);
-      lds_release();
-      if (lane == 0) lds_add(&sh.res_done, 1u);
-      if (k == K) break;
-      if (fix & 2u) {  // the prediction missed this step's window: regenerate it exactly
-        fill_window<NT>(L.RB(k), jrw, j512, nw, mk128(sh.rw[k & 1][0], sh.rw[k & 1][1]), lg, U);
-        lds_release();
-        if (lane == 0) lds_add(&sh.fill_done, 1u);
-        fill_target += EW;
-      }
-    }
-    if (k + 1 < K) {  // the next step's actions, in flight during this step
+  uint32_t pre[NS];
+  for (int k = 0; k < K; ++k) {
+    char* stg = L.stg(k, E);
+    if (k + 1 < K && !(tmode & TM_LATEACT)) {
 #pragma unroll
       for (int s = 0; s < NS; ++s) anext[s] = act[(size_t)(k + 1) * B + e0 + (size_t)s * 512 + lg];
     }
-    char* stg = L.stg(k, E);
     lds_wait(&sh.fill_done, fill_target, derr);                  // every env wave's part of this step's window
-    if (k >= NSTG) lds_wait(&sh.st_done, (uint32_t)SW * (uint32_t)(k - NSTG + 1), derr);  // staging buffer free
-    if (w == 0) WSTAMP(P, k, 2);
-    // ---- transitions (the critical path): window byte -> effective action -> move table ----
-    {
-      const uint8_t* rb = L.RB(k) + sh.rw_off[k & 1] + lg;
-      uint32_t bk[NS];
+    if (k >= NSTG) lds_wait(&sh.st_done, (uint32_t)SW * (uint32_t)(k - NSTG + 1), derr);  // this staging buffer copied out
+    if (!(tmode & TM_NOPRIO)) __builtin_amdgcn_s_setprio(2);  // the transitions are on the critical path
+    if (w == 0) WSTAMP(P, k, 0);
+    // ---- transitions (the critical path) ----
+    // Phased over the env slots so that their LDS round trips overlap: every slot's window word and threshold
+    // row first, then the effective actions, the move-table entries, and the staged outputs last (a store to
+    // the staging area between two slots' loads would order them: all of it is one LDS array to the compiler).
+    const int32_t off = sh.rw_off[k & 1];
+    uint32_t dn = 0;
+    uint32_t mvo[NS];
 #pragma unroll
-      for (int s = 0; s < NS; ++s) bk[s] = rb[s * 512];
-      uint32_t mm[NS];
+    for (int s = 0; s < NS; ++s) {
+      const uint64_t x = L.RW[s * 512 + lg + off];
+      const char* t = thr + arow[s];
+      uint32_t eb = 0;  // 2 x effective action: #{j : x > thr[a][j]} (integer form of action_utils.py:84-90)
 #pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        const uint32_t eff = (uint32_t)(ep[s] >> (4u * bk[s])) & 15u;
-        mm[s] = mv[(ae[s] & 0xFFFFu) * (uint32_t)NA + eff];
+      for (int j = 0; j + 1 < NA; j += 2) {
+        const ulonglong2 tt = *reinterpret_cast<const ulonglong2*>(t + 8 * j);
+        eb = x > tt.x ? (uint32_t)(2 * (j + 1)) : eb;
+        if (j + 2 < NA) eb = x > tt.y ? (uint32_t)(2 * (j + 2)) : eb;
       }
-      uint32_t sv[NS];
-      dn = 0;
-#pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        const uint32_t m = mm[s];
-        const uint32_t nc = m & 0x7FFFu, blocked = m >> 15;
-        const uint32_t el = (ae[s] >> 16) + 1u;
-        const bool term = nc == goal, trunc = el > tlim, done = term || trunc;
-        sv[s] = nc | ((uint32_t)term << 16) | ((uint32_t)trunc << 17) | (blocked << 18);
-        ae[s] = done ? nc : (nc | (el << 16));
-        bm[s] = ballot(done);
-        dn |= (uint32_t)done << s;
-        acc.ngoal += term ? 1u : 0u;
-        acc.nwall += (blocked && !term) ? 1u : 0u;
-      }
-      if (lane == 0) {
-#pragma unroll
-        for (int s = 0; s < NS; ++s) sh.mask[k & 1][s][w] = bm[s];
-      }
-#pragma unroll
-      for (int s = 0; s < NS; ++s) reinterpret_cast<uint32_t*>(stg)[s * 512 + lg] = sv[s];
-      acc.eps += (uint32_t)__builtin_popcount(dn);
+      mvo[s] = (ae[s] & 0xFFFFu) * (2 * NA) + eb;
     }
+    uint32_t mm[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) mm[s] = *reinterpret_cast<const uint16_t*>(mv + mvo[s]);
+    uint32_t sv[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const uint32_t m = mm[s];
+      const uint32_t nc = m & 0x7FFFu, blocked = m >> 15;
+      const uint32_t el = (ae[s] >> 16) + 1u;
+      const bool term = nc == goal, trunc = el > tlim, done = term || trunc;
+      sv[s] = nc | ((uint32_t)term << 16) | ((uint32_t)trunc << 17) | (blocked << 18);
+      ae[s] = done ? nc : (nc | (el << 16));
+      bm[s] = ballot(done);
+      dn |= (uint32_t)done << s;
+      acc.ngoal += term ? 1u : 0u;
+      acc.nwall += (blocked && !term) ? 1u : 0u;
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s) sh.mask[s][w] = bm[s];
+    }
+#pragma unroll
+    for (int s = 0; s < NS; ++s) reinterpret_cast<uint32_t*>(stg)[s * 512 + lg] = sv[s];
+    acc.eps += (uint32_t)__builtin_popcount(dn);
     lds_release();
     if (lane == 0) lds_add(&sh.trans_done, 1u);
-    if (!(tmode & TM_NOPRIO) && !(tmode & TM_FILLPRIO)) __builtin_amdgcn_s_setprio(1);
-    if (w == 0) WSTAMP(P, k, 3);
-    if (w == EW - 1) WSTAMP(P, k, 15);
-    // ---- while the exchange runs: this step's coarse states, the next step's window ----
+    if (!(tmode & TM_NOPRIO)) __builtin_amdgcn_s_setprio(0);
+    if (w == 0) WSTAMP(P, k, 1);
+    // the next step's actions (one step ahead)
+    if (k + 1 < K && (tmode & TM_LATEACT)) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s) anext[s] = act[(size_t)(k + 1) * B + e0 + (size_t)s * 512 + lg];
+    }
+    // ---- while the exchange runs: coarse states, resetter listing, the next step's window ----
     lds_wait(&sh.sx_ready, (uint32_t)k + 1u, derr);
+    if (w == 0) WSTAMP(P, k, 2);
     {
       const u128 cs = apply_jump(jcs, mk128(sh.sx[k & 1][0], sh.sx[k & 1][1]));  // S(x + B + 32 lg + 1)
       reinterpret_cast<ulonglong2*>(L.CS(k))[lg] = ulonglong2{lo64(cs), hi64(cs)};
     }
     lds_release();
     if (lane == 0) lds_add(&sh.cs_done, 1u);
+    if (w == 0) WSTAMP(P, k, 3);
+    lds_wait(&sh.trans_done, (uint32_t)EW * (uint32_t)(k + 1), derr);  // every wave's masks; nobody reads the window now
+    {
+      const uint32_t c = lane < NS * EW ? (uint32_t)__builtin_popcountll(sh.mask[lane >> 3][lane & 7]) : 0u;
+      const uint32_t ex = wave_incl_scan(c) - c;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        pre[s] = (uint32_t)__builtin_amdgcn_readlane((int)ex, s * EW + w);
+        if ((dn >> s) & 1u) sh.r2s[pre[s] + mbcnt(bm[s])] = (uint16_t)(s * 512 + lg);
+      }
+    }
+    lds_release();
+    if (lane == 0) lds_add(&sh.r2s_done, 1u);
     if (w == 0) WSTAMP(P, k, 4);
     if (k + 1 < K) {
       lds_wait(&sh.sy_ready, (uint32_t)k + 1u, derr);
-      if (!(tmode & TM_NOFILL))
-        fill_window<NT>(L.RB(k + 1), jrw, j512, nw, mk128(sh.rw[(k + 1) & 1][0], sh.rw[(k + 1) & 1][1]), lg, U);
+      const u128 Srw = mk128(sh.rw[(k + 1) & 1][0], sh.rw[(k + 1) & 1][1]);
+      if (!(tmode & TM_NOFILL)) fill_window(L.RW, jrw, j512, nw, Srw, lg);
       lds_release();
       if (lane == 0) lds_add(&sh.fill_done, 1u);
       fill_target += EW;
 #pragma unroll
-      for (int s = 0; s < NS; ++s) ep[s] = action_eff<NA>(ept, anext[s], derr);
+      for (int s = 0; s < NS; ++s) arow[s] = action_row<NA>(anext[s], derr);
     }
     if (w == 0) WSTAMP(P, k, 5);
+    if (w == EW - 1) WSTAMP(P, k, 15);
+    // ---- the exchange's outcome: the resetters' cells ----
+    lds_wait(&sh.cells_done, (uint32_t)k + 1u, derr);
+    if (w == 0) WSTAMP(P, k, 11);
+    const uint32_t fix = sh.fix[k & 1];
+    if (fix & 1u) {
+      wg_env_slow<NS>(P, sh, tb, L.CS(k), k, stg, dn, pre, bm, ae);
+    } else {
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+        if ((dn >> s) & 1u) ae[s] = reinterpret_cast<const uint16_t*>(stg)[2 * (s * 512 + lg)];
+    }
+    lds_release();
+    if (lane == 0) lds_add(&sh.res_done, 1u);
+    if (k == K - 1 && !(tmode & TM_NOSTORE)) {  // the launch's last step: its outputs straight from the env waves
+      const uint32_t* st = reinterpret_cast<const uint32_t*>(stg);
+      const size_t base = (size_t)k * B + e0 + (size_t)lg;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        const uint32_t v = st[s * 512 + lg];
+        const size_t e = base + (size_t)s * 512;
+        obs[e] = tb.ocell(v & 0xFFFFu);
+        rew[e] = (v & 0x10000u) ? P.r_goal : ((v & 0x40000u) ? P.r_wall : P.r_step);
+        term[e] = (uint8_t)((v >> 16) & 1u);
+        trunc[e] = (uint8_t)((v >> 17) & 1u);
+      }
+    }
+    if ((fix & 2u) && k + 1 < K) {  // the prediction missed the window: regenerate it exactly
+      fill_window(L.RW, jrw, j512, nw, mk128(sh.rw[(k + 1) & 1][0], sh.rw[(k + 1) & 1][1]), lg);
+      lds_release();
+      if (lane == 0) lds_add(&sh.fill_done, 1u);
+      fill_target += EW;
+    }
   }
 #pragma unroll
   for (int k = 0; k < NS; ++k) {
@@ -784,15 +799,19 @@ __device__ __forceinline__ void wg_store(const WgParams& P, WgShared& sh, const 
   const int tmode = P.tmode;
   uint32_t* derr = &P.ctl->err;
   lds_barrier();  // P1
-  for (int k = 0; k < K; ++k) {
+  for (int k = 0; k + 1 < K; ++k) {  // (the env waves write the last step themselves)
     lds_wait(&sh.res_done, (uint32_t)EW * (uint32_t)(k + 1), derr);
+    // and out of the way of the next step's transitions (the critical path): start once they are done, except for
+    // a launch's last steps, whose copies are the launch's tail
+    if (k + WG_EAGER_TAIL < K && !(tmode & TM_EAGERSTORE))
+      lds_wait(&sh.trans_done, (uint32_t)EW * (uint32_t)(k + 2), derr);
     if (sl < 64) WSTAMP(P, k, 13);
     const uint32_t* st = reinterpret_cast<const uint32_t*>(L.stg(k, E));
     const size_t base = (size_t)k * B + (size_t)beta * E;
     // Lane-contiguous: in every store instruction consecutive lanes write consecutive 16 B (obs, reward) or 4 B
     // (terminated, truncated) of 4 envs each, whole cache lines per instruction (a lane-strided pattern left the
     // lines to be merged from partial writes and ran the output stream at a fraction of the HBM rate).
-#pragma unroll 2
+#pragma unroll WG_SUNROLL
     for (int c = sl; c < E / 4 && !(tmode & TM_NOSTORE); c += SW * 64) {  // 4 envs per lane and iteration
       const uint4 x = reinterpret_cast<const uint4*>(st)[c];
       const uint32_t v[4] = {x.x, x.y, x.z, x.w};
@@ -832,27 +851,30 @@ __global__ __launch_bounds__(TPB) void wgrid_rollout(const WgParams* __restrict_
   constexpr int E = NS * 512;
   if (tid == 0) LSTAMP(P, 0);
   // stage the table image (each thread's 16-B loads in flight before its LDS stores)
-  {
+  // (the control and store waves; the env waves fill their first window meanwhile)
+  if (wid >= EW) {
+    constexpr int CT = (NWAVES - EW) * 64;
+    const int t = tid - EW * 64;
     const int n = P.lds.total >> 4;
     const uint4* s = reinterpret_cast<const uint4*>(P.limg);
     uint4* d = reinterpret_cast<uint4*>(dyn);
-    for (int i0 = tid; i0 < n; i0 += 4 * TPB) {
+    for (int i0 = t; i0 < n; i0 += 4 * CT) {
       uint4 v0, v1, v2, v3;
-      const bool a1 = i0 + TPB < n, a2 = i0 + 2 * TPB < n, a3 = i0 + 3 * TPB < n;
+      const bool a1 = i0 + CT < n, a2 = i0 + 2 * CT < n, a3 = i0 + 3 * CT < n;
       v0 = s[i0];
-      if (a1) v1 = s[i0 + TPB];
-      if (a2) v2 = s[i0 + 2 * TPB];
-      if (a3) v3 = s[i0 + 3 * TPB];
+      if (a1) v1 = s[i0 + CT];
+      if (a2) v2 = s[i0 + 2 * CT];
+      if (a3) v3 = s[i0 + 3 * CT];
       d[i0] = v0;
-      if (a1) d[i0 + TPB] = v1;
-      if (a2) d[i0 + 2 * TPB] = v2;
-      if (a3) d[i0 + 3 * TPB] = v3;
+      if (a1) d[i0 + CT] = v1;
+      if (a2) d[i0 + 2 * CT] = v2;
+      if (a3) d[i0 + 3 * CT] = v3;
     }
   }
-  if (tid == 0) {
-    sh.trans_done = sh.cs_done = sh.fill_done = sh.res_done = sh.st_done = 0;
+  if (tid == EW * 64) {
+    sh.trans_done = sh.cs_done = sh.r2s_done = sh.fill_done = sh.res_done = sh.st_done = 0;
     sh.sx_ready = sh.sy_ready = sh.cells_done = sh.pro = 0;
-    sh.fix = 0;
+    sh.fix[0] = sh.fix[1] = 0;
   }
   const Tabs tb(dyn, P);
   const Lds L(dyn, P, E);
@@ -864,7 +886,7 @@ __global__ __launch_bounds__(TPB) void wgrid_rollout(const WgParams* __restrict_
     __builtin_amdgcn_s_setprio(1);
     wg_store<NS>(P, sh, tb, L, K, obs, rew, term, trunc);
   } else {
-    wg_env<NS, NA>(P, sh, tb, L, dyn, act, K, acc);
+    wg_env<NS, NA>(P, sh, tb, L, dyn, act, K, acc, obs, rew, term, trunc);
   }
   // episode statistics of the launch (env waves; the others contribute zeros)
   float rsum = 0.f;

@@ -9,6 +9,7 @@ on torch's HIP runtime before the first device call, `--spin late` after it.
 """
 import ctypes
 import os
+os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")  # as bench.py
 import sys
 import time
 

@@ -3,16 +3,16 @@
     python gym-po-taxi_amd/build.py --stamps && python tools/wstamps.py [B] [K]
 
 Stamps are s_memrealtime (100 MHz, synchronous across XCDs), per block and step k:
-  env wave 0: 0 step k-1's resetters: wait for the exchange starts, 1 exchange outcome seen, 2 transitions start
-              (cells taken, window and staging ready), 3 transitions done, 4 coarse states done, 5 next window
-              filled; env wave 7: 15 transitions done
-  control:    6 S(x), S(y), next window base published, 7 transitions seen, 8 granule published, 9 all-gather done,
-              10 exchange outcome published (cells_done), 12 next S(x) done
-  store wave: 13 copy start, 14 copy issued
-Launch stamps per block: 0 entry, 1 P1 passed (control), 3 step loop done, 4 kernel end.
+  env wave 0: 0 step start, 1 transitions done, 2 S(y) seen, 3 coarse states done, 4 resetters listed,
+              5 window filled (before B2); env wave 7: 15 window filled
+  control:    6 S(y) + rejection check + window base published, 7 transitions seen, 8 granule publish,
+              9 all-gather done, 10 cells drawn (before B2), 11 after B2, 12 next state done
+  store wave: 13 copy start (after B2), 14 copy issued
+Launch stamps per block: 0 entry, 1 P1 passed (control), 2 P2 passed, 3 step loop done, 4 kernel end.
 """
 import ctypes
 import os
+os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")  # as bench.py
 import sys
 
 import numpy as np
@@ -25,7 +25,11 @@ from gym_po_amd import MultistoryFourRoomsEnv, _lib  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
 K = int(sys.argv[2]) if len(sys.argv) > 2 else 64
-env = MultistoryFourRoomsEnv(B, 1, obs_type="hansen")
+from gym_po_amd._lib import debug_knobs  # noqa: E402
+knobs = dict((kv.split("=")[0], int(kv.split("=")[1])) for kv in os.environ.get("GP_KNOBS", "").split(",") if kv)
+with debug_knobs(**knobs):
+    env = MultistoryFourRoomsEnv(B, 1, obs_type="hansen")
+print(f"knobs {knobs}")
 assert env.query("wgrid") == 1, "the windowed kernel is not eligible for this size"
 G = int(env.query("wgrid_blocks"))
 env.reset(seed=0)
@@ -45,7 +49,8 @@ a = raw[:NS].reshape(256, 64, 16)[:G]
 ls = raw[NS:].reshape(256, 8)[:G]
 t0 = ls[:, 0].min()
 print(f"B={B} K={K} G={G} E={env.query('wgrid_block_envs')} H={env.query('wgrid_halo')}")
-print(f"launch: entry spread {ls[:, 0].max() - t0} ns; P1 passed (max) {ls[:, 1].max() - t0}; loop done (max) {ls[:, 3].max() - t0}; kernel end (max) {ls[:, 4].max() - t0} ns")
+print(f"launch: entry spread {ls[:, 0].max() - t0} ns; P1 passed (max) {ls[:, 1].max() - t0}; P2 passed (max) "
+      f"{ls[:, 2].max() - t0}; loop done (max) {ls[:, 3].max() - t0}; kernel end (max) {ls[:, 4].max() - t0} ns")
 env.set_profiling(True)
 for _ in range(5):
     env.rollout(acts)
@@ -63,24 +68,24 @@ def rep(name, d):
           f"{np.median(d.max(0)):7.0f}")
 
 
-n = kk - 3
-A = a[:, 2:2 + n]          # step k
-N = a[:, 3:3 + n]          # step k + 1
-rep("step (transitions start -> next start)", N[:, :, 2] - A[:, :, 2])
-rep("chain: transitions, wave 0 (2->3)", A[:, :, 3] - A[:, :, 2])
-rep("chain: transitions, wave 7 (2->15)", A[:, :, 15] - A[:, :, 2])
-rep("chain: ctrl sees transitions (wave-0 start->7)", A[:, :, 7] - A[:, :, 2])
-rep("chain: ctrl publish (7->8)", A[:, :, 8] - A[:, :, 7])
-rep("chain: all-gather (8->9)", A[:, :, 9] - A[:, :, 8])
-rep("chain: R, offset, cells_done (9->10)", A[:, :, 10] - A[:, :, 9])
-rep("chain: env sees cells_done (ctrl 10 -> env 1)", N[:, :, 1] - A[:, :, 10])
-rep("chain: cells + waits (env 1 -> 2)", N[:, :, 2] - N[:, :, 1])
-rep("off: coarse states (3->4)", A[:, :, 4] - A[:, :, 3])
-rep("off: next window fill (4->5)", A[:, :, 5] - A[:, :, 4])
-rep("off: slack, fill done -> exchange seen (5 -> next 1)", N[:, :, 1] - A[:, :, 5])
-rep("ctrl: step start -> published (prev 12 -> 6)", N[:, :, 6] - A[:, :, 12])
-pub = A[:, :, 8]
+step = a[:, 3:kk, 0] - a[:, 2:kk - 1, 0]
+rep("step (env wave 0 start -> next start)", step)
+rep("env: transitions (0->1)", x[:, :, 1] - x[:, :, 0])
+rep("env: S(y) wait (1->2)", x[:, :, 2] - x[:, :, 1])
+rep("env: coarse states (2->3)", x[:, :, 3] - x[:, :, 2])
+rep("env: resetter listing (3->4)", x[:, :, 4] - x[:, :, 3])
+rep("env: window fill (4->5)", x[:, :, 5] - x[:, :, 4])
+rep("env: B2 wait (5 -> ctrl 11)", x[:, :, 11] - x[:, :, 5])
+rep("env wave 7 window done - wave 0 (15-5)", x[:, :, 15] - x[:, :, 5])
+rep("ctrl: step-start work (prev 12 -> 6)", a[:, 3:kk, 6] - a[:, 2:kk - 1, 12])
+rep("ctrl: after B2 -> next state (11->12)", x[:, :, 12] - x[:, :, 11])
+rep("ctrl: trans wait (6->7)", x[:, :, 7] - x[:, :, 6])
+rep("ctrl: publish (7->8)", x[:, :, 8] - x[:, :, 7])
+rep("ctrl: gather (8->9)", x[:, :, 9] - x[:, :, 8])
+rep("ctrl: cells (9->10)", x[:, :, 10] - x[:, :, 9])
+rep("ctrl: B2 wait (10->11)", x[:, :, 11] - x[:, :, 10])
+pub = x[:, :, 8]
 print(f"  publish spread across blocks (max-min)       median {np.median(pub.max(0) - pub.min(0)):.0f} ns")
-print(f"  gather done - last publish                   median {np.median(A[:, :, 9] - pub.max(0)[None]):.0f} ns")
-rep("store: copy issue (13->14)", A[:, :, 14] - A[:, :, 13])
-print("block 0, step 10 (ns from transitions start):", (a[0, 10] - a[0, 10, 2]).tolist())
+print(f"  gather done - last publish                   median {np.median(x[:, :, 9] - pub.max(0)[None]):.0f} ns")
+rep("store: copy issue (13->14)", x[:, :, 14] - x[:, :, 13])
+print("block 0, step 10 (ns from env start):", (a[0, 10] - a[0, 10, 0]).tolist())
