@@ -72,6 +72,9 @@ constexpr int TM_THROTTLE = 8;  // store waves drain their stores after every 16
 constexpr int TM_BUSYPOLL = 16; // the all-gather polls without s_sleep
 constexpr int TM_NOPRIO = 32;   // env waves keep priority 0 through their transitions (default: 2, above the store waves)
 constexpr int TM_EAGERSTORE = 64; // store waves copy a step as soon as it is final (default: after the next transitions)
+constexpr int TM_NOCAND = 128;  // no candidate cells during the all-gather (every resetter's cell drawn after it)
+constexpr int TM_STORELOW = 256; // store waves at priority 0 (default 1)
+constexpr int TM_ENVHIGH = 512; // env waves at priority 2 throughout (default: 2 for the transitions, 0 otherwise)
 
 constexpr int EW = 8;                 // env waves
 constexpr int SW = 2;                 // store waves
@@ -81,6 +84,8 @@ constexpr int TPB = NWAVES * 64;      // 704 threads
 constexpr int NL = EW * 64;           // env lanes (512)
 constexpr int SLICE = 62;             // u64 draws per rejection-check slice (124 half-words)
 constexpr int MAXRP = 512;            // rejected half-word positions the slow path lists
+constexpr int NCAND = 512;            // candidate resetter cells drawn during the all-gather (256 u64 draws)
+constexpr uint32_t CAND_W = 192;      // half-words of them before the predicted block prefix
 
 struct WgShared {
   uint64_t mask[8][EW];      // this step's resetter ballots by (slot k, env wave w)
@@ -103,6 +108,7 @@ struct WgShared {
   uint32_t R, h, u, nrp;     // slow path: block prefix, has_uint32 / uinteger at the step start, # positions
   uint32_t rp[MAXRP];        // slow path: rejected half-word positions, ascending
   uint16_t r2s[4096];        // resetter rank in the block -> env slot
+  uint16_t cand[NCAND];      // the cells of choice() half-words cbase .. cbase + NCAND - 1 (predicted block prefix)
 };
 
 // ------------------------------------------------------------------ small helpers ----
@@ -411,6 +417,7 @@ __device__ __forceinline__ void wg_ctrl(const WgParams& P, WgShared& sh, const T
   u128 Sx = mk128(C->s_hi, C->s_lo);
   uint32_t h = C->has_u32, u = C->uinteger;
   uint32_t bprev = C->fb_last;
+  uint32_t Rprev = (uint32_t)(((uint64_t)bprev * (uint64_t)blockIdx.x) / (uint64_t)gridDim.x);  // a first guess
   const uint32_t ts0 = C->wstep + 1u;  // tag step of k = 0 (tags are never 0: the slots start zeroed)
   const PcgJump jr = P.jrej[(size_t)beta * 64 + lane];
   const PcgJump jb = P.jblk[2 * beta], jpro = P.jblk[2 * beta + 1];
@@ -469,6 +476,25 @@ __device__ __forceinline__ void wg_ctrl(const WgParams& P, WgShared& sh, const T
       lds_release();
       __hip_atomic_store(&sh.sy_ready, (uint32_t)k + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
+    // While the granules travel (the longest wait of a step): the cells of the choice() half-words around the block
+    // prefix predicted by the last step's, so that the resetters' cells after the exchange are one LDS read each.
+    // Candidate i is half-word cbase + i; cbase = 2 d0 + h, draws d0 .. d0 + NCAND / 2 - 1 (both halves each).
+    const uint64_t* CS = L.CS(k);
+    lds_wait(&sh.cs_done, (uint32_t)EW * (uint32_t)(k + 1), derr);
+    const uint32_t d0 = min(Rprev > CAND_W + h ? (Rprev - CAND_W - h) >> 1 : 0u, 16384u - NCAND / 2);  // CS reach
+    const uint32_t cbase = 2u * d0 + h;
+    if (!(P.tmode & TM_NOCAND)) {
+#pragma unroll
+      for (int m = 0; m < NCAND / 128; ++m) {
+        const uint32_t j = (uint32_t)(lane + 64 * m);
+        const uint64_t x = pcg_output(draw_state(tb, CS, d0 + j));
+        sh.cand[2 * j] = (uint16_t)tb.avalid(lemire_value((uint32_t)x, nag));
+        sh.cand[2 * j + 1] = (uint16_t)tb.avalid(lemire_value((uint32_t)(x >> 32), nag));
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
     uint64_t g[4];
     gather(P, slots, ts << 6, g);
     WSTAMP(P, k, 9);
@@ -486,8 +512,6 @@ __device__ __forceinline__ void wg_ctrl(const WgParams& P, WgShared& sh, const T
     const uint32_t rtot = wave_sum(grej(g[0]) + grej(g[1]) + grej(g[2]) + grej(g[3]));
     const bool slow = rtot != 0 || b > 124u * (uint32_t)G;
     uint32_t used, h2;
-    const uint64_t* CS = L.CS(k);
-    lds_wait(&sh.cs_done, (uint32_t)EW * (uint32_t)(k + 1), derr);
     // (also before cells_done when nothing is drawn: every env wave has read this step's masks)
     lds_wait(&sh.r2s_done, (uint32_t)EW * (uint32_t)(k + 1), derr);
     if (!slow) {
@@ -497,15 +521,21 @@ __device__ __forceinline__ void wg_ctrl(const WgParams& P, WgShared& sh, const T
         for (uint32_t q = (uint32_t)lane; q < cb; q += 64u) {
           const uint32_t hw = R + q;
           const uint32_t slot = sh.r2s[q];
-          uint32_t word;
-          if (h && hw == 0) {
-            word = u;
+          uint32_t cell;
+          if (hw - cbase < (uint32_t)NCAND && !(P.tmode & TM_NOCAND)) {  // (hw >= cbase >= h: never the buffered half)
+            cell = sh.cand[hw - cbase];
           } else {
-            const uint32_t hh = hw - h;
-            const uint64_t x = pcg_output(draw_state(tb, CS, hh >> 1));
-            word = (hh & 1u) ? (uint32_t)(x >> 32) : (uint32_t)x;
+            uint32_t word;
+            if (h && hw == 0) {
+              word = u;
+            } else {
+              const uint32_t hh = hw - h;
+              const uint64_t x = pcg_output(draw_state(tb, CS, hh >> 1));
+              word = (hh & 1u) ? (uint32_t)(x >> 32) : (uint32_t)x;
+            }
+            cell = tb.avalid(lemire_value(word, nag));
           }
-          st[2 * slot] = (uint16_t)tb.avalid(lemire_value(word, nag));  // the low half of the staged word
+          st[2 * slot] = (uint16_t)cell;  // the low half of the staged word
         }
       }
     } else {
@@ -542,6 +572,7 @@ __device__ __forceinline__ void wg_ctrl(const WgParams& P, WgShared& sh, const T
     if (used) u = (uint32_t)(pcg_output(Sx) >> 32);  // numpy keeps the last drawn high half in uinteger
     h = h2;
     bprev = b;
+    Rprev = R;
     WSTAMP(P, k, 12);
   }
   LSTAMP(P, 3);
@@ -698,7 +729,7 @@ __device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Ta
     acc.eps += (uint32_t)__builtin_popcount(dn);
     lds_release();
     if (lane == 0) lds_add(&sh.trans_done, 1u);
-    if (!(tmode & TM_NOPRIO)) __builtin_amdgcn_s_setprio(0);
+    if (!(tmode & TM_NOPRIO) && !(tmode & TM_ENVHIGH)) __builtin_amdgcn_s_setprio(0);
     if (w == 0) WSTAMP(P, k, 1);
     // the next step's actions (one step ahead)
     if (k + 1 < K && (tmode & TM_LATEACT)) {
@@ -883,7 +914,8 @@ __global__ __launch_bounds__(TPB) void wgrid_rollout(const WgParams* __restrict_
     __builtin_amdgcn_s_setprio(3);  // the exchange is on every step's critical path
     wg_ctrl<NS, NA>(P, sh, tb, L, K);
   } else if (wid > CWAVE) {
-    __builtin_amdgcn_s_setprio(1);
+    if (P.tmode & TM_STORELOW) __builtin_amdgcn_s_setprio(0);
+    else __builtin_amdgcn_s_setprio(1);
     wg_store<NS>(P, sh, tb, L, K, obs, rew, term, trunc);
   } else {
     wg_env<NS, NA>(P, sh, tb, L, dyn, act, K, acc, obs, rew, term, trunc);

@@ -113,12 +113,35 @@ case "$task" in
       i=$((i+1))
       run 300 $O/p$i.log rocprofv3 --pmc $C --output-format csv -d $O/pmc/p$i -o p -- python3 bench.py --no-cpu-baseline --steps 20 --warmup 5
     done
-    python3 tools/pmc_to_json.py $O/pmc grid_rollout_numpy fourrooms_hansen4_B1048576_numpy $O/pmc.json fourrooms 20
+    python3 tools/pmc_to_json.py $O/pmc ${PMC_KERNEL:-wgrid_rollout} fourrooms_hansen4_B1048576_numpy $O/pmc.json fourrooms 20
     cp $O/pmc.json profiles/${R}_pmc_fourrooms_hansen4_B1048576_numpy_K20.json
     run 600 $O/bench_default.log python3 bench.py
     last_json $O/bench_default.log 3000
     run 300 $O/bench_driver.log python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline
     last_json $O/bench_driver.log 3000 ;;
+  pmcset)  # round-end PMC records beside the driver's: fourrooms at 128 steps per launch, taxi, anttag, crooms
+    R=${ROUND:-r03}
+    pm() {  # pm <name> <kernel substring> <config key> <workload> <K> <bench args...>
+      local n=$1 k=$2 c=$3 w=$4 K=$5
+      shift 5
+      local i=0
+      for C in FETCH_SIZE WRITE_SIZE; do
+        i=$((i+1))
+        run 300 $O/$n.p$i.log rocprofv3 --pmc $C --output-format csv -d $O/$n/p$i -o p -- python3 bench.py --no-cpu-baseline "$@"
+      done
+      python3 tools/pmc_to_json.py $O/$n $k $c $O/$n.json $w $K
+      cp $O/$n.json profiles/${R}_pmc_${c}_K${K}.json
+    }
+    pm fr128 wgrid_rollout fourrooms_hansen4_B1048576_numpy fourrooms 128 --steps 1280 --warmup 256 --chunk 128
+    pm taxi taxi_rollout taxi_B4194304_philox taxi 4 --workload taxi
+    pm anttag anttag_rollout anttag_B2097152_philox anttag 64 --workload anttag
+    pm crooms crooms_rollout crooms_B2097152_philox crooms 128 --workload crooms
+    for w in taxi anttag crooms; do
+      run 300 $O/b_$w.log python3 bench.py --no-cpu-baseline --workload $w
+      last_json $O/b_$w.log 1500
+    done
+    run 300 $O/b_steady.log python3 bench.py --no-cpu-baseline --steps 1280 --warmup 256 --chunk 128
+    last_json $O/b_steady.log 1500 ;;
   micro)  # VALU / PCG64 generation costs and the launch fixed costs (prebuilt tools/*.bin), then the latency probe
     for b in mb_pcg mb_valu mb_lat mb_launch; do
       [ -x tools/$b.bin ] && run 120 $O/$b.txt tools/$b.bin && cat $O/$b.txt
