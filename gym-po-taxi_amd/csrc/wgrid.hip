@@ -842,7 +842,13 @@ __device__ __forceinline__ void wg_store(const WgParams& P, WgShared& sh, const 
     // Lane-contiguous: in every store instruction consecutive lanes write consecutive 16 B (obs, reward) or 4 B
     // (terminated, truncated) of 4 envs each, whole cache lines per instruction (a lane-strided pattern left the
     // lines to be merged from partial writes and ran the output stream at a fraction of the HBM rate).
-#pragma unroll WG_SUNROLL
+#if WG_SUNROLL == 4
+#pragma unroll 4
+#elif WG_SUNROLL == 1
+#pragma unroll 1
+#else
+#pragma unroll 2
+#endif
     for (int c = sl; c < E / 4 && !(tmode & TM_NOSTORE); c += SW * 64) {  // 4 envs per lane and iteration
       const uint4 x = reinterpret_cast<const uint4*>(st)[c];
       const uint32_t v[4] = {x.x, x.y, x.z, x.w};
@@ -877,6 +883,9 @@ __global__ __launch_bounds__(TPB) void wgrid_rollout(const WgParams* __restrict_
                                                       uint8_t* __restrict__ term, uint8_t* __restrict__ trunc) {
   __shared__ WgShared sh;
   extern __shared__ __attribute__((aligned(16))) char dyn[];
+  // the step count in a scalar register for the whole launch (opaque to the compiler): the step loops would
+  // otherwise re-read it from the kernarg segment, host memory unless HIP_FORCE_DEV_KERNARG
+  asm volatile("" : "+s"(K));
   const WgParams& P = *Pp;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   constexpr int E = NS * 512;
