@@ -1178,6 +1178,9 @@ constexpr int XGW = XGT / 64;     // waves (bitmap words) per block
 constexpr int XG_LOOK = 64;       // the halo of a normal call's block view (one wave)
 constexpr int XG_SPAN = 32;       // longest slow attempt (a 15-pair tail; else GP_DERR_STREAM)
 constexpr int XG_MIN_ENVS = 4096; // at or below: the one-workgroup kernel (fewer launches per step)
+#ifndef XG_SPLIT_NORMALS
+#define XG_SPLIT_NORMALS 0        // 1: a normal call as two launches (classify, then write; rounds 3's form)
+#endif
 
 struct XgCounts {                 // per-block counts of one producer launch
   uint32_t* bc;                   // [blocks] block counts
@@ -1211,6 +1214,11 @@ struct XgCall {                   // one draw call over stream positions
   int32_t* idst;                  // choice: idst[r]
   uint32_t nv, lthr;              // choice: values, Lemire threshold
   uint32_t* err;                  // device error word (GP_DERR_STREAM)
+  // the fused normal call (xg_norm_fused): tagged per-block counts and 64-block group sums of THIS launch
+  unsigned long long* tbc;        // [blocks] tag << 32 | produced count
+  unsigned long long* tgs;        // [groups] tag << 32 | group sum (written by the group's last arriver)
+  unsigned long long* tacc;       // [groups] arrivals << 40 | count sum (zero between launches)
+  uint32_t tag;                   // this launch's tag (never 0)
 };
 
 // Block-wide sum (every thread gets it). Uses its own LDS; safe to call repeatedly.
@@ -1557,6 +1565,143 @@ __global__ __launch_bounds__(XGT) void xg_norm_classify(XgCall a) {
   if (t == 0) xg_publish(a.pc, blockIdx.x, (need + XGT - 1) / XGT, cnt);
 }
 
+
+// The fused normal call (round 4): N1's classification, then the block's count published with this launch's tag,
+// the counts of the blocks before it waited for (64-block group sums from each group's last arriver + the earlier
+// blocks of its own group: at most 256 + 63 polls, all of lower-index blocks, which the in-order dispatch has
+// started), and N2's indexing and writes from the values still in registers. One launch and no position buffers
+// per normal call instead of two launches. A wait that does not end is flagged (GP_DERR_TIMEOUT) and reads 0.
+__device__ __forceinline__ uint32_t xg_tpoll(const unsigned long long* p, uint32_t tag, uint32_t* err) {
+  for (uint32_t spins = 0;; ++spins) {
+    const unsigned long long v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((uint32_t)(v >> 32) == tag) return (uint32_t)v;
+    if (spins > (1u << 24)) {
+      atomicOr(err, GP_DERR_TIMEOUT);
+      return 0u;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+__device__ __forceinline__ void xg_tpublish(const XgCall& a, int bid, int nblocks, uint32_t cnt) {
+  __hip_atomic_store(&a.tbc[bid], ((unsigned long long)a.tag << 32) | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int g = bid >> 6;
+  const unsigned long long old = atomicAdd(&a.tacc[g], (1ull << 40) | (unsigned long long)cnt);
+  if ((int)(old >> 40) == min(64, nblocks - 64 * g) - 1) {
+    const uint32_t gsum = (uint32_t)(old & ((1ull << 40) - 1ull)) + cnt;
+    __hip_atomic_store(&a.tacc[g], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&a.tgs[g], ((unsigned long long)a.tag << 32) | gsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+__device__ __forceinline__ uint32_t xg_tprefix(const XgCall& a, int bid) {
+  const int g = bid >> 6, t = threadIdx.x;
+  uint32_t x = 0;
+  for (int j = t; j < g; j += XGT) x += xg_tpoll(&a.tgs[j], a.tag, a.err);
+  if (t < bid - 64 * g) x += xg_tpoll(&a.tbc[64 * g + t], a.tag, a.err);
+  return xg_block_sum(x);
+}
+
+__global__ __launch_bounds__(XGT) void xg_norm_fused(XgCall a) {
+  const int64_t n = xg_n(a);
+  const int need = xg_norm_need(a, n);
+  const int bid = blockIdx.x, q0 = bid * XGT;
+  const CrRng s0 = a.st[a.rd];
+  if (n == 0) {  // nothing drawn: the state carries over
+    if (bid == 0 && threadIdx.x == 0) a.st[a.wr] = s0;
+    return;
+  }
+  if (q0 >= need) return;
+  __shared__ XgView v;
+  __shared__ uint64_t hb[2];
+  __shared__ uint64_t pmw[XGW];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  if (t == 64) {  // the halo's base state (wave 1) beside the block's (thread 0, in xg_base_state)
+    const u128 h = q0 >= XG_LOOK ? pcg_jump_ilp(a.jt, mk128(s0.s_hi, s0.s_lo), (uint32_t)(q0 - XG_LOOK)) : (u128)0;
+    hb[0] = hi64(h);
+    hb[1] = lo64(h);
+  }
+  const u128 sb = xg_base_state(a, s0, q0, nullptr);
+  const ZigTabs zt = xg_zig();
+  const u128 inc = xg_inc(s0);
+  double val = 0.0, zf = 0.0;
+  int span = 1;
+#pragma unroll
+  for (int part = 0; part < 2; ++part) {
+    if (part == 1 && t >= XG_LOOK) break;  // wave-uniform (XG_LOOK = one wave)
+    const int i = part == 0 ? XG_LOOK + t : t;
+    const int q = q0 - XG_LOOK + i;
+    const bool live = q >= 0 && q < need;
+    const u128 X = apply_jump(a.wj[t + 1], part == 0 ? sb : mk128(hb[0], hb[1]));
+    double z;
+    const bool slow = live && !zig_fast(zt, pcg_output(X), z);
+    if (part == 0) zf = z;
+    const uint64_t m = __ballot(slow);
+    if (lane == 0) v.bits[i >> 6] = m;
+    if (slow) {
+      int u = 1;
+      double vv = 0.0;
+      const int r = xg_attempt(zt, X, inc, u, vv);
+      if (r < 0) atomicOr(a.err, GP_DERR_STREAM);
+      v.span[i] = (uint16_t)u;
+      v.flag[i] = (uint8_t)(r > 0 ? 2u : 0u);
+      if (part == 0) {
+        val = vv;
+        span = u;
+      }
+    }
+  }
+  __syncthreads();
+  const int i = XG_LOOK + t, q = q0 + t;
+  const bool slow = xv_slow(v, i);
+  int on = 0;
+  if (slow && (on = xv_on_chain(v, i, q0 == 0)) < 0) on = xg_on_chain_abs(a, v, q0, s0, q);
+  const int ih = XG_SPAN + t;
+  int onh = 0;
+  const bool slowh = t < XG_LOOK - XG_SPAN && xv_slow(v, ih);
+  if (slowh && (onh = xv_on_chain(v, ih, q0 == 0)) < 0) onh = xg_on_chain_abs(a, v, q0, s0, q0 - XG_LOOK + ih);
+  __syncthreads();
+  if (slow && on) v.flag[i] |= 1u;
+  if (slowh && onh) v.flag[ih] |= 1u;
+  __syncthreads();
+  bool prod;
+  if (q >= need) {
+    prod = false;
+  } else if (slow) {
+    prod = (v.flag[i] & 3u) == 3u;
+  } else {
+    prod = true;
+    uint64_t m[3];
+    int base;
+    xv_window(v, i - XG_SPAN, i, m, base);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      uint64_t w = m[k];
+      while (w) {
+        const int p = base + 64 * k + __builtin_ctzll(w);
+        w &= w - 1;
+        if ((v.flag[p] & 1u) && p + (int)v.span[p] > i) prod = false;
+      }
+    }
+  }
+  const uint64_t pm = __ballot(prod);
+  if (lane == 0) pmw[wv] = pm;
+  const uint32_t cnt = xg_block_sum(lane == 0 ? (uint32_t)__builtin_popcountll(pm) : 0u);  // (syncs pmw too)
+  const int nb = (need + XGT - 1) / XGT;
+  if (t == 0) xg_tpublish(a, bid, nb, cnt);
+  const int64_t pre = xg_tprefix(a, bid);
+  if (bid == nb - 1 && t == 0 && pre + cnt < n) atomicOr(a.err, GP_DERR_STREAM);
+  if (pre >= n || !prod) return;
+  uint32_t before = __builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u));
+#pragma unroll
+  for (int j = 0; j < XGW; ++j) before += j < wv ? (uint32_t)__builtin_popcountll(pmw[j]) : 0u;
+  const int64_t r = pre + before;
+  if (r >= n) return;
+  a.dst[r] = 0.0 + a.scale * (slow ? val : zf);  // numpy: loc + scale * standard_normal
+  if (r == n - 1) {
+    const uint32_t endpos = (uint32_t)q + (slow ? (uint32_t)span : 1u);
+    xg_put_state(a.st, a.wr, s0, pcg_jump_ilp(a.jt, mk128(s0.s_hi, s0.s_lo), endpos), s0.has_u32, s0.uinteger);
+  }
+}
+
 // N2: every produced normal's index r (prefix of the block counts + its rank in the block) -> dst[r]; the n-th
 // one ends the call. No block waits on another.
 __global__ __launch_bounds__(XGT) void xg_norm_write(XgCall a) {
@@ -1825,6 +1970,8 @@ struct CRoomsBackend : EnvBackend {
   int x_upload_rng(const RngHost& r);
   // multi-workgroup exact mode (B > XG_MIN_ENVS): position buffers, block counts, the env phases' flags
   DevBuf xg_jt, xg_bits, xg_pbits, xg_bstate, xg_span, xg_val, xg_cnt, xg_ebits;
+  DevBuf xg_tbc, xg_tgs, xg_tacc;  // the fused normal call's tagged counts (tacc zero between launches)
+  uint32_t xg_tag = 0;
   int xg_P = 0;                  // positions of a draw call (>= what normal(2B) needs)
   int xg_nbe = 0;                // env blocks
   int xg_slot = 0;               // the stream-state slot holding the current state (0 between API calls)
@@ -1888,8 +2035,17 @@ struct CRoomsBackend : EnvBackend {
     a.scale = scale;
     a.dst = dst;
     const unsigned nbp = (unsigned)(xg_P / XGT);
+#if XG_SPLIT_NORMALS
     hipLaunchKernelGGL(xg_norm_classify, dim3(nbp), dim3(XGT), 0, s, a);
     hipLaunchKernelGGL(xg_norm_write, dim3(nbp), dim3(XGT), 0, s, a);
+#else
+    a.tbc = xg_tbc.as<unsigned long long>();
+    a.tgs = xg_tgs.as<unsigned long long>();
+    a.tacc = xg_tacc.as<unsigned long long>();
+    if (++xg_tag == 0) xg_tag = 1;  // (a wrapped tag could only meet slots 2^32 launches old)
+    a.tag = xg_tag;
+    hipLaunchKernelGGL(xg_norm_fused, dim3(nbp), dim3(XGT), 0, s, a);
+#endif
     xg_slot ^= 1;
     GP_HIP_CHECK(hipGetLastError());
     return GP_OK;
@@ -2405,7 +2561,8 @@ int CRoomsBackend::x_alloc() {
     if ((e = xg_jt.alloc(sizeof(PcgJump) * JT_LEVELS * JT_RADIX)) || (e = xg_bits.alloc((size_t)P / 8)) ||
         (e = xg_pbits.alloc((size_t)P / 8)) || (e = xg_bstate.alloc(16 * nbp)) || (e = xg_span.alloc(2 * (size_t)P)) ||
         (e = xg_val.alloc(8 * (size_t)P)) || (e = xg_cnt.alloc(xg_cnt_bytes())) ||
-        (e = xg_ebits.alloc(2 * 8 * (size_t)xg_nbe * XGW)))
+        (e = xg_ebits.alloc(2 * 8 * (size_t)xg_nbe * XGW)) || (e = xg_tbc.alloc(8 * (nbp + 64))) ||
+        (e = xg_tgs.alloc(8 * (nbp / 64 + 2))) || (e = xg_tacc.alloc(8 * (nbp / 64 + 2))))
       return e;
     GP_HIP_CHECK(hipMemset(xg_cnt.p, 0, xg_cnt_bytes()));  // the group accumulators start (and stay) cleared
   }
