@@ -1179,7 +1179,13 @@ constexpr int XG_LOOK = 64;       // the halo of a normal call's block view (one
 constexpr int XG_SPAN = 32;       // longest slow attempt (a 15-pair tail; else GP_DERR_STREAM)
 constexpr int XG_MIN_ENVS = 4096; // at or below: the one-workgroup kernel (fewer launches per step)
 #ifndef XG_SPLIT_NORMALS
-#define XG_SPLIT_NORMALS 0        // 1: a normal call as two launches (classify, then write; rounds 3's form)
+#define XG_SPLIT_NORMALS 0        // 1: normal / choice calls as two launches each (count, then write; round 3's form)
+#endif
+// Above this many envs a call goes back to two launches: the fused kernel's in-launch prefix is a chain over
+// every earlier block, and at 2^20 envs and up it costs what the second launch saved (A/B on MI355X, DESIGN 6d:
+// 143 vs 194 us/step at 2^17 envs, 568 vs 569 at 2^20, 1035 vs 970 at 2^21).
+#ifndef XG_FUSE_MAX_ENVS
+#define XG_FUSE_MAX_ENVS 1048576
 #endif
 
 struct XgCounts {                 // per-block counts of one producer launch
@@ -1760,6 +1766,46 @@ __global__ __launch_bounds__(XGT) void xg_cho_count(XgCall a) {
   const uint32_t cnt = xg_block_sum((uint32_t)__builtin_popcount(xg_cho_flags(a, s0, q0 + threadIdx.x, need, w)));
   if (threadIdx.x == 0) xg_publish(a.pc, blockIdx.x, (need + XGT - 1) / XGT, cnt);
 }
+// The fused choice call (round 4): C1's count, published with this launch's tag, the prefix over the earlier blocks
+// waited for in-launch (xg_tprefix), then C2's writes: one launch per choice call instead of two.
+__global__ __launch_bounds__(XGT) void xg_cho_fused(XgCall a) {
+  const int64_t n = xg_n(a);
+  const int need = xg_cho_need(a, n);
+  const int bid = blockIdx.x, q0 = bid * XGT;
+  const CrRng s0 = a.st[a.rd];
+  if (n == 0) {
+    if (bid == 0 && threadIdx.x == 0) a.st[a.wr] = s0;
+    return;
+  }
+  if (q0 >= need) return;
+  const int q = q0 + threadIdx.x;
+  const u128 sb = xg_base_state(a, s0, q0, nullptr);
+  const uint64_t w = pcg_output(apply_jump(a.wj[threadIdx.x + 1], sb));
+  const uint32_t f = xg_cho_flags(a, s0, q, need, w);
+  uint32_t tot;
+  const uint32_t off = xg_block_scan((uint32_t)__builtin_popcount(f), tot);
+  const int nb = (need + XGT - 1) / XGT;
+  if (threadIdx.x == 0) xg_tpublish(a, bid, nb, tot);
+  const int64_t pre = xg_tprefix(a, bid);
+  if (bid == nb - 1 && threadIdx.x == 0 && pre + tot < n) atomicOr(a.err, GP_DERR_STREAM);
+  if (pre >= n) return;
+  int64_t r = pre + off;
+  // candidates in stream order: buffered half (code 0), lo of word q (2q + 1), hi (2q + 2)
+  const uint32_t cand[3] = {s0.uinteger, (uint32_t)w, (uint32_t)(w >> 32)};
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    if (!((f >> c) & 1u)) continue;
+    if (r < n) a.idst[r] = (int32_t)lemire_value(cand[c], a.nv);
+    if (r == n - 1) {
+      const uint32_t e = c == 0 ? 0u : 2u * (uint32_t)q + (uint32_t)c;  // the last candidate consumed
+      const uint32_t words = (e + 1u) / 2u;
+      // numpy's next_uint32 buffers the high half of every word it draws and keeps it after handing it out
+      xg_put_state(a.st, a.wr, s0, pcg_jump_ilp(a.jt, mk128(s0.s_hi, s0.s_lo), words), (e & 1u),
+                   e ? (uint32_t)(w >> 32) : s0.uinteger);
+    }
+    ++r;
+  }
+}
 // C2: the draws to idst[r]; the n-th one fixes the next state, has_uint32 and uinteger.
 __global__ __launch_bounds__(XGT) void xg_cho_write(XgCall a) {
   const int64_t n = xg_n(a);
@@ -2035,17 +2081,17 @@ struct CRoomsBackend : EnvBackend {
     a.scale = scale;
     a.dst = dst;
     const unsigned nbp = (unsigned)(xg_P / XGT);
-#if XG_SPLIT_NORMALS
-    hipLaunchKernelGGL(xg_norm_classify, dim3(nbp), dim3(XGT), 0, s, a);
-    hipLaunchKernelGGL(xg_norm_write, dim3(nbp), dim3(XGT), 0, s, a);
-#else
-    a.tbc = xg_tbc.as<unsigned long long>();
-    a.tgs = xg_tgs.as<unsigned long long>();
-    a.tacc = xg_tacc.as<unsigned long long>();
-    if (++xg_tag == 0) xg_tag = 1;  // (a wrapped tag could only meet slots 2^32 launches old)
-    a.tag = xg_tag;
-    hipLaunchKernelGGL(xg_norm_fused, dim3(nbp), dim3(XGT), 0, s, a);
-#endif
+    if (XG_SPLIT_NORMALS || B > XG_FUSE_MAX_ENVS) {
+      hipLaunchKernelGGL(xg_norm_classify, dim3(nbp), dim3(XGT), 0, s, a);
+      hipLaunchKernelGGL(xg_norm_write, dim3(nbp), dim3(XGT), 0, s, a);
+    } else {
+      a.tbc = xg_tbc.as<unsigned long long>();
+      a.tgs = xg_tgs.as<unsigned long long>();
+      a.tacc = xg_tacc.as<unsigned long long>();
+      if (++xg_tag == 0) xg_tag = 1;  // (a wrapped tag could only meet slots 2^32 launches old)
+      a.tag = xg_tag;
+      hipLaunchKernelGGL(xg_norm_fused, dim3(nbp), dim3(XGT), 0, s, a);
+    }
     xg_slot ^= 1;
     GP_HIP_CHECK(hipGetLastError());
     return GP_OK;
@@ -2054,8 +2100,17 @@ struct CRoomsBackend : EnvBackend {
     XgCall a = xg_call(n_host, nsrc, 1);
     a.idst = dst;
     const unsigned nbc = (unsigned)((B / 2 + B / 1024 + 256 + XGT - 1) / XGT);
-    hipLaunchKernelGGL(xg_cho_count, dim3(nbc), dim3(XGT), 0, s, a);
-    hipLaunchKernelGGL(xg_cho_write, dim3(nbc), dim3(XGT), 0, s, a);
+    if (XG_SPLIT_NORMALS || B > XG_FUSE_MAX_ENVS) {
+      hipLaunchKernelGGL(xg_cho_count, dim3(nbc), dim3(XGT), 0, s, a);
+      hipLaunchKernelGGL(xg_cho_write, dim3(nbc), dim3(XGT), 0, s, a);
+    } else {
+      a.tbc = xg_tbc.as<unsigned long long>();
+      a.tgs = xg_tgs.as<unsigned long long>();
+      a.tacc = xg_tacc.as<unsigned long long>();
+      if (++xg_tag == 0) xg_tag = 1;
+      a.tag = xg_tag;
+      hipLaunchKernelGGL(xg_cho_fused, dim3(nbc), dim3(XGT), 0, s, a);
+    }
     xg_slot ^= 1;
     GP_HIP_CHECK(hipGetLastError());
     return GP_OK;

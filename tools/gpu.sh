@@ -13,7 +13,8 @@
 #   bash tools/gpu.sh measure                 driver-config + steady headline lines, MEASURE_WL workloads, VALU costs,
 #                                              CRATE="B ..." C-ROOMS exact-mode rates
 #   bash tools/gpu.sh multi                    bench.py's N>1 path with 2 gloo ranks on one GPU
-# Env: PMC_KERNEL / PMC_CFG / PMC_WORKLOAD for pmc (defaults: the headline kernel and config).
+# Env: PMC_KERNEL / PMC_CFG / PMC_WORKLOAD for pmc (defaults: the headline kernel and config); PMCSET_ONLY="crooms .."
+#      limits pmcset to those workloads.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -124,6 +125,7 @@ case "$task" in
     pm() {  # pm <name> <kernel substring> <config key> <workload> <K> <bench args...>
       local n=$1 k=$2 c=$3 w=$4 K=$5
       shift 5
+      [ -n "$PMCSET_ONLY" ] && [[ " $PMCSET_ONLY " != *" $w "* ]] && return 0
       local i=0
       for C in FETCH_SIZE WRITE_SIZE; do
         i=$((i+1))
@@ -136,10 +138,12 @@ case "$task" in
     pm taxi taxi_rollout taxi_B4194304_philox taxi 4 --workload taxi
     pm anttag anttag_rollout anttag_B2097152_philox anttag 64 --workload anttag
     pm crooms crooms_rollout crooms_B2097152_philox crooms 128 --workload crooms
-    for w in taxi anttag crooms; do
+    for w in ${PMCSET_ONLY:-taxi anttag crooms}; do
+      [ "$w" = fourrooms ] && continue
       run 300 $O/b_$w.log python3 bench.py --no-cpu-baseline --workload $w
       last_json $O/b_$w.log 1500
     done
+    [ -n "$PMCSET_ONLY" ] && [[ " $PMCSET_ONLY " != *" fourrooms "* ]] && exit 0
     run 300 $O/b_steady.log python3 bench.py --no-cpu-baseline --steps 1280 --warmup 256 --chunk 128
     last_json $O/b_steady.log 1500 ;;
   micro)  # VALU / PCG64 generation costs and the launch fixed costs (prebuilt tools/*.bin), then the latency probe
