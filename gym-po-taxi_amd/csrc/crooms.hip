@@ -79,6 +79,7 @@ struct CrDev {
   uint32_t* goal;        // gy | gx << 16 (int16 each; a fixed goal may lie off the grid)
   int32_t* el;
   CrSlot* mslot;
+  int32_t nslot;         // metric slots (the exact-mode step kernel spreads its blocks' atomics over them)
   uint32_t* derr;        // device error word (GP_DERR_*)
   // replay
   const uint64_t* rp_u;
@@ -1188,6 +1189,25 @@ constexpr int XG_MIN_ENVS = 4096; // at or below: the one-workgroup kernel (fewe
 #define XG_FUSE_MAX_ENVS 1048576
 #endif
 
+// GP_STAMPS diagnostic builds (tools/xstamps.py): s_memrealtime stamps (100 MHz, chip-synchronous) by thread 0 of
+// blocks < 1024, per kernel kind (0 action normals, 1 dry step, 2 wall normals, 3 step, 4 choices, 5 resets),
+// overwritten by every launch of that kind (the last step of a rollout is what is read back).
+#ifdef GP_STAMPS
+__device__ unsigned long long* g_xgdbg;
+#define XSTAMP(ty, i)                                                                                    \
+  do {                                                                                                   \
+    if (threadIdx.x == 0 && blockIdx.x < 1024) {                                                         \
+      unsigned long long t_;                                                                             \
+      asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                     \
+      g_xgdbg[((size_t)(ty) * 1024 + blockIdx.x) * 8 + (i)] = t_;                                        \
+    }                                                                                                    \
+  } while (0)
+#else
+#define XSTAMP(ty, i) \
+  do {                \
+  } while (0)
+#endif
+
 struct XgCounts {                 // per-block counts of one producer launch
   uint32_t* bc;                   // [blocks] block counts
   unsigned long long* acc;        // [groups] arrivals << 40 | count sum (zero between launches)
@@ -1225,6 +1245,15 @@ struct XgCall {                   // one draw call over stream positions
   unsigned long long* tgs;        // [groups] tag << 32 | group sum (written by the group's last arriver)
   unsigned long long* tacc;       // [groups] arrivals << 40 | count sum (zero between launches)
   uint32_t tag;                   // this launch's tag (never 0)
+  // the wall-noise extension (round 4): the action-noise call (xinfo set) goes on to draw up to xmax more
+  // normals, scaled by xscale, into xdst with each one's end position (from the call's start) in xend and the
+  // count made in xinfo[0]; the wall-noise call (xg_wall_one) then only sets the stream state when its n <=
+  // xinfo[0], and records its n in xinfo[1] (the next extension asks for 5/4 of it + 1024)
+  double* xdst;
+  uint32_t* xend;
+  uint32_t* xinfo;
+  uint32_t xmax;
+  double xscale;
 };
 
 // Block-wide sum (every thread gets it). Uses its own LDS; safe to call repeatedly.
@@ -1607,10 +1636,18 @@ __device__ __forceinline__ uint32_t xg_tprefix(const XgCall& a, int bid) {
 }
 
 __global__ __launch_bounds__(XGT) void xg_norm_fused(XgCall a) {
+  const int xty = a.nsrc.gs ? 2 : 0;
+  XSTAMP(xty, 0);
+  const CrRng s0 = a.st[a.rd];  // (issued before n's loads and barrier)
   const int64_t n = xg_n(a);
-  const int need = xg_norm_need(a, n);
+  XSTAMP(xty, 1);
   const int bid = blockIdx.x, q0 = bid * XGT;
-  const CrRng s0 = a.st[a.rd];
+  int64_t X = 0;  // the extension's normals past n (the next call's, xg_wall_one)
+  if (a.xinfo) {
+    const int64_t want = a.xinfo[1];
+    X = min((int64_t)a.xmax, want + want / 4 + 1024);
+  }
+  const int need = xg_norm_need(a, n + X);
   if (n == 0) {  // nothing drawn: the state carries over
     if (bid == 0 && threadIdx.x == 0) a.st[a.wr] = s0;
     return;
@@ -1626,6 +1663,7 @@ __global__ __launch_bounds__(XGT) void xg_norm_fused(XgCall a) {
     hb[1] = lo64(h);
   }
   const u128 sb = xg_base_state(a, s0, q0, nullptr);
+  XSTAMP(xty, 2);
   const ZigTabs zt = xg_zig();
   const u128 inc = xg_inc(s0);
   double val = 0.0, zf = 0.0;
@@ -1656,6 +1694,7 @@ __global__ __launch_bounds__(XGT) void xg_norm_fused(XgCall a) {
     }
   }
   __syncthreads();
+  XSTAMP(xty, 3);
   const int i = XG_LOOK + t, q = q0 + t;
   const bool slow = xv_slow(v, i);
   int on = 0;
@@ -1668,6 +1707,7 @@ __global__ __launch_bounds__(XGT) void xg_norm_fused(XgCall a) {
   if (slow && on) v.flag[i] |= 1u;
   if (slowh && onh) v.flag[ih] |= 1u;
   __syncthreads();
+  XSTAMP(xty, 4);
   bool prod;
   if (q >= need) {
     prod = false;
@@ -1693,19 +1733,89 @@ __global__ __launch_bounds__(XGT) void xg_norm_fused(XgCall a) {
   const uint32_t cnt = xg_block_sum(lane == 0 ? (uint32_t)__builtin_popcountll(pm) : 0u);  // (syncs pmw too)
   const int nb = (need + XGT - 1) / XGT;
   if (t == 0) xg_tpublish(a, bid, nb, cnt);
+  XSTAMP(xty, 5);
   const int64_t pre = xg_tprefix(a, bid);
-  if (bid == nb - 1 && t == 0 && pre + cnt < n) atomicOr(a.err, GP_DERR_STREAM);
-  if (pre >= n || !prod) return;
+  XSTAMP(xty, 6);
+  if (bid == nb - 1 && t == 0) {
+    if (pre + cnt < n) atomicOr(a.err, GP_DERR_STREAM);
+    if (X > 0) a.xinfo[0] = (uint32_t)min(X, max((int64_t)0, pre + (int64_t)cnt - n));
+  }
+  if (pre >= n + X || !prod) return;
   uint32_t before = __builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u));
 #pragma unroll
   for (int j = 0; j < XGW; ++j) before += j < wv ? (uint32_t)__builtin_popcountll(pmw[j]) : 0u;
   const int64_t r = pre + before;
-  if (r >= n) return;
+  if (r >= n) {
+    if (r < n + X) {  // the extension: the next call's normals, at its scale, with their end positions
+      a.xdst[r - n] = 0.0 + a.xscale * (slow ? val : zf);
+      a.xend[r - n] = (uint32_t)q + (slow ? (uint32_t)span : 1u);
+    }
+    return;
+  }
   a.dst[r] = 0.0 + a.scale * (slow ? val : zf);  // numpy: loc + scale * standard_normal
   if (r == n - 1) {
     const uint32_t endpos = (uint32_t)q + (slow ? (uint32_t)span : 1u);
     xg_put_state(a.st, a.wr, s0, pcg_jump_ilp(a.jt, mk128(s0.s_hi, s0.s_lo), endpos), s0.has_u32, s0.uinteger);
   }
+  XSTAMP(xty, 7);
+}
+
+// The wall-noise call after an extended action-noise call, in one workgroup (crooms.py:321-325: normal(0.5,
+// (n_oob, 2)), n = 2 * the dry step's wall hits). When the extension made them (n <= xinfo[0]) only the stream
+// state moves, to the end of the extension's n-th normal; otherwise (the first step, or a jump in the wall-hit
+// count past the extension's 5/4 margin) the call is drawn here from the action-noise call's end, one 1024-word
+// window per round (x_normals). One small launch per step instead of a grid-wide normal call.
+__global__ __launch_bounds__(XT) void xg_wall_one(XgCall a, CrExact x) {
+  __shared__ XShared sh;
+  __shared__ uint32_t red[XT / 64];
+  const int t = threadIdx.x;
+  XSTAMP(2, 0);
+  const CrRng s0 = a.st[a.rd];  // the action-noise call's end
+  uint32_t c = 0;
+  for (int j = t; j < (a.nsrc_blocks + 63) / 64; j += XT) c += a.nsrc.gs[j];
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
+  if ((t & 63) == 0) red[t >> 6] = c;
+  __syncthreads();
+  uint32_t tot = 0;
+#pragma unroll
+  for (int i = 0; i < XT / 64; ++i) tot += red[i];
+  const int64_t n = (int64_t)a.nmul * tot;
+  XSTAMP(2, 1);
+  if (t == 0) a.xinfo[1] = (uint32_t)n;
+  if (n == 0) {
+    if (t == 0) a.st[a.wr] = s0;
+    return;
+  }
+  if (n <= (int64_t)a.xinfo[0]) {
+    if (t == 0) {
+      const CrRng sa = a.st[a.wr];  // the action-noise call's start (the slot this call writes)
+      xg_put_state(a.st, a.wr, sa, pcg_jump_ilp(a.jt, mk128(sa.s_hi, sa.s_lo), a.xend[n - 1]), sa.has_u32,
+                   sa.uinteger);
+    }
+    XSTAMP(2, 7);
+    return;
+  }
+  const PcgJump myj = a.wj[t + 1];
+  for (int i = t; i < 768; i += XT) sh.zt[i] = d_zig[i];
+  if (t == 0) {
+    sh.st_hi = s0.s_hi;
+    sh.st_lo = s0.s_lo;
+    sh.has_u32 = s0.has_u32;
+    sh.uinteger = s0.uinteger;
+    sh.err = 0;
+  }
+  __syncthreads();
+  x_normals(sh, x, myj, n, a.scale, a.dst);
+  __syncthreads();
+  if (t == 0) {
+    if (sh.err) atomicOr(a.err, GP_DERR_STREAM);
+    CrRng o = s0;
+    o.s_hi = sh.st_hi;
+    o.s_lo = sh.st_lo;
+    a.st[a.wr] = o;
+  }
+  XSTAMP(2, 6);
 }
 
 // N2: every produced normal's index r (prefix of the block counts + its rank in the block) -> dst[r]; the n-th
@@ -1769,10 +1879,23 @@ __global__ __launch_bounds__(XGT) void xg_cho_count(XgCall a) {
 // The fused choice call (round 4): C1's count, published with this launch's tag, the prefix over the earlier blocks
 // waited for in-launch (xg_tprefix), then C2's writes: one launch per choice call instead of two.
 __global__ __launch_bounds__(XGT) void xg_cho_fused(XgCall a) {
+  XSTAMP(4, 0);
+#ifdef GP_STAMPS
+  {
+    const int rd_ = a.rd;
+    asm volatile("" ::"s"(rd_));
+    XSTAMP(4, 4);
+  }
+#endif
+  const CrRng s0 = a.st[a.rd];  // (issued before n's loads and barrier)
+#ifdef GP_STAMPS
+  asm volatile("" ::"s"(s0.s_lo));
+  XSTAMP(4, 3);
+#endif
   const int64_t n = xg_n(a);
+  XSTAMP(4, 1);
   const int need = xg_cho_need(a, n);
   const int bid = blockIdx.x, q0 = bid * XGT;
-  const CrRng s0 = a.st[a.rd];
   if (n == 0) {
     if (bid == 0 && threadIdx.x == 0) a.st[a.wr] = s0;
     return;
@@ -1780,13 +1903,16 @@ __global__ __launch_bounds__(XGT) void xg_cho_fused(XgCall a) {
   if (q0 >= need) return;
   const int q = q0 + threadIdx.x;
   const u128 sb = xg_base_state(a, s0, q0, nullptr);
+  XSTAMP(4, 2);
   const uint64_t w = pcg_output(apply_jump(a.wj[threadIdx.x + 1], sb));
   const uint32_t f = xg_cho_flags(a, s0, q, need, w);
   uint32_t tot;
   const uint32_t off = xg_block_scan((uint32_t)__builtin_popcount(f), tot);
   const int nb = (need + XGT - 1) / XGT;
   if (threadIdx.x == 0) xg_tpublish(a, bid, nb, tot);
+  XSTAMP(4, 5);
   const int64_t pre = xg_tprefix(a, bid);
+  XSTAMP(4, 6);
   if (bid == nb - 1 && threadIdx.x == 0 && pre + tot < n) atomicOr(a.err, GP_DERR_STREAM);
   if (pre >= n) return;
   int64_t r = pre + off;
@@ -1805,6 +1931,7 @@ __global__ __launch_bounds__(XGT) void xg_cho_fused(XgCall a) {
     }
     ++r;
   }
+  XSTAMP(4, 7);
 }
 // C2: the draws to idst[r]; the n-th one fixes the next state, has_uint32 and uinteger.
 __global__ __launch_bounds__(XGT) void xg_cho_write(XgCall a) {
@@ -1860,6 +1987,7 @@ __global__ __launch_bounds__(XGT) void xg_uniforms(XgCall a, uint64_t* __restric
 // Dry step on copies: which envs hit a wall (the wall-noise draw count, crooms.py:321-325) -> fd.
 template <int OK>
 __global__ __launch_bounds__(XGT) void xg_dry(CrDev p, XgFlags fd, const void* __restrict__ act, size_t off) {
+  XSTAMP(1, 0);
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   for (int i = threadIdx.x; i < p.tab_bytes / 16; i += XGT) ((uint4*)lds)[i] = ((const uint4*)p.tabs)[i];
   __syncthreads();
@@ -1879,6 +2007,7 @@ __global__ __launch_bounds__(XGT) void xg_dry(CrDev p, XgFlags fd, const void* _
     f = o.oob != 0;
   }
   xg_flag_block(fd, blockIdx.x, gridDim.x, f);
+  XSTAMP(1, 7);
 }
 
 // The step with the wall noise in place (crooms.py:276-298; an env that hits a wall reads pair r of the wall
@@ -1888,9 +2017,11 @@ __global__ __launch_bounds__(XGT) void xg_step(CrDev p, XgFlags fd, XgFlags fs, 
                                                size_t off, void* __restrict__ obs, float* __restrict__ rew,
                                                uint8_t* __restrict__ term, uint8_t* __restrict__ trunc) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  XSTAMP(3, 0);
   for (int i = threadIdx.x; i < p.tab_bytes / 16; i += XGT) ((uint4*)lds)[i] = ((const uint4*)p.tabs)[i];
   const int bid = blockIdx.x;
   const uint32_t wpre = xg_prefix(fd.c, bid);  // (its block sum syncs the table copy too)
+  XSTAMP(3, 1);
   uint32_t wbefore;
   xg_block_bit(fd.bits + (size_t)bid * XGW, wbefore);
   const int env = bid * XGT + threadIdx.x;
@@ -1921,6 +2052,7 @@ __global__ __launch_bounds__(XGT) void xg_step(CrDev p, XgFlags fd, XgFlags fs, 
     p.el[env] = el;
   }
   xg_flag_block(fs, bid, gridDim.x, f);
+  XSTAMP(3, 2);
   // episode statistics: block reduction, one set of atomics per block into slot 0
   __shared__ float m_r[XGW];
   __shared__ uint32_t m_e[XGW], m_l[XGW], m_n[XGW];
@@ -1938,12 +2070,13 @@ __global__ __launch_bounds__(XGT) void xg_step(CrDev p, XgFlags fd, XgFlags fs, 
     float r = 0.f;
     uint32_t ee = 0, l = 0, nn = 0;
     for (int i = 0; i < XGW; ++i) { r += m_r[i]; ee += m_e[i]; l += m_l[i]; nn += m_n[i]; }
-    CrSlot& m = p.mslot[0];
+    CrSlot& m = p.mslot[bid % p.nslot];  // (one slot for every block serialised up to 6 us of atomics)
     atomicAdd(&m.return_sum, (double)r);
     atomicAdd(&m.episodes, (unsigned long long)ee);
     atomicAdd(&m.length_sum, (unsigned long long)l);
     atomicAdd(&m.env_steps, (unsigned long long)nn);
   }
+  XSTAMP(3, 7);
 }
 
 // The resets (crooms.py:217-244 goal then agent; :251-266 for reset()): fs's envs, the env of rank r taking
@@ -1952,6 +2085,7 @@ template <int OK>
 __global__ __launch_bounds__(XGT) void xg_apply_resets(CrDev p, XgFlags fs, const int32_t* __restrict__ gi,
                                                        const int32_t* __restrict__ ai, void* __restrict__ obs) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  XSTAMP(5, 0);
   const int bid = blockIdx.x, env = bid * XGT + threadIdx.x;
   int r = env;
   bool f = env < p.B;
@@ -1968,6 +2102,7 @@ __global__ __launch_bounds__(XGT) void xg_apply_resets(CrDev p, XgFlags fs, cons
   }
   for (int i = threadIdx.x; i < p.tab_bytes / 16; i += XGT) ((uint4*)lds)[i] = ((const uint4*)p.tabs)[i];
   __syncthreads();
+  XSTAMP(5, 1);
   if (!f) return;
   Draws d;
   d.k53 = 0;
@@ -2018,10 +2153,22 @@ struct CRoomsBackend : EnvBackend {
   DevBuf xg_jt, xg_bits, xg_pbits, xg_bstate, xg_span, xg_val, xg_cnt, xg_ebits;
   DevBuf xg_tbc, xg_tgs, xg_tacc;  // the fused normal call's tagged counts (tacc zero between launches)
   uint32_t xg_tag = 0;
+#ifdef GP_STAMPS
+  DevBuf xg_dbg;  // [6 kinds][1024 blocks][8] stamps (tools/xstamps.py)
+  int debug_stamps(unsigned long long* out, int cap) override {
+    GP_HIP_CHECK(hipDeviceSynchronize());
+    if (!xg_dbg.p) return 0;
+    const int n = std::min(cap, 6 * 1024 * 8);
+    GP_HIP_CHECK(hipMemcpy(out, xg_dbg.p, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost));
+    return n;
+  }
+#endif
   int xg_P = 0;                  // positions of a draw call (>= what normal(2B) needs)
   int xg_nbe = 0;                // env blocks
   int xg_slot = 0;               // the stream-state slot holding the current state (0 between API calls)
   bool xg_on() const { return rng_mode == GP_RNG_NUMPY && B > XG_MIN_ENVS; }
+  bool xg_fused() const { return !XG_SPLIT_NORMALS && B <= XG_FUSE_MAX_ENVS; }  // one launch per draw call
+  DevBuf xg_xend, xg_xinfo;      // the wall-noise extension of the action-noise call (XgCall::xinfo)
   // count sets in xg_cnt: 0 = the draw calls' positions, 1 = dry-step wall hits, 2 = resetting envs
   // One count set: acc (8-B atomics) | gs | bc, the set's size rounded up to 256 B so that every set's acc
   // array stays 8-byte aligned (a misaligned 64-bit atomic faults the queue; with an odd group count the
@@ -2076,12 +2223,22 @@ struct CRoomsBackend : EnvBackend {
     a.err = derr.ptr();
     return a;
   }
-  int xg_normals(int64_t n_host, int nsrc, int nmul, double scale, double* dst, hipStream_t s) {
+  // ext: 1 = the action-noise call extended by the wall noise (xd.wall), 2 = the wall-noise call after it
+  int xg_normals(int64_t n_host, int nsrc, int nmul, double scale, double* dst, hipStream_t s, int ext = 0) {
     XgCall a = xg_call(n_host, nsrc, nmul);
     a.scale = scale;
     a.dst = dst;
+    if (ext && xg_fused()) {
+      a.xinfo = xg_xinfo.as<uint32_t>();
+      a.xend = xg_xend.as<uint32_t>();
+      a.xdst = xd.wall;
+      a.xmax = (uint32_t)(2 * B);
+      a.xscale = 0.5;
+    }
     const unsigned nbp = (unsigned)(xg_P / XGT);
-    if (XG_SPLIT_NORMALS || B > XG_FUSE_MAX_ENVS) {
+    if (ext == 2 && a.xinfo) {
+      hipLaunchKernelGGL(xg_wall_one, dim3(1), dim3(XT), 0, s, a, xd);
+    } else if (!xg_fused()) {
       hipLaunchKernelGGL(xg_norm_classify, dim3(nbp), dim3(XGT), 0, s, a);
       hipLaunchKernelGGL(xg_norm_write, dim3(nbp), dim3(XGT), 0, s, a);
     } else {
@@ -2100,7 +2257,7 @@ struct CRoomsBackend : EnvBackend {
     XgCall a = xg_call(n_host, nsrc, 1);
     a.idst = dst;
     const unsigned nbc = (unsigned)((B / 2 + B / 1024 + 256 + XGT - 1) / XGT);
-    if (XG_SPLIT_NORMALS || B > XG_FUSE_MAX_ENVS) {
+    if (!xg_fused()) {
       hipLaunchKernelGGL(xg_cho_count, dim3(nbc), dim3(XGT), 0, s, a);
       hipLaunchKernelGGL(xg_cho_write, dim3(nbc), dim3(XGT), 0, s, a);
     } else {
@@ -2580,6 +2737,7 @@ int CRoomsBackend::build(const gp_crooms_config* cfg) {
   grid = std::max(1, std::min(d.ntiles, prop.multiProcessorCount * occ));
   if ((e = b_slot.alloc(sizeof(CrSlot) * grid))) return e;
   d.mslot = b_slot.as<CrSlot>();
+  d.nslot = grid;
   if ((e = derr.alloc())) return e;
   d.derr = derr.ptr();
   if (rng_mode == GP_RNG_NUMPY && (e = x_alloc())) return e;
@@ -2604,8 +2762,10 @@ int CRoomsBackend::x_alloc() {
   xd.rank = x_rank.as<int32_t>();
   xd.lemire_thr = lemire_threshold((uint32_t)d.n_valid);
   if (B > XG_MIN_ENVS) {
-    // positions of a draw call: normal(2B) needs 2B + 2B / 16 + 4096 at most (xg_norm_need), rounded to blocks
-    const int64_t P = ((2 * b + 2 * b / 16 + 4096 + 64 * XGT - 1) / (64 * XGT)) * (64 * XGT);
+    // positions of a draw call: normal(2B) needs 2B + 2B / 16 + 4096 at most (xg_norm_need), rounded to blocks;
+    // with the wall-noise extension (fused calls) up to 2B more normals
+    const int64_t nmax = (xg_fused() ? 4 : 2) * b;
+    const int64_t P = ((nmax + nmax / 16 + 4096 + 64 * XGT - 1) / (64 * XGT)) * (64 * XGT);
     if (P > (int64_t)1 << 30) {
       gp_set_error("crooms numpy mode: num_envs too large");
       return GP_E_INVALID;
@@ -2620,6 +2780,15 @@ int CRoomsBackend::x_alloc() {
         (e = xg_tgs.alloc(8 * (nbp / 64 + 2))) || (e = xg_tacc.alloc(8 * (nbp / 64 + 2))))
       return e;
     GP_HIP_CHECK(hipMemset(xg_cnt.p, 0, xg_cnt_bytes()));  // the group accumulators start (and stay) cleared
+    if (xg_fused()) {
+      if ((e = xg_xend.alloc(4 * 2 * b)) || (e = xg_xinfo.alloc(16))) return e;
+      GP_HIP_CHECK(hipMemset(xg_xinfo.p, 0, 16));
+    }
+#ifdef GP_STAMPS
+    if ((e = xg_dbg.alloc(8 * 6 * 1024 * 8))) return e;
+    GP_HIP_CHECK(hipMemset(xg_dbg.p, 0, 8 * 6 * 1024 * 8));
+    GP_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_xgdbg), &xg_dbg.p, sizeof(void*)));
+#endif
   }
   return x_upload_rng(rng);
 }
@@ -2665,16 +2834,15 @@ int CRoomsBackend::xg_rollout(int K, const void* act, void* obs, float* rew, uin
       hipLaunchKernelGGL(xg_uniforms, dim3(nbe), dim3(XGT), 0, s, a, xd.u);
       xg_slot ^= 1;
     }
-    if ((d.action_kind == 0 || d.action_std != 0.0) &&
-        (e = xg_normals(2 * B, 0, 1, d.action_std, xd.noise, s)))
-      return e;
+    const bool noise = d.action_kind == 0 || d.action_std != 0.0;
+    if (noise && (e = xg_normals(2 * B, 0, 1, d.action_std, xd.noise, s, 1))) return e;
     // the dry step: which envs hit a wall; their noise normal(0.5, (n_oob, 2)) (crooms.py:321-325)
     e = dispatch_obs(d.obs_kind, [&](auto okc) -> int {
       constexpr int OK = decltype(okc)::value;
       hipLaunchKernelGGL(xg_dry<OK>, dim3(nbe), dim3(XGT), d.tab_bytes, s, dd, fd, act, off);
       return GP_OK;
     });
-    if (e || (e = xg_normals(0, 1, 2, 0.5, xd.wall, s))) return e;
+    if (e || (e = xg_normals(0, 1, 2, 0.5, xd.wall, s, noise ? 2 : 0))) return e;
     // the step itself with the wall noise in place, resets deferred; then the resetting envs' goals / agents
     e = dispatch_obs(d.obs_kind, [&](auto okc) -> int {
       constexpr int OK = decltype(okc)::value;
