@@ -1254,6 +1254,8 @@ struct XgCall {                   // one draw call over stream positions
   uint32_t* xinfo;
   uint32_t xmax;
   double xscale;
+  const PcgJump* bj;              // [blocks + 1] jump by bid * XGT positions (nullptr: the radix tables)
+  const PcgJump* hj;              // [blocks + 1] jump by bid * XGT - XG_LOOK (bid >= 1): a block's halo
 };
 
 // Block-wide sum (every thread gets it). Uses its own LDS; safe to call repeatedly.
@@ -1342,6 +1344,32 @@ __device__ __forceinline__ int64_t xg_n(const XgCall& a) {
   return a.nsrc.gs ? (int64_t)a.nmul * (int64_t)xg_total(a.nsrc, a.nsrc_blocks) : a.n_host;
 }
 __device__ __forceinline__ u128 xg_inc(const CrRng& s) { return mk128(s.i_hi, s.i_lo); }
+// The stream state of slot k through the vector memory path (a VGPR offset keeps the compiler from a scalar load):
+// a scalar load of the slot the previous kernels wrote took 3-17 us on MI355X (GP_STAMPS, tools/xstamps.py).
+__device__ __forceinline__ uint32_t xg_vload(const uint32_t* p) {  // the same for one word
+  int z;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)p[z]);
+}
+__device__ __forceinline__ CrRng xg_state(const CrRng* st, int k) {
+  int z;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+  const uint4* p = reinterpret_cast<const uint4*>(st + k) + z;
+  const uint4 a = p[0], b = p[1], c = p[2];
+  auto u = [](uint32_t v) -> uint32_t { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
+  auto u64 = [&](uint32_t lo, uint32_t hi) -> uint64_t { return ((uint64_t)u(hi) << 32) | (uint64_t)u(lo); };
+  CrRng r;
+  r.s_hi = u64(a.x, a.y);
+  r.s_lo = u64(a.z, a.w);
+  r.i_hi = u64(b.x, b.y);
+  r.i_lo = u64(b.z, b.w);
+  r.has_u32 = u(c.x);
+  r.uinteger = u(c.y);
+  r.err = u(c.z);
+  r.pad = u(c.w);
+  return r;
+}
+
 // positions a normal call of n draws may need (words per normal: 1.012 on average; capped by the buffers)
 __device__ __forceinline__ int xg_norm_need(const XgCall& a, int64_t n) {
   return (int)min((int64_t)a.P, n + n / 16 + 4096);
@@ -1362,7 +1390,8 @@ __device__ __forceinline__ void xg_put_state(CrRng* st, int wr, const CrRng& old
 __device__ __forceinline__ u128 xg_base_state(const XgCall& a, const CrRng& s0, int q0, uint64_t* bstate) {
   __shared__ uint64_t bb[2];
   if (threadIdx.x == 0) {
-    const u128 b = pcg_jump_ilp(a.jt, mk128(s0.s_hi, s0.s_lo), (uint32_t)q0);
+    const u128 S = mk128(s0.s_hi, s0.s_lo);
+    const u128 b = a.bj ? apply_jump(a.bj[blockIdx.x], S) : pcg_jump_ilp(a.jt, S, (uint32_t)q0);
     bb[0] = hi64(b);
     bb[1] = lo64(b);
     if (bstate) {
@@ -1522,10 +1551,13 @@ __global__ __launch_bounds__(XGT) void xg_norm_classify(XgCall a) {
   if (n == 0 || q0 >= need) return;
   __shared__ XgView v;
   __shared__ uint64_t hb[2];
-  const CrRng s0 = a.st[a.rd];
+  const CrRng s0 = xg_state(a.st, a.rd);
   const int t = threadIdx.x, lane = t & 63;
   if (t == 64) {  // the halo's base state (wave 1) beside the block's (thread 0, in xg_base_state)
-    const u128 h = q0 >= XG_LOOK ? pcg_jump_ilp(a.jt, mk128(s0.s_hi, s0.s_lo), (uint32_t)(q0 - XG_LOOK)) : (u128)0;
+    const u128 S = mk128(s0.s_hi, s0.s_lo);
+    const u128 h = q0 < XG_LOOK ? (u128)0
+                   : a.hj  ? apply_jump(a.hj[blockIdx.x], S)
+                           : pcg_jump_ilp(a.jt, S, (uint32_t)(q0 - XG_LOOK));
     hb[0] = hi64(h);
     hb[1] = lo64(h);
   }
@@ -1638,16 +1670,15 @@ __device__ __forceinline__ uint32_t xg_tprefix(const XgCall& a, int bid) {
 __global__ __launch_bounds__(XGT) void xg_norm_fused(XgCall a) {
   const int xty = a.nsrc.gs ? 2 : 0;
   XSTAMP(xty, 0);
-  const CrRng s0 = a.st[a.rd];  // (issued before n's loads and barrier)
+  const PcgJump myj = a.wj[threadIdx.x + 1];  // (independent of everything: issued first)
+  const CrRng s0 = xg_state(a.st, a.rd);  // (issued before n's loads and barrier)
+  const int64_t want = a.xinfo ? (int64_t)xg_vload(a.xinfo + 1) : 0;
   const int64_t n = xg_n(a);
   XSTAMP(xty, 1);
   const int bid = blockIdx.x, q0 = bid * XGT;
-  int64_t X = 0;  // the extension's normals past n (the next call's, xg_wall_one)
-  if (a.xinfo) {
-    const int64_t want = a.xinfo[1];
-    X = min((int64_t)a.xmax, want + want / 4 + 1024);
-  }
-  const int need = xg_norm_need(a, n + X);
+  // the extension's normals past n (the next call's, xg_wall_one)
+  const int64_t X = a.xinfo ? min((int64_t)a.xmax, want + want / 4 + 1024) : 0;
+  const int need = min(xg_norm_need(a, n + X), (int)(gridDim.x * XGT));  // (the launch may cap the extension)
   if (n == 0) {  // nothing drawn: the state carries over
     if (bid == 0 && threadIdx.x == 0) a.st[a.wr] = s0;
     return;
@@ -1658,7 +1689,10 @@ __global__ __launch_bounds__(XGT) void xg_norm_fused(XgCall a) {
   __shared__ uint64_t pmw[XGW];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   if (t == 64) {  // the halo's base state (wave 1) beside the block's (thread 0, in xg_base_state)
-    const u128 h = q0 >= XG_LOOK ? pcg_jump_ilp(a.jt, mk128(s0.s_hi, s0.s_lo), (uint32_t)(q0 - XG_LOOK)) : (u128)0;
+    const u128 S = mk128(s0.s_hi, s0.s_lo);
+    const u128 h = q0 < XG_LOOK ? (u128)0
+                   : a.hj  ? apply_jump(a.hj[blockIdx.x], S)
+                           : pcg_jump_ilp(a.jt, S, (uint32_t)(q0 - XG_LOOK));
     hb[0] = hi64(h);
     hb[1] = lo64(h);
   }
@@ -1674,7 +1708,7 @@ __global__ __launch_bounds__(XGT) void xg_norm_fused(XgCall a) {
     const int i = part == 0 ? XG_LOOK + t : t;
     const int q = q0 - XG_LOOK + i;
     const bool live = q >= 0 && q < need;
-    const u128 X = apply_jump(a.wj[t + 1], part == 0 ? sb : mk128(hb[0], hb[1]));
+    const u128 X = apply_jump(myj, part == 0 ? sb : mk128(hb[0], hb[1]));
     double z;
     const bool slow = live && !zig_fast(zt, pcg_output(X), z);
     if (part == 0) zf = z;
@@ -1770,7 +1804,8 @@ __global__ __launch_bounds__(XT) void xg_wall_one(XgCall a, CrExact x) {
   __shared__ uint32_t red[XT / 64];
   const int t = threadIdx.x;
   XSTAMP(2, 0);
-  const CrRng s0 = a.st[a.rd];  // the action-noise call's end
+  const CrRng s0 = xg_state(a.st, a.rd);  // the action-noise call's end
+  const uint32_t made = xg_vload(a.xinfo);  // the extension's normals
   uint32_t c = 0;
   for (int j = t; j < (a.nsrc_blocks + 63) / 64; j += XT) c += a.nsrc.gs[j];
 #pragma unroll
@@ -1787,11 +1822,11 @@ __global__ __launch_bounds__(XT) void xg_wall_one(XgCall a, CrExact x) {
     if (t == 0) a.st[a.wr] = s0;
     return;
   }
-  if (n <= (int64_t)a.xinfo[0]) {
+  if (n <= (int64_t)made) {
     if (t == 0) {
-      const CrRng sa = a.st[a.wr];  // the action-noise call's start (the slot this call writes)
-      xg_put_state(a.st, a.wr, sa, pcg_jump_ilp(a.jt, mk128(sa.s_hi, sa.s_lo), a.xend[n - 1]), sa.has_u32,
-                   sa.uinteger);
+      const CrRng sa = xg_state(a.st, a.wr);  // the action-noise call's start (the slot this call writes)
+      xg_put_state(a.st, a.wr, sa, pcg_jump_ilp(a.jt, mk128(sa.s_hi, sa.s_lo), xg_vload(a.xend + (n - 1))),
+                   sa.has_u32, sa.uinteger);
     }
     XSTAMP(2, 7);
     return;
@@ -1824,7 +1859,7 @@ __global__ __launch_bounds__(XGT) void xg_norm_write(XgCall a) {
   const int64_t n = xg_n(a);
   const int need = xg_norm_need(a, n);
   const int bid = blockIdx.x, q0 = bid * XGT;
-  const CrRng s0 = a.st[a.rd];
+  const CrRng s0 = xg_state(a.st, a.rd);
   if (n == 0) {  // nothing drawn: the state carries over
     if (bid == 0 && threadIdx.x == 0) a.st[a.wr] = s0;
     return;
@@ -1870,7 +1905,7 @@ __global__ __launch_bounds__(XGT) void xg_cho_count(XgCall a) {
   const int need = xg_cho_need(a, n);
   const int q0 = blockIdx.x * XGT;
   if (n == 0 || q0 >= need) return;
-  const CrRng s0 = a.st[a.rd];
+  const CrRng s0 = xg_state(a.st, a.rd);
   const u128 sb = xg_base_state(a, s0, q0, a.bstate);
   const uint64_t w = pcg_output(apply_jump(a.wj[threadIdx.x + 1], sb));
   const uint32_t cnt = xg_block_sum((uint32_t)__builtin_popcount(xg_cho_flags(a, s0, q0 + threadIdx.x, need, w)));
@@ -1887,7 +1922,7 @@ __global__ __launch_bounds__(XGT) void xg_cho_fused(XgCall a) {
     XSTAMP(4, 4);
   }
 #endif
-  const CrRng s0 = a.st[a.rd];  // (issued before n's loads and barrier)
+  const CrRng s0 = xg_state(a.st, a.rd);  // (issued before n's loads and barrier)
 #ifdef GP_STAMPS
   asm volatile("" ::"s"(s0.s_lo));
   XSTAMP(4, 3);
@@ -1938,7 +1973,7 @@ __global__ __launch_bounds__(XGT) void xg_cho_write(XgCall a) {
   const int64_t n = xg_n(a);
   const int need = xg_cho_need(a, n);
   const int bid = blockIdx.x, q0 = bid * XGT;
-  const CrRng s0 = a.st[a.rd];
+  const CrRng s0 = xg_state(a.st, a.rd);
   if (n == 0) {
     if (bid == 0 && threadIdx.x == 0) a.st[a.wr] = s0;
     return;
@@ -1974,7 +2009,7 @@ __global__ __launch_bounds__(XGT) void xg_cho_write(XgCall a) {
 __global__ __launch_bounds__(XGT) void xg_uniforms(XgCall a, uint64_t* __restrict__ dst) {
   const int64_t n = a.n_host;
   const int q0 = blockIdx.x * XGT;
-  const CrRng s0 = a.st[a.rd];
+  const CrRng s0 = xg_state(a.st, a.rd);
   const u128 S = mk128(s0.s_hi, s0.s_lo);
   if (blockIdx.x == 0 && threadIdx.x == 0) xg_put_state(a.st, a.wr, s0, pcg_jump_ilp(a.jt, S, (uint32_t)n), s0.has_u32,
                                                          s0.uinteger);
@@ -2169,6 +2204,7 @@ struct CRoomsBackend : EnvBackend {
   bool xg_on() const { return rng_mode == GP_RNG_NUMPY && B > XG_MIN_ENVS; }
   bool xg_fused() const { return !XG_SPLIT_NORMALS && B <= XG_FUSE_MAX_ENVS; }  // one launch per draw call
   DevBuf xg_xend, xg_xinfo;      // the wall-noise extension of the action-noise call (XgCall::xinfo)
+  DevBuf xg_bj, xg_hj;           // per-block base / halo jumps (XgCall::bj, hj) for the stream's increment
   // count sets in xg_cnt: 0 = the draw calls' positions, 1 = dry-step wall hits, 2 = resetting envs
   // One count set: acc (8-B atomics) | gs | bc, the set's size rounded up to 256 B so that every set's acc
   // array stays 8-byte aligned (a misaligned 64-bit atomic faults the queue; with an odd group count the
@@ -2201,6 +2237,8 @@ struct CRoomsBackend : EnvBackend {
   XgCall xg_call(int64_t n_host, int nsrc, int nmul) {  // nsrc: n = nmul * (flagged envs of count set nsrc)
     XgCall a{};
     a.jt = xg_jt.as<PcgJump>();
+    a.bj = xg_bj.as<PcgJump>();
+    a.hj = xg_hj.as<PcgJump>();
     a.wj = x_wj.as<PcgJump>();
     a.st = x_rng.as<CrRng>();
     a.rd = xg_slot;
@@ -2235,7 +2273,11 @@ struct CRoomsBackend : EnvBackend {
       a.xmax = (uint32_t)(2 * B);
       a.xscale = 0.5;
     }
-    const unsigned nbp = (unsigned)(xg_P / XGT);
+    unsigned nbp = (unsigned)(xg_P / XGT);
+    if (ext == 1 && a.xinfo) {  // the extension's launch covers up to B / 2 normals past n (a 25% wall-hit rate)
+      const int64_t nx = n_host + B / 2;
+      nbp = (unsigned)std::min<int64_t>(nbp, (nx + nx / 16 + 4096 + XGT - 1) / XGT);
+    }
     if (ext == 2 && a.xinfo) {
       hipLaunchKernelGGL(xg_wall_one, dim3(1), dim3(XT), 0, s, a, xd);
     } else if (!xg_fused()) {
@@ -2780,6 +2822,7 @@ int CRoomsBackend::x_alloc() {
         (e = xg_tgs.alloc(8 * (nbp / 64 + 2))) || (e = xg_tacc.alloc(8 * (nbp / 64 + 2))))
       return e;
     GP_HIP_CHECK(hipMemset(xg_cnt.p, 0, xg_cnt_bytes()));  // the group accumulators start (and stay) cleared
+    if ((e = xg_bj.alloc(sizeof(PcgJump) * (nbp + 1))) || (e = xg_hj.alloc(sizeof(PcgJump) * (nbp + 1)))) return e;
     if (xg_fused()) {
       if ((e = xg_xend.alloc(4 * 2 * b)) || (e = xg_xinfo.alloc(16))) return e;
       GP_HIP_CHECK(hipMemset(xg_xinfo.p, 0, 16));
@@ -2878,6 +2921,22 @@ int CRoomsBackend::x_upload_rng(const RngHost& r) {
   if (xg_jt.p) {
     const std::vector<PcgJump> jt = build_jump_tables(r.inc);
     GP_HIP_CHECK(hipMemcpy(xg_jt.p, jt.data(), sizeof(PcgJump) * jt.size(), hipMemcpyHostToDevice));
+    // per-block jumps: bj[b] = b * XGT steps, hj[b] = b * XGT - XG_LOOK steps (= XGT - XG_LOOK after bj[b - 1])
+    const size_t nb = xg_bj.n / sizeof(PcgJump);
+    std::vector<PcgJump> bj(nb), hj(nb);
+    const PcgJump J = pcg_jump_params((u128)XGT, r.inc), Jh = pcg_jump_params((u128)(XGT - XG_LOOK), r.inc);
+    auto after = [](const PcgJump& second, const PcgJump& first) {  // second o first
+      const u128 A2 = mk128(second.a_hi, second.a_lo), C2 = mk128(second.c_hi, second.c_lo);
+      const u128 A = A2 * mk128(first.a_hi, first.a_lo), C = A2 * mk128(first.c_hi, first.c_lo) + C2;
+      return PcgJump{hi64(A), lo64(A), hi64(C), lo64(C)};
+    };
+    bj[0] = hj[0] = PcgJump{0, 1, 0, 0};
+    for (size_t k = 1; k < nb; ++k) {
+      bj[k] = after(J, bj[k - 1]);
+      hj[k] = after(Jh, bj[k - 1]);
+    }
+    GP_HIP_CHECK(hipMemcpy(xg_bj.p, bj.data(), sizeof(PcgJump) * nb, hipMemcpyHostToDevice));
+    GP_HIP_CHECK(hipMemcpy(xg_hj.p, hj.data(), sizeof(PcgJump) * nb, hipMemcpyHostToDevice));
   }
   xg_slot = 0;
   CrRng h{hi64(r.state), lo64(r.state), hi64(r.inc), lo64(r.inc), r.has_u32, r.uinteger, 0u, 0u};

@@ -61,5 +61,13 @@ for rep in range(REPS):
             if len(c):
                 line.append(f"s{i} {np.median(c) - e0:6.0f}/{c.max() - e0:6d} ({len(c)})")
         print("  " + "; ".join(line))
+        # per-block phase costs: median over blocks of (stamp i - the block's previous stamp)
+        ords = {4: [0, 4, 3, 1, 2, 5, 6, 7]}.get(k, list(range(8)))
+        d = []
+        for i0, i1 in zip(ords, ords[1:]):
+            m = (v[:, i0] > 0) & (v[:, i1] > 0)
+            if m.sum():
+                d.append(f"{i0}->{i1} {np.median(v[m, i1] - v[m, i0]):6.0f}")
+        print("      per block (median ns): " + "; ".join(d))
         prev_end = ends.max()
     print(f"  step total {prev_end - t_first} ns (action normals entry -> last resets stamp)")
