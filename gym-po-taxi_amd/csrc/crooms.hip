@@ -1649,8 +1649,14 @@ __device__ __forceinline__ uint32_t xg_tpoll(const unsigned long long* p, uint32
     __builtin_amdgcn_s_sleep(1);
   }
 }
+// Up to XG_FLAT_MAX blocks a block's prefix sums the tagged block counts themselves (<= XG_FLAT_MAX / XGT loads
+// per thread, issued together): the publish is one store, with no returning atomic and no group-sum hop.
+#ifndef XG_FLAT_MAX
+#define XG_FLAT_MAX 4096
+#endif
 __device__ __forceinline__ void xg_tpublish(const XgCall& a, int bid, int nblocks, uint32_t cnt) {
   __hip_atomic_store(&a.tbc[bid], ((unsigned long long)a.tag << 32) | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (nblocks <= XG_FLAT_MAX) return;
   const int g = bid >> 6;
   const unsigned long long old = atomicAdd(&a.tacc[g], (1ull << 40) | (unsigned long long)cnt);
   if ((int)(old >> 40) == min(64, nblocks - 64 * g) - 1) {
@@ -1659,9 +1665,25 @@ __device__ __forceinline__ void xg_tpublish(const XgCall& a, int bid, int nblock
     __hip_atomic_store(&a.tgs[g], ((unsigned long long)a.tag << 32) | gsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
-__device__ __forceinline__ uint32_t xg_tprefix(const XgCall& a, int bid) {
+__device__ __forceinline__ uint32_t xg_tprefix(const XgCall& a, int bid, int nblocks) {
   const int g = bid >> 6, t = threadIdx.x;
   uint32_t x = 0;
+  if (nblocks <= XG_FLAT_MAX) {
+    for (int c = 0; c * XGT < bid; c += 4) {  // block-uniform
+      unsigned long long v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int j = t + (c + i) * XGT;
+        v[i] = j < bid ? __hip_atomic_load(&a.tbc[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int j = t + (c + i) * XGT;
+        if (j < bid) x += (uint32_t)(v[i] >> 32) == a.tag ? (uint32_t)v[i] : xg_tpoll(&a.tbc[j], a.tag, a.err);
+      }
+    }
+    return xg_block_sum(x);
+  }
   for (int j = t; j < g; j += XGT) x += xg_tpoll(&a.tgs[j], a.tag, a.err);
   if (t < bid - 64 * g) x += xg_tpoll(&a.tbc[64 * g + t], a.tag, a.err);
   return xg_block_sum(x);
@@ -1768,7 +1790,7 @@ __global__ __launch_bounds__(XGT) void xg_norm_fused(XgCall a) {
   const int nb = (need + XGT - 1) / XGT;
   if (t == 0) xg_tpublish(a, bid, nb, cnt);
   XSTAMP(xty, 5);
-  const int64_t pre = xg_tprefix(a, bid);
+  const int64_t pre = xg_tprefix(a, bid, nb);
   XSTAMP(xty, 6);
   if (bid == nb - 1 && t == 0) {
     if (pre + cnt < n) atomicOr(a.err, GP_DERR_STREAM);
@@ -1946,7 +1968,7 @@ __global__ __launch_bounds__(XGT) void xg_cho_fused(XgCall a) {
   const int nb = (need + XGT - 1) / XGT;
   if (threadIdx.x == 0) xg_tpublish(a, bid, nb, tot);
   XSTAMP(4, 5);
-  const int64_t pre = xg_tprefix(a, bid);
+  const int64_t pre = xg_tprefix(a, bid, nb);
   XSTAMP(4, 6);
   if (bid == nb - 1 && threadIdx.x == 0 && pre + tot < n) atomicOr(a.err, GP_DERR_STREAM);
   if (pre >= n) return;
