@@ -2043,20 +2043,61 @@ __global__ __launch_bounds__(XGT) void xg_uniforms(XgCall a, uint64_t* __restric
 
 // Dry step on copies: which envs hit a wall (the wall-noise draw count, crooms.py:321-325) -> fd.
 template <int OK>
-__global__ __launch_bounds__(XGT) void xg_dry(CrDev p, XgFlags fd, const void* __restrict__ act, size_t off) {
+// Round 4: the previous step's resets (fr: its resetting envs, gi / ai their draws, obs_prev its observation row)
+// are applied here first, as xg_apply_resets would (one launch per step fewer); fr.bits == nullptr: none pending.
+__global__ __launch_bounds__(XGT) void xg_dry(CrDev p, XgFlags fd, const void* __restrict__ act, size_t off,
+                                              XgFlags fr, const int32_t* __restrict__ gi,
+                                              const int32_t* __restrict__ ai, void* __restrict__ obs_prev) {
   XSTAMP(1, 0);
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int bid = blockIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // the block's reset bitmap words, lane-indexed (vector loads: the previous step's kernel wrote them)
+  uint64_t rw = 0;
+  if (fr.bits && lane < XGW) rw = fr.bits[(size_t)bid * XGW + lane];
+  uint64_t any = 0, mine = 0;
+  uint32_t before = 0;
+#pragma unroll
+  for (int j = 0; j < XGW; ++j) {
+    const uint64_t x = __shfl(rw, j, 64);
+    any |= x;
+    if (j < wv) before += (uint32_t)__builtin_popcountll(x);
+    if (j == wv) mine = x;
+  }
   for (int i = threadIdx.x; i < p.tab_bytes / 16; i += XGT) ((uint4*)lds)[i] = ((const uint4*)p.tabs)[i];
+  uint32_t pre = 0;
+  if (any) pre = xg_prefix(fr.c, bid);  // block-uniform (its block sum syncs the table copy too)
   __syncthreads();
-  const int env = blockIdx.x * XGT + threadIdx.x;
+  before += (uint32_t)__builtin_popcountll(mine & ((1ull << lane) - 1ull));
+  const bool rf = (mine >> lane) & 1ull;
+  const int env = bid * XGT + threadIdx.x;
   bool f = false;
   if (env < p.B) {
     double a0, a1;
     int ad;
     x_load_action(p, act, off, env, a0, a1, ad);
-    double ay = p.ay[env], ax = p.ax[env];
-    double vy = p.use_velocity ? p.vy[env] : 0.0, vx = p.use_velocity ? p.vx[env] : 0.0;
-    uint32_t g = x_goal(p, env);
+    double ay, ax, vy, vx;
+    uint32_t g;
+    if (rf) {  // crooms.py:217-244 with the previous step's draws (as xg_apply_resets)
+      const int r = (int)(pre + before);
+      Draws d;
+      d.k53 = 0;
+      d.gi = p.goal_fixed ? 0u : (uint32_t)gi[r];
+      d.ai = p.agent_fixed ? 0u : (uint32_t)ai[r];
+      g = x_goal(p, env);
+      reset_env(p, lds, d, ay, ax, vy, vx, g);
+      vy = vx = 0.0;
+      p.ay[env] = ay;
+      p.ax[env] = ax;
+      if (p.use_velocity) { p.vy[env] = 0.0; p.vx[env] = 0.0; }
+      if (!p.goal_fixed) p.goal[env] = g;
+      write_obs<OK>(p, lds, env, ay, ax, g, obs_prev);
+    } else {
+      ay = p.ay[env];
+      ax = p.ax[env];
+      vy = p.use_velocity ? p.vy[env] : 0.0;
+      vx = p.use_velocity ? p.vx[env] : 0.0;
+      g = x_goal(p, env);
+    }
     int32_t el = p.el[env];
     float rs = 0.f;
     uint32_t ep = 0, ln = 0;
@@ -2904,7 +2945,8 @@ int CRoomsBackend::xg_rollout(int K, const void* act, void* obs, float* rew, uin
     // the dry step: which envs hit a wall; their noise normal(0.5, (n_oob, 2)) (crooms.py:321-325)
     e = dispatch_obs(d.obs_kind, [&](auto okc) -> int {
       constexpr int OK = decltype(okc)::value;
-      hipLaunchKernelGGL(xg_dry<OK>, dim3(nbe), dim3(XGT), d.tab_bytes, s, dd, fd, act, off);
+      hipLaunchKernelGGL(xg_dry<OK>, dim3(nbe), dim3(XGT), d.tab_bytes, s, dd, fd, act, off, k ? fs : XgFlags{},
+                         (const int32_t*)xd.gi, (const int32_t*)xd.ai, k ? (void*)(ob - B * osz) : nullptr);
       return GP_OK;
     });
     if (e || (e = xg_normals(0, 1, 2, 0.5, xd.wall, s, noise ? 2 : 0))) return e;
@@ -2918,6 +2960,7 @@ int CRoomsBackend::xg_rollout(int K, const void* act, void* obs, float* rew, uin
     if (e) return e;
     if (!d.goal_fixed && (e = xg_choices(0, 2, xd.gi, s))) return e;
     if (!d.agent_fixed && (e = xg_choices(0, 2, xd.ai, s))) return e;
+    if (k + 1 < K) continue;  // the next step's dry kernel applies these resets
     e = dispatch_obs(d.obs_kind, [&](auto okc) -> int {
       constexpr int OK = decltype(okc)::value;
       hipLaunchKernelGGL(xg_apply_resets<OK>, dim3(nbe), dim3(XGT), d.tab_bytes, s, dd, fs, (const int32_t*)xd.gi,
