@@ -1182,11 +1182,11 @@ constexpr int XG_MIN_ENVS = 4096; // at or below: the one-workgroup kernel (fewe
 #ifndef XG_SPLIT_NORMALS
 #define XG_SPLIT_NORMALS 0        // 1: normal / choice calls as two launches each (count, then write; round 3's form)
 #endif
-// Above this many envs a call goes back to two launches: the fused kernel's in-launch prefix is a chain over
-// every earlier block, and at 2^20 envs and up it costs what the second launch saved (A/B on MI355X, DESIGN 6d:
-// 143 vs 194 us/step at 2^17 envs, 568 vs 569 at 2^20, 1035 vs 970 at 2^21).
+// Above this many envs a call goes back to two launches (the fused kernel's in-launch prefix is a chain over every
+// earlier block). A/B on MI355X, µs/step fused vs two launches: before the round-4 state loads and the
+// wall-noise extension 568 vs 569 at 2^20 and 1035 vs 970 at 2^21; after them 571-576 vs 597 at 2^21.
 #ifndef XG_FUSE_MAX_ENVS
-#define XG_FUSE_MAX_ENVS 1048576
+#define XG_FUSE_MAX_ENVS 2097152
 #endif
 
 // GP_STAMPS diagnostic builds (tools/xstamps.py): s_memrealtime stamps (100 MHz, chip-synchronous) by thread 0 of
@@ -2265,7 +2265,8 @@ struct CRoomsBackend : EnvBackend {
   int xg_nbe = 0;                // env blocks
   int xg_slot = 0;               // the stream-state slot holding the current state (0 between API calls)
   bool xg_on() const { return rng_mode == GP_RNG_NUMPY && B > XG_MIN_ENVS; }
-  bool xg_fused() const { return !XG_SPLIT_NORMALS && B <= XG_FUSE_MAX_ENVS; }  // one launch per draw call
+  bool xg_split = false;         // gp_debug_set("disable_fused", 1) at create: the two-launch draw calls (tests)
+  bool xg_fused() const { return !XG_SPLIT_NORMALS && !xg_split && B <= XG_FUSE_MAX_ENVS; }  // one launch per call
   DevBuf xg_xend, xg_xinfo;      // the wall-noise extension of the action-noise call (XgCall::xinfo)
   DevBuf xg_bj, xg_hj;           // per-block base / halo jumps (XgCall::bj, hj) for the stream's increment
   // count sets in xg_cnt: 0 = the draw calls' positions, 1 = dry-step wall hits, 2 = resetting envs
@@ -2845,6 +2846,7 @@ int CRoomsBackend::build(const gp_crooms_config* cfg) {
   d.nslot = grid;
   if ((e = derr.alloc())) return e;
   d.derr = derr.ptr();
+  xg_split = gp_debug_knobs().disable_fused != 0;
   if (rng_mode == GP_RNG_NUMPY && (e = x_alloc())) return e;
   return GP_OK;
 }

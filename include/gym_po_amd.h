@@ -262,8 +262,8 @@ int gp_profile_read_resolver(gp_env* env, double* total_ms, int64_t* n_launches)
 
 /* ---- diagnostics (never needed in production; no reference counterpart) ----
  * Process-wide test / tuning knobs, read by gp_create (handles created earlier keep their values):
- *   "disable_fused" (GRID numpy mode: 1 = the two-kernel path only), "no_staging" (1 = the fused kernel's
- *   env waves store outputs directly), "xmode" (fused exchange variant, default 1), "spin_limit" (polls
+ *   "disable_fused" (GRID numpy mode: 1 = the two-kernel path only; CROOMS numpy mode: 1 = two launches per
+ *   draw call), "no_staging" (1 = the fused kernel's env waves store outputs directly), "xmode" (fused exchange variant, default 1), "spin_limit" (polls
  *   before a cross-block wait gives up, 0 = default), "fault_block" (this block never publishes: forces
  *   the timeout path; -1 = off), "fused_tile" (GRID fused kernel envs per tile: 512, 1024 or 2048; 0 = by
  *   size), "no_spw" (GRID fused kernel: 1 = no speculative word windows), "generic_kernels" (CROOMS: 1 = the

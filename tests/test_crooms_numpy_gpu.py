@@ -88,6 +88,18 @@ ORACLE_CASES = [
 ]
 
 
+# the two-launch draw calls (the form above XG_FUSE_MAX_ENVS = 2^21 envs), forced at a size the oracle runs fast
+SPLIT_CASES = [({"obs_type": "vector_mdp", "action_std": 0.5, "time_limit": 6}, 65536, 12, 6),
+               ({"obs_type": "vector_goal_mdp", "goal_xy": None, "use_velocity": True, "time_limit": 25}, 30001, 30, 3)]
+
+
+@pytest.mark.parametrize("kw,B,steps,K", SPLIT_CASES)
+def test_numpy_mode_two_launch_calls_vs_oracle(kw, B, steps, K, gpu_device):
+    from gym_po_amd._lib import debug_knobs
+    with debug_knobs(disable_fused=1):
+        test_numpy_mode_vs_oracle(kw, B, steps, K, gpu_device)
+
+
 @pytest.mark.parametrize("kw,B,steps,K", ORACLE_CASES)
 def test_numpy_mode_vs_oracle(kw, B, steps, K, gpu_device):
     """Every step against the oracle on numpy's Generator; K-step launches; final PCG64 state."""
