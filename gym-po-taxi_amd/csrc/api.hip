@@ -37,6 +37,9 @@ const char* gp_derr_text(uint32_t flags) {
   if (flags & GP_DERR_BTPE)
     strncat(buf, "a Taxi numpy-mode reset needed numpy's BTPE binomial (not restated on the device); ",
             sizeof(buf) - strlen(buf) - 1);
+  if (flags & GP_DERR_LOGIC)
+    strncat(buf, "the windowed kernel's early reset count disagreed with its step masks (internal error); ",
+            sizeof(buf) - strlen(buf) - 1);
   if (flags & GP_DERR_STREAM)
     strncat(buf, "a numpy normal needed more words than one stream window holds; ", sizeof(buf) - strlen(buf) - 1);
   return buf;

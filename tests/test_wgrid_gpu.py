@@ -172,3 +172,53 @@ def test_wgrid_single_steps_equal_rollout(gpu_device):
         assert torch.equal(o1[k], o2) and torch.equal(r1[k], r2) and torch.equal(d1[k], d2) and torch.equal(t1[k], t2)
     assert e1.rng_state == e2.rng_state
     assert e1.metrics() == e2.metrics()
+
+
+def _goal_adjacent_cells(ora):
+    """Flat cells from which some move lands on the (fixed) goal, and the goal itself (msrooms.py:401-407)."""
+    shape = ora.grid.shape
+    goal = np.asarray(ora.goal[0])
+    out = [int(np.ravel_multi_index(tuple(goal), shape))]
+    for c in np.asarray(ora.valid_agent).ravel():
+        zyx = np.array(np.unravel_index(int(c), shape))
+        if any((zyx + off == goal).all() for off in np.asarray(ora.actions)):
+            out.append(int(c))
+    return np.unique(np.array(out, np.int64))
+
+
+@pytest.mark.parametrize("B,frac", [(1 << 20, 0.9), (1 << 20, 0.2), (1 << 20, 0.05), (1 << 17, 0.5)])
+def test_wgrid_goal_crowd_bit_exact(B, frac, gpu_device):
+    """Most (or many) envs put on goal-adjacent cells with set_state: the early reset count lists every such env.
+    frac 0.9 overflows the per-block list (the count falls back to the step's masks) and resets hundreds of
+    thousands of envs at once (slow path, env-wave placement); 0.2 / 0.05 keep the list under its cap with a few
+    hundred / tens of resetters per block (control- and env-wave placement). Every later step is bit-exact too."""
+    env = _fourrooms(B, gpu_device)
+    assert env.query("wgrid") == 1
+    ora = gridworld.FourRoomsOracle(B, 1, obs_type="hansen")
+    _reset_obs(env, 17)
+    ora.reset_seed(17)
+    near = _goal_adjacent_cells(ora)
+    assert len(near) >= 2
+    rng = np.random.default_rng(5)
+    valid = np.asarray(ora.valid_agent).ravel()
+    cells = np.where(rng.random(B) < frac, rng.choice(near, B), rng.choice(valid, B)).astype(np.int64)
+    el = rng.integers(0, ora.time_limit + 1, B).astype(np.int64)
+    env.set_state(agent_cells=cells.astype(np.int32), elapsed=el.astype(np.int32))
+    ora.agent = np.array(np.unravel_index(cells, ora.grid.shape)).swapaxes(0, 1).astype(int)
+    ora.elapsed = el.astype(int)
+    _check_chunks(env, ora, (6, 1, 9), action_seed=11, n_act=4)
+
+
+@pytest.mark.parametrize("tmode", [4, 512, 1024, 512 | 1024])
+def test_wgrid_schedule_variants_bit_exact(tmode, gpu_device):
+    """Test-only schedules of the windowed kernel (gp_debug_set wg_tmode): 4 = the count published from the masks
+    after the full transitions (no early count), 512 = every window word re-derived from the window's base state
+    (the path a high-half tie takes), 1024 = the env waves place every step's resetters."""
+    from gym_po_amd._lib import debug_knobs
+    B = 1 << 18
+    with debug_knobs(wg_tmode=tmode):
+        env = _fourrooms(B, gpu_device)
+    assert env.query("wgrid") == 1
+    ora = gridworld.FourRoomsOracle(B, 1, obs_type="hansen")
+    np.testing.assert_array_equal(_reset_obs(env, 23).astype(np.int64), np.asarray(ora.reset_seed(23)).astype(np.int64))
+    _check_chunks(env, ora, (7, 12), action_seed=2, n_act=4)

@@ -2,13 +2,16 @@
 
     python gym-po-taxi_amd/build.py --stamps && python tools/wstamps.py [B] [K]
 
-Stamps are s_memrealtime (100 MHz, synchronous across XCDs), per block and step k:
-  env wave 0: 0 step start, 1 transitions done, 2 S(y) seen, 3 coarse states done, 4 resetters listed,
-              5 window filled (before B2); env wave 7: 15 window filled
-  control:    6 S(y) + rejection check + window base published, 7 transitions seen, 8 granule publish,
-              9 all-gather done, 10 cells drawn (before B2), 11 after B2, 12 next state done
-  store wave: 13 copy start (after B2), 14 copy issued
-Launch stamps per block: 0 entry, 1 P1 passed (control), 2 P2 passed, 3 step loop done, 4 kernel end.
+Stamps are s_memrealtime (100 MHz, synchronous across XCDs), kept in LDS, for the first 32 steps of a launch,
+per block and step k (round-5 early-count schedule):
+  env wave 0: 16 cells_done seen, 17 resetter cells taken, 0 step start (window regenerated if it missed),
+              12 coarse states done, 1 transitions start
+              (after the window / staging waits), 2 transitions done (lists appended), 3 resetters listed,
+              4 next window filled, 18 next actions converted; env wave 7: 15 next window filled
+  control:    7 S(y) / next window base published, 5 lists + window ready, 6 granule published (early count),
+              8 candidate cells done, 9 all-gather done, 10 cells placed / cells_done, 11 next rejection check done
+  store wave: 13 copy start, 14 copy issued
+Launch stamps per block: 0 entry, 1 P1 passed (control), 3 step loop done, 4 kernel end.
 """
 import ctypes
 import os
@@ -41,16 +44,20 @@ L = _lib.lib()
 fn = L.gp_debug_stamps
 fn.restype = ctypes.c_int
 fn.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
-NS = 256 * 64 * 16
+NS = 256 * 32 * 32
 buf = (ctypes.c_ulonglong * (NS + 256 * 8))()
 fn(env._handle, buf, NS + 256 * 8)
 raw = np.frombuffer(buf, dtype=np.uint64).astype(np.int64) * 10  # ns
-a = raw[:NS].reshape(256, 64, 16)[:G]
+a = raw[:NS].reshape(256, 32, 32)[:G]
 ls = raw[NS:].reshape(256, 8)[:G]
 t0 = ls[:, 0].min()
+out = os.environ.get("WSTAMPS_RAW")
+if out:
+    np.savez_compressed(out, a=a, ls=ls)
 print(f"B={B} K={K} G={G} E={env.query('wgrid_block_envs')} H={env.query('wgrid_halo')}")
-print(f"launch: entry spread {ls[:, 0].max() - t0} ns; P1 passed (max) {ls[:, 1].max() - t0}; P2 passed (max) "
-      f"{ls[:, 2].max() - t0}; loop done (max) {ls[:, 3].max() - t0}; kernel end (max) {ls[:, 4].max() - t0} ns")
+print(f"launch: entry spread {ls[:, 0].max() - t0} ns; P1 passed (max) {ls[:, 1].max() - t0}; "
+      f"loop done (max) {ls[:, 3].max() - t0}; kernel end (max) {ls[:, 4].max() - t0} ns")
+print(f"first step: env start (max) {a[:, 0, 0].max() - t0}; first publish (max) {a[:, 0, 6].max() - t0} ns")
 env.set_profiling(True)
 for _ in range(5):
     env.rollout(acts)
@@ -59,33 +66,39 @@ env.set_profiling(False)
 print(f"event-timed kernel: {ms / nk * 1e3:.1f} us per launch ({ms / nk / K * 1e6:.0f} ns/step)")
 if K < 8:
     sys.exit(0)
-kk = min(K, 64)
+kk = min(K, 32)
 x = a[:, 2:kk - 1]
+nx = a[:, 3:kk]   # the next step's stamps
+pv = a[:, 1:kk - 2]  # the previous step's stamps
 
 
 def rep(name, d):
-    print(f"  {name:44s} median {np.median(d):7.0f} ns  p90 {np.percentile(d, 90):7.0f}  max-over-blocks(median) "
+    print(f"  {name:46s} median {np.median(d):7.0f} ns  p90 {np.percentile(d, 90):7.0f}  max-over-blocks(median) "
           f"{np.median(d.max(0)):7.0f}")
 
 
-step = a[:, 3:kk, 0] - a[:, 2:kk - 1, 0]
-rep("step (env wave 0 start -> next start)", step)
-rep("env: transitions (0->1)", x[:, :, 1] - x[:, :, 0])
-rep("env: S(y) wait (1->2)", x[:, :, 2] - x[:, :, 1])
-rep("env: coarse states (2->3)", x[:, :, 3] - x[:, :, 2])
-rep("env: resetter listing (3->4)", x[:, :, 4] - x[:, :, 3])
-rep("env: window fill (4->5)", x[:, :, 5] - x[:, :, 4])
-rep("env: B2 wait (5 -> ctrl 11)", x[:, :, 11] - x[:, :, 5])
-rep("env wave 7 window done - wave 0 (15-5)", x[:, :, 15] - x[:, :, 5])
-rep("ctrl: step-start work (prev 12 -> 6)", a[:, 3:kk, 6] - a[:, 2:kk - 1, 12])
-rep("ctrl: after B2 -> next state (11->12)", x[:, :, 12] - x[:, :, 11])
-rep("ctrl: trans wait (6->7)", x[:, :, 7] - x[:, :, 6])
-rep("ctrl: publish (7->8)", x[:, :, 8] - x[:, :, 7])
+rep("step (env wave 0 start -> next start)", nx[:, :, 0] - x[:, :, 0])
+rep("env: take cells + coarse states (0->12)", x[:, :, 12] - x[:, :, 0])
+rep("env: window / staging wait (12->1)", x[:, :, 1] - x[:, :, 12])
+rep("env: transitions + lists (1->2)", x[:, :, 2] - x[:, :, 1])
+rep("env: masks wait + resetter listing (2->3)", x[:, :, 3] - x[:, :, 2])
+rep("env: S(y) wait + next window fill (3->4)", x[:, :, 4] - x[:, :, 3])
+rep("env: next actions converted (4->18)", x[:, :, 18] - x[:, :, 4])
+rep("env: wait cells_done (18->next 16)", nx[:, :, 16] - x[:, :, 18])
+rep("env: take cells (16->17)", x[:, :, 17] - x[:, :, 16])
+rep("env: regeneration (17->0)", x[:, :, 0] - x[:, :, 17])
+rep("env wave 7 fill done - wave 0 (15-4)", x[:, :, 15] - x[:, :, 4])
+rep("ctrl: S(y) + window base (prev 11 -> 7)", x[:, :, 7] - pv[:, :, 11])
+rep("ctrl: wait lists/window (7 -> 5)", x[:, :, 5] - x[:, :, 7])
+rep("ctrl: resolve + publish (5->6)", x[:, :, 6] - x[:, :, 5])
+rep("ctrl: candidates (6->8)", x[:, :, 8] - x[:, :, 6])
 rep("ctrl: gather (8->9)", x[:, :, 9] - x[:, :, 8])
-rep("ctrl: cells (9->10)", x[:, :, 10] - x[:, :, 9])
-rep("ctrl: B2 wait (10->11)", x[:, :, 11] - x[:, :, 10])
-pub = x[:, :, 8]
-print(f"  publish spread across blocks (max-min)       median {np.median(pub.max(0) - pub.min(0)):.0f} ns")
-print(f"  gather done - last publish                   median {np.median(x[:, :, 9] - pub.max(0)[None]):.0f} ns")
+rep("ctrl: publish -> gather done (6->9)", x[:, :, 9] - x[:, :, 6])
+rep("ctrl: r2s wait + cells + next state (9->10)", x[:, :, 10] - x[:, :, 9])
+rep("ctrl: next rejection check (10->11)", x[:, :, 11] - x[:, :, 10])
+pub = x[:, :, 6]
+print(f"  publish spread across blocks (max-min)         median {np.median(pub.max(0) - pub.min(0)):.0f} ns")
+print(f"  gather done - last publish                     median {np.median(x[:, :, 9] - pub.max(0)[None]):.0f} ns")
+print(f"  window ready (ctrl 5) - env fill done (4, prev)  median {np.median(x[:, :, 5] - pv[:, :, 4]):.0f} ns")
 rep("store: copy issue (13->14)", x[:, :, 14] - x[:, :, 13])
 print("block 0, step 10 (ns from env start):", (a[0, 10] - a[0, 10, 0]).tolist())
