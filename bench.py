@@ -23,16 +23,18 @@ import sys
 import time
 
 # Kernel arguments in device memory (a HIP runtime setting, read when HIP initialises: set before torch loads).
-# The fused kernel's parameter block is ~600 B; where the runtime keeps kernel arguments in host memory,
-# every wave of the 256 persistent blocks reads them across PCIe at launch: +1.5-8 µs per launch, by box
-# (DESIGN.md §5). An explicit setting in the environment wins.
+# The headline's windowed kernel takes a 52-B argument block (a pointer to its device-resident parameters, K and
+# five buffers); the older fused kernels and the C-ROOMS exact-mode draw calls take parameter blocks of ~200-600 B
+# by value, which every wave reads at launch: +1.5-8 µs per launch, by box, where the runtime keeps them in host
+# memory. The package itself leaves the variable alone; an explicit setting wins.
 os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "gym-po-taxi_amd"))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec); 6.29 TB/s measured float4 copy
-# Algorithmic bytes per env-step of the numpy-mode step kernel:
+# Algorithmic bytes per env-step of a ONE-step numpy-mode launch of the two-kernel path (grid_step_numpy +
+# grid_resolve_numpy; only used when a timed launch is a single step, never by the default or driver lines):
 #   read  action int32 (4) + state agent|elapsed uint32 (4)
 #   write state (4) + obs int32 (4) + reward f32 (4) + terminated u8 (1) + truncated u8 (1)
 BYTES_PER_ENV_STEP = 22
@@ -64,23 +66,24 @@ def _anttag(B, dev, mode):
 # The headline (BASELINE.json configs[1]) and the other single-GPU configs, measured the same way.
 # bytes: algorithmic bytes per env-step of a fused rollout launch; state: bytes per env read + written
 # once per launch in SURVEY.md §8(d)'s canonical layout (agent / goal / elapsed int32 = 12 B each way: "14 B + 24/K";
-# C-ROOMS 20 B each way). The kernels keep a packed 4-8 B state, so their own traffic is below this count.
+# C-ROOMS 20 B each way): the byte model of `roofline.frac`. state_packed: what the kernels actually keep (one
+# packed uint32 per env each way; C-ROOMS its float64 SoA), reported beside it as `frac_packed_state`.
 WORKLOADS = {
-    "fourrooms": dict(make=_fourrooms, envs=1 << 20, n_actions=4, mode="numpy", bytes=14, state=24, chunk=128,
+    "fourrooms": dict(make=_fourrooms, envs=1 << 20, n_actions=4, mode="numpy", bytes=14, state=24, state_packed=8, chunk=128,
                       metric=HEADLINE_METRIC, dtype="int32",
                       desc="configs[1]: FourRooms 11x11 (FR_MAP) Hansen-4 obs, {B} envs per GPU, "
                            "MultistoryFourRoomsEnv(grid_z=1, obs_type='hansen')"),
-    "taxi": dict(make=_taxi_onehot, envs=1 << 22, n_actions=5, mode="philox", bytes=4 + 320 + 4 + 1 + 1, state=24,
+    "taxi": dict(make=_taxi_onehot, envs=1 << 22, n_actions=5, mode="philox", bytes=4 + 320 + 4 + 1 + 1, state=24, state_packed=8,
                  metric="env steps/sec, PO-Taxi 5x5 Hansen one-hot obs (uint8[320]) at 4M envs per GPU",
                  dtype="uint8", kernel="taxi_rollout<16,false>", chunk=4,
                  desc="configs[2]: PO-Taxi 5x5 (TAXI_MAP) Hansen obs one-hot uint8[B,320], {B} envs per GPU, "
                       "HansenTaxiVecEnv(one_hot=True)"),
-    "crooms": dict(make=_crooms, envs=1 << 21, n_actions=None, mode="philox", bytes=8 + 8 + 4 + 1 + 1, state=40,
+    "crooms": dict(make=_crooms, envs=1 << 21, n_actions=None, mode="philox", bytes=8 + 8 + 4 + 1 + 1, state=40, state_packed=40,
                    metric="env steps/sec, C-ROOMS layout 4 continuous (y,x) + N(0,0.2) action noise, 2M envs per GPU",
                    dtype="f64 state / f32 I/O", kernel="crooms_rollout<GP_OBS_F32,false>", chunk=128,
                    desc="configs[4]: C-ROOMS layout 4, yx actions f32 U[-1,1]^2, vector_mdp obs f32[B,2], {B} envs per "
                         "GPU, CRoomsEnv(obs_type='vector_mdp')"),
-    "anttag": dict(make=_anttag, envs=1 << 21, n_actions=5, mode="philox", bytes=4 + 16 + 4 + 1 + 1, state=24,
+    "anttag": dict(make=_anttag, envs=1 << 21, n_actions=5, mode="philox", bytes=4 + 16 + 4 + 1 + 1, state=24, state_packed=8,
                    metric="env steps/sec, grid Ant-Tag 10x10 (build-defined), 2M envs per GPU (16M on 8 GPUs)",
                    dtype="int32", kernel="anttag_rollout<false>",
                    desc="configs[3]: grid Ant-Tag 10x10, {B} envs per GPU (2M x 8 GPUs = 16M), AntTagGridEnv()"),
@@ -416,9 +419,11 @@ def main():
     if args.workload != "fourrooms" or steps_per_launch > 1.5:
         # fused launch of several steps; state read+written once per launch
         bytes_per_launch = B * (W["bytes"] * steps_per_launch + W["state"])
+        bytes_packed = B * (W["bytes"] * steps_per_launch + W["state_packed"])
     else:
-        bytes_per_launch = B * BYTES_PER_ENV_STEP
+        bytes_per_launch = bytes_packed = B * BYTES_PER_ENV_STEP
     achieved = bytes_per_launch / (kavg_ms * 1e-3) / 1e9
+    achieved_packed = bytes_packed / (kavg_ms * 1e-3) / 1e9
 
     m = shard.allreduce_metrics(env.metrics(), dev)  # RCCL: the only collective (episode statistics)
 
@@ -489,6 +494,10 @@ def main():
                    "parallelism": f"independent env shards x{world}", "steps_per_launch_call": C},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "byte_model": (f"SURVEY 8(d): {W['bytes']} B per env-step + {W['state']} B per env per launch "
+                                    "(canonical state layout)"),
+                     "frac_packed_state": achieved_packed / HBM_PEAK_GBS,
+                     "bytes_per_launch_packed_state": bytes_packed,
                      "traffic_over_algorithmic": traffic / bytes_per_launch if traffic else None,
                      "traffic_source": traffic_src,
                      "kernel": W.get("kernel") or (kernel_name if kernel_name else ("grid_rollout_numpy<GP_OBS_HANSEN,2,4,true>" if steps_per_launch > 1.5

@@ -29,9 +29,18 @@ def deps():
     return sources() + glob.glob(os.path.join(HERE, "csrc", "*.h")) + [os.path.join(ROOT, "include", "gym_po_amd.h")]
 
 
-def up_to_date():
+def up_to_date(key=None):
+    """The library is newer than every source and was built with the same compiler and flags (`key`, kept in
+    libgympo_amd.so.key): a changed GP_OFFLOAD_ARCH / HIPCC / --debug rebuilds it."""
     if not os.path.exists(OUT):
         return False
+    if key is not None:
+        try:
+            with open(OUT + ".key") as f:
+                if f.read().strip() != key:
+                    return False
+        except OSError:
+            return False
     t = os.path.getmtime(OUT)
     return all(os.path.getmtime(d) <= t for d in deps())
 
@@ -39,8 +48,6 @@ def up_to_date():
 def build(force=False, debug=False, verbose=True, stamps=False, asan=False):
     """Compile each csrc/*.hip to an object in parallel (one hipcc per source), then link the .so."""
     out = OUT.replace(".so", "_stamps.so") if stamps else (OUT.replace(".so", "_asan.so") if asan else OUT)
-    if not force and not stamps and not asan and up_to_date():
-        return OUT
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     flags = [f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-O1" if debug else "-O3", "-Wno-unused-result",
              "-I", os.path.join(ROOT, "include")]
@@ -55,6 +62,8 @@ def build(force=False, debug=False, verbose=True, stamps=False, asan=False):
     # objects are keyed on the compiler and every flag (arch included): a changed GP_OFFLOAD_ARCH / HIPCC never
     # links objects built for another target
     key = hashlib.sha1(" ".join([hipcc] + flags).encode()).hexdigest()[:10]
+    if not force and not stamps and not asan and up_to_date(key):
+        return OUT
     kind = "stamps" if stamps else ("asan" if asan else ("debug" if debug else "release"))
     objdir = os.path.join(HERE, "build", kind + "-" + key)
     os.makedirs(objdir, exist_ok=True)
@@ -81,6 +90,9 @@ def build(force=False, debug=False, verbose=True, stamps=False, asan=False):
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     os.replace(out + ".tmp", out)
+    if out == OUT:
+        with open(OUT + ".key", "w") as f:
+            f.write(key + "\n")
     return out
 
 

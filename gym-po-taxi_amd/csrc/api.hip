@@ -231,6 +231,21 @@ int gp_debug_set(const char* key, int64_t value) {
 void gp_debug_reset(void) { g_dbg = GpDebugKnobs{}; }
 int gp_abi_version(void) { return GP_ABI_VERSION; }
 
+// Makes the env's device current for one C-ABI call and gives the calling thread its own current device back on
+// return (a caller whose current device is another GPU, e.g. torch's, must not find it switched afterwards).
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    int cur = -1;
+    if (hipGetDevice(&cur) == hipSuccess && cur != dev && hipSetDevice(dev) == hipSuccess) prev = cur;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  DeviceGuard(const DeviceGuard&) = delete;
+  DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
+
 int gp_create(int kind, const void* config, int64_t num_envs, int device, int rng_mode, gp_env** out) {
   if (!out || !config) {
     gp_set_error("gp_create: null argument");
@@ -247,7 +262,7 @@ int gp_create(int kind, const void* config, int64_t num_envs, int device, int rn
     gp_set_error("gp_create: device %d not present (%d devices)", device, ndev);
     return GP_E_INVALID;
   }
-  GP_HIP_CHECK(hipSetDevice(device));
+  DeviceGuard guard(device);
   int err = GP_OK;
   std::unique_ptr<EnvBackend> be;
   switch (kind) {
@@ -272,13 +287,11 @@ int gp_create(int kind, const void* config, int64_t num_envs, int device, int rn
 void gp_destroy(gp_env* env) { delete env; }
 
 #define GP_REQUIRE_ENV()                 \
-  do {                                   \
-    if (!env || !env->be) {              \
-      gp_set_error("null env handle");   \
-      return GP_E_INVALID;               \
-    }                                    \
-    (void)hipSetDevice(env->be->device); \
-  } while (0)
+  if (!env || !env->be) {                \
+    gp_set_error("null env handle");     \
+    return GP_E_INVALID;                 \
+  }                                      \
+  DeviceGuard gp_device_guard_(env->be->device)
 
 int gp_obs_info(const gp_env* env, int* dtype, int* width) {
   if (!env || !env->be) {
@@ -388,7 +401,7 @@ int gp_plan_run(gp_plan* plan) {
     gp_set_error("gp_plan_run: null plan");
     return GP_E_INVALID;
   }
-  (void)hipSetDevice(plan->env->be->device);  // the env's device, whatever the calling thread's current one is
+  DeviceGuard guard(plan->env->be->device);  // the env's device, whatever the calling thread's current one is
   return plan->env->be->rollout(plan->K, plan->act, plan->obs, plan->rew, plan->term, plan->trunc, plan->stream);
 }
 

@@ -112,7 +112,11 @@ __device__ __forceinline__ void stage_tables(const CrDev& p, uint8_t* lds) {
 // IEEE double ops without contraction, so tail values equal numpy's bit for bit; host copy gp_log1p_libm for
 // the CPU test against libm (tests/test_log1p_cpu.py). exp of the wedge test: glibc 2.35's exp restated
 // (gp_libm.h, pinned against libm by tests/test_libm_cpu.py), so wedge accepts / rejects are numpy's exactly.
-__device__ __forceinline__ double zexp(double y) { return gp_libm::exp<true>(y); }
+// The host libm's exp build (gp_exp_host_variant: 1 the -mfma build, 0 the plain one), set at create time.
+__device__ int g_crooms_exp_fma = 1;
+__device__ __forceinline__ double zexp(double y) {
+  return g_crooms_exp_fma ? gp_libm::exp<true>(y) : gp_libm::exp<false>(y);
+}
 GP_HD int32_t zhi(double x) { return (int32_t)(__builtin_bit_cast(uint64_t, x) >> 32); }
 GP_HD double zset_hi(double x, int32_t h) {
   return __builtin_bit_cast(double, (__builtin_bit_cast(uint64_t, x) & 0xFFFFFFFFull) | ((uint64_t)(uint32_t)h << 32));
@@ -3169,6 +3173,14 @@ std::unique_ptr<EnvBackend> make_crooms_backend(const gp_crooms_config* cfg, int
   if (e) {
     *err = e;
     return nullptr;
+  }
+  if (rng_mode == GP_RNG_NUMPY) {  // the ziggurat wedge's exp(-x^2/2) from the host's libm build
+    const int fma = gp_exp_host_variant() == 0 ? 0 : 1;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_crooms_exp_fma), &fma, sizeof(fma)) != hipSuccess) {
+      gp_set_error("crooms: hipMemcpyToSymbol(exp variant) failed");
+      *err = GP_E_HIP;
+      return nullptr;
+    }
   }
   return be;
 }

@@ -522,6 +522,9 @@ struct NpCats {
   const uint64_t* etab;  // exp table (LDS copy)
 };
 
+// The host libm's exp build (gp_exp_host_variant: 1 the -mfma build, 0 the plain one), set at create time.
+__device__ int g_taxi_exp_fma = 1;
+
 // One multinomial row from state s: the argmax category; `used` = doubles drawn.
 __device__ __forceinline__ uint32_t np_row(const TaxiNpDev& q, const NpCats& c, u128 s, u128 inc, uint32_t& used,
                                            uint32_t& flags) {
@@ -533,7 +536,8 @@ __device__ __forceinline__ uint32_t np_row(const TaxiNpDev& q, const NpCats& c, 
     int64_t X = 0;
     if (pp * (double)dn <= 30.0) {  // random_binomial -> random_binomial_inversion(dn, pp)
       const double qq = c.q[k];
-      const double qn = gp_libm::exp<true>((double)dn * c.lq[k], c.etab);
+      const double qn = g_taxi_exp_fma ? gp_libm::exp<true>((double)dn * c.lq[k], c.etab)
+                                       : gp_libm::exp<false>((double)dn * c.lq[k], c.etab);
       const double np = (double)dn * pp;
       const double bnd = np + 10.0 * __builtin_sqrt(np * qq + 1.0);
       const int64_t bound = (int64_t)((double)dn < bnd ? (double)dn : bnd);
@@ -1275,6 +1279,14 @@ std::unique_ptr<EnvBackend> make_taxi_backend(const gp_taxi_config* cfg, int64_t
   if (e) {
     *err = e;
     return nullptr;
+  }
+  if (rng_mode == GP_RNG_NUMPY) {  // numpy's q^n = exp(n log q) from the host's libm build
+    const int fma = gp_exp_host_variant() == 0 ? 0 : 1;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_taxi_exp_fma), &fma, sizeof(fma)) != hipSuccess) {
+      gp_set_error("taxi: hipMemcpyToSymbol(exp variant) failed");
+      *err = GP_E_HIP;
+      return nullptr;
+    }
   }
   return be;
 }

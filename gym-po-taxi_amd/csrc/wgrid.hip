@@ -749,13 +749,13 @@ struct Acc {
 // List this wave's goal-adjacent envs (nr: entries ent) and its truncation count for a step: one LDS atomic per
 // wave reserves the entries' places.
 template <int NS>
-__device__ __forceinline__ void append_near(uint32_t* NLp, uint32_t* nlcp, const bool (&nr)[NS],
-                                            const uint32_t (&ent)[NS], uint32_t ntr) {
+__device__ __forceinline__ void append_near(uint32_t* NLp, uint32_t* nlcp, uint32_t nrm, const uint32_t (&ent)[NS],
+                                            uint32_t ntr) {
   const int lane = threadIdx.x & 63;
   uint32_t tot = 0, pos[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
-    const uint64_t m = ballot(nr[s]);
+    const uint64_t m = ballot((nrm >> s) & 1u);
     pos[s] = tot + mbcnt(m);
     tot += popc(m);
   }
@@ -766,7 +766,7 @@ __device__ __forceinline__ void append_near(uint32_t* NLp, uint32_t* nlcp, const
     base = (uint32_t)__builtin_amdgcn_readlane((int)base, 0) & 0xFFFFu;
 #pragma unroll
     for (int s = 0; s < NS; ++s)
-      if (nr[s] && base + pos[s] < (uint32_t)NCAP) NLp[base + pos[s]] = ent[s];
+      if (((nrm >> s) & 1u) && base + pos[s] < (uint32_t)NCAP) NLp[base + pos[s]] = ent[s];
   }
 }
 
@@ -789,11 +789,9 @@ __device__ __forceinline__ void env_take(const WgParams& P, WgShared& sh, const 
   const u128 Sy = mk128(sh.sy[kp & 1][0], sh.sy[kp & 1][1]);
   const uint64_t* CS = L.CS(kp);
   const uint32_t R = sh.R, h = sh.h, u = sh.u, n = sh.nrp;
-  bool nr[NS];
-  uint32_t ent[NS];
+  uint32_t nrm = 0, ent[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
-    nr[s] = false;
     ent[s] = 0;
     if (!((dn >> s) & 1u)) continue;
     uint32_t p = R + pre[s] + mbcnt(bm[s]);
@@ -810,10 +808,10 @@ __device__ __forceinline__ void env_take(const WgParams& P, WgShared& sh, const 
     const uint32_t v = tb.avalid(lemire_value(word, (uint32_t)P.n_agent));
     st[2 * (s * 512 + lg)] = (uint16_t)v;
     ae[s] = v & 0xFFFFu;
-    nr[s] = list_next && (v >> 16) != 0u;
+    nrm |= (list_next && (v >> 16) != 0u) ? (1u << s) : 0u;
     ent[s] = (uint32_t)(s * 512 + lg) | (ai[s] << 12) | ((v >> 16) << 16);
   }
-  if (list_next) append_near<NS>(L.NL(kp + 1), &sh.nlc[(kp + 1) & 1], nr, ent, 0u);
+  if (list_next) append_near<NS>(L.NL(kp + 1), &sh.nlc[(kp + 1) & 1], nrm, ent, 0u);
 }
 
 // Fill a window (high halves): word j = m * 512 + lg is the base state advanced by j (this lane: jump by lg, then
@@ -875,18 +873,19 @@ __device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Ta
     acc.lens += ae[s] >> 16;  // episode lengths: + elapsed at the start - elapsed at the end + steps
   }
   {  // step 0's truncations and goal-adjacent envs
-    bool nr[NS];
-    uint32_t ent[NS], ntr = 0;
+    uint32_t nrm = 0, trm = 0, ent[NS], ntr = 0;
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       const uint32_t c = ae[s] & 0xFFFFu, el = (ae[s] >> 16) + 1u;
-      const bool tr = el > tlim;
+      const uint32_t tr = el > tlim ? 1u : 0u;
       const uint32_t gm = tb.gmp[c];
-      nr[s] = !tr && gm != 0u;
+      trm |= tr << s;
+      nrm |= (!tr && gm != 0u) ? (1u << s) : 0u;
       ent[s] = (uint32_t)(s * 512 + lg) | (ai[s] << 12) | (gm << 16);
-      ntr += popc(ballot(tr));
     }
-    append_near<NS>(L.NL(0), &sh.nlc[0], nr, ent, ntr);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) ntr += popc(ballot((trm >> s) & 1u));
+    append_near<NS>(L.NL(0), &sh.nlc[0], nrm, ent, ntr);
   }
   lds_release();
   if (lane == 0) {
@@ -951,34 +950,40 @@ __device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Ta
     uint32_t mm[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) mm[s] = tb.mvp[(ae[s] & 0xFFFFu) * NA + fe[s]];
-    uint32_t sv[NS], ent[NS], ntr = 0;
-    bool nr[NS];
+    // Per-slot outcomes as bits of VGPR words (bit s), not as live lane masks: eight slots' worth of 64-bit masks
+    // would not fit the SGPRs and spill through v_writelane / v_readlane.
+    uint32_t sv[NS], ent[NS], trm = 0, nrm = 0;
     dn = 0;
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       const uint32_t m = mm[s];
       const uint32_t nc = m & 0x7FFFu, blocked = (m >> 15) & 1u, gmn = m >> 16;
       const uint32_t el = (ae[s] >> 16) + 1u;
-      const bool term = nc == goal, trunc = el > tlim, done = term || trunc;
-      sv[s] = nc | ((uint32_t)term << 16) | ((uint32_t)trunc << 17) | (blocked << 18);
+      const uint32_t term = nc == goal ? 1u : 0u, trunc = el > tlim ? 1u : 0u, done = term | trunc;
+      sv[s] = nc | (term << 16) | (trunc << 17) | (blocked << 18);
       ae[s] = done ? nc : (nc | (el << 16));
-      bm[s] = ballot(done);
-      dn |= (uint32_t)done << s;
-      acc.ngoal += term ? 1u : 0u;
-      acc.nwall += (blocked && !term) ? 1u : 0u;
+      dn |= done << s;
+      acc.ngoal += term;
+      acc.nwall += blocked & (term ^ 1u);
       // the next step: truncated for sure, or goal-adjacent (its word decides); resetters are the control's
-      const bool tr1 = !done && el + 1u > tlim;
-      ntr += popc(ballot(tr1));
-      nr[s] = !done && !tr1 && gmn != 0u;
+      const uint32_t tr1 = (done ^ 1u) & (el + 1u > tlim ? 1u : 0u);
+      trm |= tr1 << s;
+      nrm |= ((done | tr1) ^ 1u) & (gmn != 0u ? 1u : 0u) ? (1u << s) : 0u;
       ent[s] = (uint32_t)(s * 512 + lg) | (an[s] << 12) | (gmn << 16);
+    }
+#pragma unroll
+    for (int s = 0; s < NS; ++s) reinterpret_cast<uint32_t*>(stg)[s * 512 + lg] = sv[s];
+    uint32_t ntr = 0;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      bm[s] = ballot((dn >> s) & 1u);
+      ntr += popc(ballot((trm >> s) & 1u));
     }
     if (lane == 0) {
 #pragma unroll
       for (int s = 0; s < NS; ++s) sh.mask[s][w] = bm[s];
     }
-#pragma unroll
-    for (int s = 0; s < NS; ++s) reinterpret_cast<uint32_t*>(stg)[s * 512 + lg] = sv[s];
-    if (k + 1 < K) append_near<NS>(L.NL(k + 1), &sh.nlc[(k + 1) & 1], nr, ent, ntr);
+    if (k + 1 < K) append_near<NS>(L.NL(k + 1), &sh.nlc[(k + 1) & 1], nrm, ent, ntr);
     acc.eps += (uint32_t)__builtin_popcount(dn);
     lds_release();
     if (lane == 0) lds_add(&sh.trans_done, 1u);

@@ -288,6 +288,11 @@ int gp_zig_log1p_neg(const double* u, double* out, int64_t n);
  * distributions.c). fma != 0: the -mfma build glibc selects on CPUs with FMA (x86-64 ifunc), else the plain one.
  * Host-only check entry for the CPU tests. */
 int gp_exp_libm(const double* x, double* out, int64_t n, int fma);
+/* Which build of the C library's exp this host runs (the one numpy's distributions get): 1 = the -mfma build,
+ * 0 = the plain build, -1 = neither restatement matches (exact-stream exp-dependent branches then follow the FMA
+ * build: parity unpinned). Decided once per process by comparing libm with both restatements where they differ;
+ * the exact-stream kernels (Taxi numpy-mode resets, C-ROOMS exact-mode wedge) use that build on the device. */
+int gp_exp_host_variant(void);
 /* P(argmax = k), k < m, for Multinomial(n, uniform over m) counts, ties to the first index:
  * the law of TaxiVecEnv._reset_mask (extended_taxi.py:344-352). Returns m. */
 int gp_argmax_multinomial_distribution(int m, int n, double* out);

@@ -2,10 +2,11 @@
 
 bench.py's headline is `MultistoryFourRoomsEnv(2^20, grid_z=1, obs_type="hansen")` in numpy mode,
 stepped through `rollout_plan` with chunks of C steps per launch (C = 20 at the driver's
-`--steps 20`, 128 by default). At 2^20 envs on a 256-CU MI355X that is one persistent launch of
-`grid_rollout_numpy<GP_OBS_HANSEN, 2, 4, true>`: 256 blocks x 2 tiles of 2048 envs, outputs staged
-in LDS and copied out by the store waves while the env waves run the next step, env state in
-registers across the K steps. These tests run that kernel with K > 1 and compare EVERY step's obs,
+`--steps 20`, 128 by default). At 2^20 envs on a 256-CU MI355X that is one persistent launch of the
+windowed kernel `wgrid_rollout<8, 4>` (csrc/wgrid.hip): 256 blocks of 4096 envs, each step's reset count
+published early from the truncations and the goal-adjacent envs' words, outputs staged in LDS and copied out
+by the store waves while the env waves run the next step, env state in registers across the K steps.
+These tests run that kernel with K > 1 and compare EVERY step's obs,
 reward, terminated and truncated, plus the final env state and PCG64 state, against the numpy
 oracle (tests/test_oracle_golden.py pins the oracle to reference-generated fixtures):
 - K = 20 and K = 128 launches (the driver's and bench's chunks), one after the other;

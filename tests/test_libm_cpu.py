@@ -52,3 +52,29 @@ def test_exp_equals_libm_bit_for_bit():
     got, want = _ours(x, 1), _libm_exp(x)
     bad = np.flatnonzero(got.view(np.uint64) != want.view(np.uint64))
     assert bad.size == 0, f"{bad.size} mismatches, e.g. x={x[bad[:3]]}"
+
+
+def test_host_variant_detection():
+    """gp_exp_host_variant() names the build this machine's libm runs (the exact-stream kernels use it): the FMA
+    build on CPUs with FMA (glibc's ifunc), the plain build otherwise."""
+    from gym_po_amd import _lib as L
+    v = L.lib().gp_exp_host_variant()
+    assert v in (0, 1)
+    assert v == (1 if _cpu_has_fma() else 0)
+    rng = np.random.default_rng(3)
+    x = rng.uniform(-60.0, 20.0, 50_000)
+    assert np.array_equal(_ours(x, v).view(np.uint64), _libm_exp(x).view(np.uint64))
+
+
+def test_plain_variant_is_a_faithful_exp():
+    """The non-FMA restatement (what a host without FMA runs) is self-consistent: within one ulp of the FMA build
+    everywhere, differing from it on some inputs (so the two are really distinct code paths), and exact on the
+    special cases."""
+    rng = np.random.default_rng(7)
+    x = np.concatenate([rng.uniform(-745.0, 709.7, 200_000), -0.5 * rng.uniform(0, 3.7, 50_000) ** 2])
+    a, b = _ours(x, 1), _ours(x, 0)
+    ulp = np.abs(a.view(np.int64) - b.view(np.int64))
+    assert ulp.max() <= 1
+    assert (ulp == 1).sum() > 0
+    sp = np.array([0.0, -0.0, np.inf, -np.inf, 709.79, -746.0])
+    np.testing.assert_array_equal(_ours(sp, 0), _ours(sp, 1))

@@ -5,6 +5,7 @@ Usage (GPU box): python tools/crooms_numpy_rate.py  -> one JSON line per (mode, 
 """
 import json
 import os
+os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")  # as bench.py
 import sys
 import time
 
