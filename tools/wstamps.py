@@ -3,13 +3,12 @@
     python gym-po-taxi_amd/build.py --stamps && python tools/wstamps.py [B] [K]
 
 Stamps are s_memrealtime (100 MHz, synchronous across XCDs), kept in LDS, for the first 32 steps of a launch,
-per block and step k (round-5 early-count schedule):
-  env wave 0: 16 cells_done seen, 17 resetter cells taken, 0 step start (window regenerated if it missed),
-              12 coarse states done, 1 transitions start
-              (after the window / staging waits), 2 transitions done (lists appended), 3 resetters listed,
-              4 next window filled, 18 next actions converted; env wave 7: 15 next window filled
-  control:    7 S(y) / next window base published, 5 lists + window ready, 6 granule published (early count),
-              8 candidate cells done, 9 all-gather done, 10 cells placed / cells_done, 11 next rejection check done
+per block and step k (round-5 schedule: early count, per-env PCG states):
+  env wave 0: 16 cells_done seen, 0 states advanced + resetter cells taken (step start), 12 coarse states done,
+              1 transitions start (after the staging wait), 2 transitions done (lists appended), 3 resetters listed,
+              18 next actions converted
+  control:    5 lists ready, 6 granule published (early count), 8 candidate cells done, 9 all-gather done,
+              10 cells placed / cells_done, 11 next rejection check + block base done
   store wave: 13 copy start, 14 copy issued
 Launch stamps per block: 0 entry, 1 P1 passed (control), 3 step loop done, 4 kernel end.
 """
@@ -54,7 +53,7 @@ t0 = ls[:, 0].min()
 out = os.environ.get("WSTAMPS_RAW")
 if out:
     np.savez_compressed(out, a=a, ls=ls)
-print(f"B={B} K={K} G={G} E={env.query('wgrid_block_envs')} H={env.query('wgrid_halo')}")
+print(f"B={B} K={K} G={G} E={env.query('wgrid_block_envs')}")
 print(f"launch: entry spread {ls[:, 0].max() - t0} ns; P1 passed (max) {ls[:, 1].max() - t0}; "
       f"loop done (max) {ls[:, 3].max() - t0}; kernel end (max) {ls[:, 4].max() - t0} ns")
 print(f"first step: env start (max) {a[:, 0, 0].max() - t0}; first publish (max) {a[:, 0, 6].max() - t0} ns")
@@ -78,27 +77,23 @@ def rep(name, d):
 
 
 rep("step (env wave 0 start -> next start)", nx[:, :, 0] - x[:, :, 0])
-rep("env: take cells + coarse states (0->12)", x[:, :, 12] - x[:, :, 0])
-rep("env: window / staging wait (12->1)", x[:, :, 1] - x[:, :, 12])
+rep("env: coarse states (0->12)", x[:, :, 12] - x[:, :, 0])
+rep("env: staging wait (12->1)", x[:, :, 1] - x[:, :, 12])
 rep("env: transitions + lists (1->2)", x[:, :, 2] - x[:, :, 1])
 rep("env: masks wait + resetter listing (2->3)", x[:, :, 3] - x[:, :, 2])
-rep("env: S(y) wait + next window fill (3->4)", x[:, :, 4] - x[:, :, 3])
-rep("env: next actions converted (4->18)", x[:, :, 18] - x[:, :, 4])
+rep("env: next actions converted (3->18)", x[:, :, 18] - x[:, :, 3])
 rep("env: wait cells_done (18->next 16)", nx[:, :, 16] - x[:, :, 18])
-rep("env: take cells (16->17)", x[:, :, 17] - x[:, :, 16])
-rep("env: regeneration (17->0)", x[:, :, 0] - x[:, :, 17])
-rep("env wave 7 fill done - wave 0 (15-4)", x[:, :, 15] - x[:, :, 4])
-rep("ctrl: S(y) + window base (prev 11 -> 7)", x[:, :, 7] - pv[:, :, 11])
-rep("ctrl: wait lists/window (7 -> 5)", x[:, :, 5] - x[:, :, 7])
+rep("env: advance + take cells (16->0)", x[:, :, 0] - x[:, :, 16])
+rep("ctrl: wait lists (prev 11 -> 5)", x[:, :, 5] - pv[:, :, 11])
 rep("ctrl: resolve + publish (5->6)", x[:, :, 6] - x[:, :, 5])
-rep("ctrl: candidates (6->8)", x[:, :, 8] - x[:, :, 6])
+rep("ctrl: S(y) + candidates (6->8)", x[:, :, 8] - x[:, :, 6])
 rep("ctrl: gather (8->9)", x[:, :, 9] - x[:, :, 8])
 rep("ctrl: publish -> gather done (6->9)", x[:, :, 9] - x[:, :, 6])
-rep("ctrl: r2s wait + cells + next state (9->10)", x[:, :, 10] - x[:, :, 9])
-rep("ctrl: next rejection check (10->11)", x[:, :, 11] - x[:, :, 10])
+rep("ctrl: J + r2s wait + cells (9->10)", x[:, :, 10] - x[:, :, 9])
+rep("ctrl: next rejection check + base (10->11)", x[:, :, 11] - x[:, :, 10])
 pub = x[:, :, 6]
 print(f"  publish spread across blocks (max-min)         median {np.median(pub.max(0) - pub.min(0)):.0f} ns")
 print(f"  gather done - last publish                     median {np.median(x[:, :, 9] - pub.max(0)[None]):.0f} ns")
-print(f"  window ready (ctrl 5) - env fill done (4, prev)  median {np.median(x[:, :, 5] - pv[:, :, 4]):.0f} ns")
+print(f"  cells_done -> env transitions done (10 -> next 2)  median {np.median(nx[:, :, 2] - x[:, :, 10]):.0f} ns")
 rep("store: copy issue (13->14)", x[:, :, 14] - x[:, :, 13])
 print("block 0, step 10 (ns from env start):", (a[0, 10] - a[0, 10, 0]).tolist())
