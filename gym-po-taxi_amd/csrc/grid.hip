@@ -2704,7 +2704,7 @@ struct GridBackend : EnvBackend {
       b_limg, b_ofix, b_avo;
   int fused_G = 0, fused_qpt = 0;  // fused numpy rollout geometry (0 = not eligible)
   // windowed numpy rollout (wgrid.hip): G blocks of E = 512 * NS envs; 0 = not eligible
-  int wg_G = 0, wg_E = 0, wg_NS = 0;
+  int wg_G = 0, wg_E = 0, wg_NS = 0, wg_H = 0;
   size_t wg_lds = 0;
   WgParams wg{};
   std::vector<char> wg_img;        // LDS image of its tables (the PCG jump parts rebuilt on every seed)
@@ -2743,6 +2743,7 @@ struct GridBackend : EnvBackend {
     else if (!strcmp(key, "wgrid")) *v = wg_G > 0 ? 1 : 0;
     else if (!strcmp(key, "wgrid_blocks")) *v = wg_G;
     else if (!strcmp(key, "wgrid_block_envs")) *v = wg_E;
+    else if (!strcmp(key, "wgrid_halo")) *v = wg_H;
     else return EnvBackend::query(key, v);
     return GP_OK;
   }
@@ -2956,6 +2957,7 @@ int GridBackend::build_wgrid(const std::vector<uint16_t>& move, const std::vecto
   if (!E) return GP_OK;  // not eligible: the older fused kernel serves this size
   for (int c : ocell)
     if (c < INT32_MIN / 2 || c > INT32_MAX / 2) return GP_OK;
+  const int H = dbg.wg_halo == 512 ? 512 : 256;
   const int nc = d.ncells, na = d.nact;
   // LDS image: j32 | jt8 | move | thr | ocell | avalid, 16-B aligned pieces
   WgLds L{};
@@ -2968,11 +2970,12 @@ int GridBackend::build_wgrid(const std::vector<uint16_t>& move, const std::vecto
   put(L.jt8, sizeof(PcgJump) * 512);
   put(L.move, (size_t)nc * na * 4);
   put(L.thr, (size_t)na * na * 8);
+  put(L.thh, (size_t)na * na * 4);
   put(L.ocell, (size_t)nc * 4);
   put(L.avalid, agent_valid_h.size() * 4);
   put(L.gmc, (size_t)nc);
   L.total = off;
-  const size_t lds = (size_t)wg_dyn_bytes(L.total, E);
+  const size_t lds = (size_t)wg_dyn_bytes(L.total, E, H);
   if (!wgrid_fits(E / 512, na, lds)) return GP_OK;
   // goal-action masks (msrooms.py:401-407): bit a of gm[c] <=> effective action a moves an agent on c onto the goal
   // (a blocked move stays on c). Only envs on cells with gm != 0 can terminate at a step: the early count.
@@ -2982,20 +2985,25 @@ int GridBackend::build_wgrid(const std::vector<uint16_t>& move, const std::vecto
     for (int a = 0; a < na; ++a)
       if ((uint32_t)(move[(size_t)c * na + a] & 0x7FFFu) == goal) gm[(size_t)c] |= (uint8_t)(1u << a);
   auto gm_of = [&](uint32_t c) -> uint32_t { return c < (uint32_t)nc ? gm[c] : 0u; };
-  std::vector<uint32_t> mv(move.size()), av(agent_valid_h.size());
+  std::vector<uint32_t> mv(move.size()), th_hi(thr.size()), av(agent_valid_h.size());
   for (size_t i = 0; i < move.size(); ++i) mv[i] = (uint32_t)move[i] | (gm_of(move[i] & 0x7FFFu) << 16);
   for (size_t i = 0; i < agent_valid_h.size(); ++i) av[i] = (uint32_t)agent_valid_h[i] | (gm_of(agent_valid_h[i]) << 16);
   wg_img.assign((size_t)L.total, 0);
   memcpy(wg_img.data() + L.move, mv.data(), mv.size() * 4);
   std::vector<uint64_t> th(thr.size());
-  for (size_t i = 0; i < thr.size(); ++i) th[i] = thr_on_u64(thr[i]);
+  for (size_t i = 0; i < thr.size(); ++i) {
+    th[i] = thr_on_u64(thr[i]);
+    th_hi[i] = (uint32_t)(th[i] >> 32);
+  }
   memcpy(wg_img.data() + L.thr, th.data(), th.size() * 8);
+  memcpy(wg_img.data() + L.thh, th_hi.data(), th_hi.size() * 4);
   memcpy(wg_img.data() + L.ocell, ocell.data(), ocell.size() * 4);
   memcpy(wg_img.data() + L.avalid, av.data(), av.size() * 4);
   memcpy(wg_img.data() + L.gmc, gm.data(), gm.size());
   wg_G = (int)(B / E);
   wg_E = E;
   wg_NS = E / 512;
+  wg_H = H;
   wg_lds = lds;
   WgParams& w = wg;
   w.B = (int32_t)B;
@@ -3008,17 +3016,20 @@ int GridBackend::build_wgrid(const std::vector<uint16_t>& move, const std::vecto
   w.goal = d.fixed_goal;
   w.thr_agent = d.thr_agent;
   w.time_limit = d.time_limit;
+  w.halo = H;
   w.r_step = d.r_step;
   w.r_wall = d.r_wall;
   w.r_goal = d.r_goal;
   w.spin_limit = d.spin_limit;
   w.fault_block = d.fault_block;
+  w.rw_words = (E + 2 * H) / 512;
+  w.wg_bias = dbg.wg_bias;
   w.tmode = dbg.wg_tmode;
   w.lds = L;
   int e;
   if ((e = b_wgp.alloc(sizeof(WgParams))) || (e = b_wlimg.alloc((size_t)L.total)) ||
       (e = b_wjlane.alloc(sizeof(PcgJump) * 1024)) || (e = b_wjrej.alloc(sizeof(PcgJump) * 64 * (size_t)wg_G)) ||
-      (e = b_wjblk.alloc(sizeof(PcgJump) * (size_t)wg_G)) || (e = b_wslots.alloc(sizeof(uint64_t) * 4 * (size_t)wg_G)))
+      (e = b_wjblk.alloc(sizeof(PcgJump) * 2 * (size_t)wg_G)) || (e = b_wslots.alloc(sizeof(uint64_t) * 4 * (size_t)wg_G)))
     return e;
   w.limg = b_wlimg.as<char>();
   w.jlane = b_wjlane.as<PcgJump>();
@@ -3044,7 +3055,7 @@ int GridBackend::upload_wgrid() {
     jt8[i] = pcg_jump_params((u128)i, inc);
     jt8[256 + i] = pcg_jump_params((u128)(256 * i), inc);
   }
-  std::vector<PcgJump> jl(1024), jr((size_t)64 * wg_G), jb((size_t)wg_G);
+  std::vector<PcgJump> jl(1024), jr((size_t)64 * wg_G), jb(2 * (size_t)wg_G);
   const PcgJump one = pcg_jump_params((u128)1, inc), j32s = pcg_jump_params((u128)32, inc);
   const PcgJump jBp1 = pcg_jump_params((u128)B + 1, inc);  // B + 1
   jl[0] = PcgJump{0, 1, 0, 0};
@@ -3062,10 +3073,12 @@ int GridBackend::upload_wgrid() {
       x = compose(one, x);
     }
     row = compose(j62, row);
-    jb[b] = pcg_jump_params((u128)wg_E * b + 1, inc);
+    jb[2 * b] = pcg_jump_params((u128)B + (u128)(b ? wg_E * b - wg_H : 0), inc);
+    jb[2 * b + 1] = b ? pcg_jump_params((u128)(wg_E * b - wg_H + 1), inc) : PcgJump{0, 1, 0, 0};
   }
   w.jB = pcg_jump_params((u128)B, inc);
   w.j512 = pcg_jump_params((u128)512, inc);
+  w.j1024 = pcg_jump_params((u128)1024, inc);
   w.jt64 = d.jt;
   w.dbg = d.dbg;
   w.ctl = d.ctl;

@@ -25,38 +25,42 @@ struct alignas(32) MetricSlot {
 // ---------------------------------------------------------------- windowed fused rollout (wgrid.hip) ----
 // The envs are cut into G blocks of E = 512 * NS consecutive envs (one workgroup per CU). Parameters live in
 // device memory (WgParams, refreshed on every seed); the launch passes a pointer and the per-call buffers.
-constexpr int WG_NCAP = 1024;  // goal-adjacent envs per block and step the early count lists (more: masks)
+constexpr int WG_HMAX = 512;  // largest halo (u64 draws on each side of a predicted window)
+
+constexpr int WG_NLW = 64;     // goal-adjacent envs per env wave and step the early count lists (more: its masks)
 
 struct WgLds {  // byte offsets of the tables in the LDS image (WgParams::limg, copied verbatim into LDS)
   // move: u32 [ncells][NA] = new cell | blocked << 15 | goal-action mask of the new cell << 16
-  // thr: u64 [NA][NA] thresholds on the full draw
+  // thr: u64 [NA][NA] thresholds on the full draw; thh: u32 [NA][NA] their high halves
   // avalid: u32 [n_agent] = valid agent cell | its goal-action mask << 16; gmc: u8 [ncells] goal-action masks
-  int32_t j32, jt8, move, thr, ocell, avalid, gmc, total;
+  int32_t j32, jt8, move, thr, thh, ocell, avalid, gmc, total;
 };
 
 struct WgParams {
   int32_t B, G, E, NS;          // envs, blocks, envs per block, env slots per env lane (E / 512)
   int32_t nact, ncells, n_agent, goal;
   uint32_t thr_agent;           // Lemire rejection threshold of choice(n_agent)
-  int32_t time_limit;           // episode limit
+  int32_t time_limit, halo;     // episode limit; window halo H (u64 draws each side, multiple of 256, <= WG_HMAX)
   float r_step, r_wall, r_goal;
   uint32_t spin_limit;          // polls before a cross-block wait gives up (flags GridCtl::err)
   int32_t fault_block;          // test knob: this block never publishes (-1 off)
-  int32_t tmode;                // timing-study / test knob (gp_debug_set wg_tmode; 0 in production): see wgrid.hip TM_*
+  int32_t rw_words;             // words per env lane per window fill: (E + 2H) / 512
+  int32_t wg_bias;              // test knob: added to the predicted reset count (forces window misses); 0
+  int32_t tmode;                // timing-study knob (gp_debug_set wg_tmode; 0 in production): see wgrid.hip TM_*
   WgLds lds;
   const char* limg;             // [lds.total] LDS image of the tables
   // Per-lane / per-block constant jumps, all applied to S(x_t), the state at a step's start (B = num envs):
-  const PcgJump* jlane;         // [512][2]: by lg (an env lane's first slot within its block), by B + 32 lg + 1
-                                //   (coarse state lg)
+  const PcgJump* jlane;         // [512][2]: by lg (window fill from its base) and by B + 32 lg + 1 (coarse state lg)
   const PcgJump* jrej;          // [G][64]: by B + 62 beta + l + 1 (rejection-check slice of block beta, lane l)
-  const PcgJump* jblk;          // [G]: by E beta + 1 (the state whose output is block beta's first env word)
+  const PcgJump* jblk;          // [G][2]: by B + E beta - H (beta > 0; B for beta 0): the next window's base after
+                                //   the choice() draws; by E beta - H + 1 (beta > 0; 0 for beta 0): a launch's first
   const PcgJump* jt64;          // radix-64 general jump tables (JT_LEVELS x 64) for the rare paths
-  PcgJump jB, j512;             // jump by B (random(B)), by 512 (an env lane's next slot)
+  PcgJump jB, j512, j1024;      // jump by B (random(B)), by 512 / 1024 (a lane's next window words)
   GridCtl* ctl;
   MetricSlot* mslot;            // [G]
   uint32_t* ae;                 // [B] agent cell | elapsed << 16
   uint64_t* slots;              // [2 step parities][2 round parities][G] tagged granules
-  unsigned long long* dbg;      // GP_STAMPS builds: [G][32][32] step stamps, then [G][8] launch stamps
+  unsigned long long* dbg;      // GP_STAMPS builds: [G][64][16] step stamps, then [G][8] launch stamps
 };
 
 struct WgArgs {  // one launch: K steps, caller-owned action [K][B] and output [K][B] buffers
@@ -69,12 +73,13 @@ struct WgArgs {  // one launch: K steps, caller-owned action [K][B] and output [
   uint8_t* trunc;
 };
 
-// Dynamic LDS bytes of a launch (tables + coarse states + staging + near lists).
-__host__ __device__ constexpr int wg_dyn_bytes(int tables, int E) {
+// Dynamic LDS bytes of a launch (tables + two windows of high halves + coarse states + staging + the env waves'
+// near lists, 8 env waves).
+__host__ __device__ constexpr int wg_dyn_bytes(int tables, int E, int H) {
 #ifndef WG_NSTG
 #define WG_NSTG 3
 #endif
-  return tables + 2 * 512 * 16 + WG_NSTG * E * 4 + 2 * WG_NCAP * 4;
+  return tables + 2 * (E + 2 * H) * 4 + 2 * 512 * 16 + WG_NSTG * E * 4 + 2 * 8 * WG_NLW * 4;
 }
 // Launch on `s` (host; csrc/wgrid.hip). Returns hipError_t as int.
 int wgrid_launch(const WgArgs& a, int NS, int NA, int G, size_t dyn_lds, hipStream_t s);

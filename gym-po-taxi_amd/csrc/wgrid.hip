@@ -8,20 +8,24 @@
 //
 // Design (one workgroup of 11 waves per CU, block beta owns the E = 512 * NS consecutive envs [E beta, E beta + E);
 // env slot i = k * 512 + 64 w + l of env wave w, lane l, slot k):
+//  * WINDOWS. The random(B) words a block needs at step t+1 depend on the stream only through the position
+//    x_{t+1} = y_t + used_t (y_t = x_t + B). The env waves fill a window of E + 2H consecutive draws (their high 32
+//    bits) around the predicted position (used predicted from the previous step's b) while step t runs; env i then
+//    reads window word i + rw_off. Two windows (by step parity). A prediction more than H off regenerates the window
+//    exactly; a word whose high half equals a threshold's high half (p ~ 2^-32 per compare) is re-derived exactly.
 //  * EARLY COUNT. Only two things end an episode at step t (msrooms.py:405-412): truncation, elapsed + 1 >
-//    time_limit, known from the state alone, and reaching the goal, which needs the env's random word, its action
-//    and its cell. An env can reach the goal only from a cell where some effective action lands on the goal (the
-//    goal-action mask gm[cell], a per-cell table built from the move table); on FR_MAP that is ~3% of the envs.
-//    So when step t-1's transitions are done, the env waves list step t's truncations (a count) and its
-//    goal-adjacent envs (slot, next action, gm); after the exchange the control wave adds the block's resetters
-//    whose new cell is goal-adjacent, draws only the listed envs' words (a jump from the block's first word) and
-//    publishes b_t's block part. The full transitions of the 4096 envs run after that publish, while the granules
-//    travel. A list longer than WG_NCAP falls back to counting the step's masks; every step checks the early count
-//    against the masks (GP_DERR_LOGIC).
-//  * ENV STATES. Env e's random(B) word at step t is the output of S(x_t + 1 + e); x_{t+1} = x_t + B + used_t,
-//    so every env's state advances by the SAME jump J_t = jump(B + used_t) per step. Each env lane keeps its
-//    slots' 128-bit states in registers and applies J_t (published by the control wave with the step's cells):
-//    one affine 128-bit map per env-step, eight independent chains per lane, exact 64-bit words.
+//    time_limit, known from the state alone, and reaching the goal, which needs the env's word, action and cell.
+//    An env can reach the goal only from a cell where some effective action lands on it (the goal-action mask
+//    gm[cell], from the move table; ~3% of the envs on FR_MAP). Each env wave lists its goal-adjacent envs for the
+//    next step during its transitions (and its resetters that land next to the goal when it takes their cells), so
+//    at a step's start it resolves only those (one compacted pass: window word, thresholds, gm) and adds its done
+//    count; the control wave publishes the block's count as soon as the 8 waves have, and the full transitions and
+//    the next window's fill run while the granules travel. A wave whose list overflows counts from its full
+//    transitions instead; every step checks each wave's done ballots against the step's done bitmap
+//    (GP_DERR_LOGIC).
+//  * RANKS. The step's done bitmap (truncations written by the env waves a step ahead, goal hits OR-ed in by the
+//    early count) gives every resetter its rank in the block before the exchange ends; the control wave places the
+//    cells by rank (rank q takes choice() half-word R + q) and each env wave takes its resetters' cells by rank.
 //  * choice() words: 512 COARSE STATES S(y + 1 + 32 j) (one per env lane, a per-lane constant jump) cover the
 //    first 16384 draws after random(B); a resetter's word is one jump (<= 31 steps, LDS table) from a coarse state.
 //    During the exchange the control wave draws the cells of the 512 half-words around the predicted block prefix.
@@ -74,16 +78,18 @@ namespace {
 
 // Timing-study and test variants (WgParams::tmode, gp_debug_set "wg_tmode"; 0 in production). TM_NOSTORE and
 // TM_NOFILL drop work (results invalid: measurement only); the others give exact results.
-constexpr int TM_NOSTORE = 1;     // store waves skip the output copy (results invalid: measurement only)
-constexpr int TM_LATE = 4;        // publish the count from the step's masks after the full transitions (round-4 order)
+constexpr int TM_NOSTORE = 1;     // store waves skip the output copy
+constexpr int TM_NOFILL = 2;      // env waves skip the window fill (stale words)
+constexpr int TM_LATE = 4;        // every env wave counts from its full transitions (no early count)
 constexpr int TM_THROTTLE = 8;    // store waves drain their stores after every 16-env chunk (vmcnt(0))
 constexpr int TM_BUSYPOLL = 16;   // the all-gather polls without s_sleep
 constexpr int TM_NOPRIO = 32;     // env waves keep priority 0 (default: 2, above the store waves)
 constexpr int TM_EAGERSTORE = 64; // store waves copy a step as soon as it is final (default: after the next transitions)
 constexpr int TM_NOCAND = 128;    // no candidate cells during the all-gather (every resetter's cell drawn after it)
 constexpr int TM_STORELOW = 256;  // store waves at priority 0 (default 1)
+constexpr int TM_EXACTW = 512;    // every window word re-derived from the base state (the tie path, for parity tests)
 constexpr int TM_ENVPLACE = 1024; // the env waves place every step's resetters (the slow-path placement, for tests)
-constexpr int TM_ENVDROP = 2048;  // env waves drop to priority 0 after their transitions (default: 2 throughout)
+constexpr int TM_TRANSFIRST = 2048; // env waves run the transitions before the next window's fill (default: after)
 constexpr int TM_CTRLHIGH = 4096; // the control wave stays at priority 3 while it draws candidates (default: 1)
 
 constexpr int EW = 8;                 // env waves
@@ -96,27 +102,34 @@ constexpr int MAXRP = 512;            // rejected half-word positions the slow p
 constexpr int NCAND = 512;            // candidate resetter cells drawn during the all-gather (256 u64 draws)
 constexpr uint32_t CAND_W = 192;      // half-words of them before the predicted block prefix
 constexpr uint32_t CB_CTRL = 256;     // resetters per block the control wave places itself (more: the env waves)
-constexpr int NCAP = WG_NCAP;
+constexpr int NLW = WG_NLW;           // goal-adjacent envs per env wave and step the early count lists
 
 struct WgShared {
-  uint64_t mask[8][EW];      // this step's resetter ballots by (slot k, env wave w)
+  // Per step parity, one 64-bit word per (env slot k, env wave w) = 64 env slots: dmask = the step's done envs
+  // (truncations written a step ahead, goal hits OR-ed in by the early count), pre = the block's resetters before
+  // each word (the ranks).
+  uint64_t dmask[2][64];
+  uint32_t pre[2][64];
   // monotone LDS counters: the waves never meet at a workgroup barrier inside the step loop
-  uint32_t trans_done;       // env waves done with step 0's lists (prologue), then with each step's transitions
+  uint32_t trans_done;       // env waves done with a step's full transitions
+  uint32_t cnt_done;         // env waves done adding a step's done count (EW per step)
   uint32_t cs_done;          // env waves done with a step's coarse states
-  uint32_t r2s_done;         // env waves done listing a step's resetters in r2s
+  uint32_t fill_done;        // env-wave window fills (and exact regenerations) completed
   uint32_t res_done;         // env waves done taking (or placing) the previous step's resetter cells
   uint32_t st_done;          // store-wave step copies completed (SW per step)
-  uint32_t cells_done;       // control wave: step k's exchange done, cells placed, S(x_{k+1}), J_k, fix (k + 1)
-  uint32_t pro;              // prologue: S(x_0) published
-  uint32_t nlc[2];           // by step parity: listed goal-adjacent envs (low 16) | truncations (high 16)
+  uint32_t sy_ready;         // control wave: step k's S(y) and step k+1's window base published (k + 1)
+  uint32_t cells_done;       // control wave: step k's exchange done, cells placed, S(x_{k+1}), rw_off, fix (k + 1)
+  uint32_t pro;              // prologue: the first window's base and S(x_0) are published
+  uint32_t cnt[2];           // by step parity: the block's done count (the env waves' adds)
   uint64_t sx[2][2];         // by step parity: S(x_t) (hi, lo), the state at the step's start
   uint64_t sy[2][2];         // by step parity: S(y_t) (hi, lo), the state after the step's random(B)
-  uint64_t jst[2][4];        // by parity of step t: J_t = jump by B + used_t (A hi, A lo, C hi, C lo)
+  uint64_t rw[2][2];         // by parity of the step a window serves: its base state (hi, lo)
+  int32_t rw_off[2];         // by step parity: env i of that step reads window word i + rw_off
   uint32_t fix[2];           // by step parity, acted on at the step's start: bit 0 the env waves place the previous
-                             // step's resetters (slow path / many resetters)
+                             // step's resetters (slow path / many resetters), bit 1 regenerate the step's window
   uint32_t R, h, u, nrp;     // env placement: block prefix, has_uint32 / uinteger at the step start, # positions
   uint32_t rp[MAXRP];        // slow path: rejected half-word positions, ascending
-  uint16_t r2s[4096];        // resetter rank in the block -> env slot | next step's action index << 12
+  uint32_t rc[CB_CTRL];      // the control wave's placement: cell of resetter rank q | its goal-action mask << 16
   uint32_t cand[NCAND];      // half-words cbase .. cbase + NCAND - 1: candidate cell | its goal-action mask << 16
 #ifdef GP_STAMPS
   unsigned long long stp[32][32];  // step stamps of the first 32 steps (GP_STAMPS builds)
@@ -208,6 +221,7 @@ struct Tabs {  // the LDS copy of the tables (pointers resolved once per role)
   const PcgJump* jt8p;   // [2][256] jump by d, by 256 d
   const uint32_t* mvp;   // [ncells][NA] new cell | blocked << 15 | goal-action mask of the new cell << 16
   const uint64_t* thp;   // [NA][NA] thresholds on the full draw
+  const uint32_t* thhp;  // [NA][NA] their high halves
   const int32_t* ocp;    // [ncells] obs of the agent cell (fixed goal)
   const uint32_t* avp;   // [n_agent] valid agent cell | goal-action mask << 16
   const uint8_t* gmp;    // [ncells] goal-action masks
@@ -215,18 +229,38 @@ struct Tabs {  // the LDS copy of the tables (pointers resolved once per role)
   __device__ __forceinline__ Tabs(const char* d, const WgParams& P)
       : j32p(reinterpret_cast<const PcgJump*>(d + P.lds.j32)), jt8p(reinterpret_cast<const PcgJump*>(d + P.lds.jt8)),
         mvp(reinterpret_cast<const uint32_t*>(d + P.lds.move)), thp(reinterpret_cast<const uint64_t*>(d + P.lds.thr)),
-        ocp(reinterpret_cast<const int32_t*>(d + P.lds.ocell)), avp(reinterpret_cast<const uint32_t*>(d + P.lds.avalid)),
-        gmp(reinterpret_cast<const uint8_t*>(d + P.lds.gmc)), jt64(P.jt64) {}
+        thhp(reinterpret_cast<const uint32_t*>(d + P.lds.thh)), ocp(reinterpret_cast<const int32_t*>(d + P.lds.ocell)),
+        avp(reinterpret_cast<const uint32_t*>(d + P.lds.avalid)), gmp(reinterpret_cast<const uint8_t*>(d + P.lds.gmc)),
+        jt64(P.jt64) {}
   __device__ __forceinline__ const PcgJump& j32(uint32_t i) const { return j32p[i]; }
   __device__ __forceinline__ const PcgJump& jt8(uint32_t i) const { return jt8p[i]; }
   __device__ __forceinline__ int32_t ocell(uint32_t c) const { return ocp[c]; }
   __device__ __forceinline__ uint32_t avalid(uint32_t v) const { return avp[v]; }
 };
 
-// Effective action (action_utils.py:84-90 in integer form: #{j : x > thr[a][j]}, thresholds pre-shifted to the
-// full 64-bit draw).
+// Effective action (action_utils.py:84-90 in integer form: #{j : x > thr[a][j]}) from the high half of the draw;
+// `tie` when the high half equals a threshold's (then only the full draw decides).
 template <int NA>
-__device__ __forceinline__ uint32_t eff_action(const Tabs& tb, uint64_t x, uint32_t a) {
+__device__ __forceinline__ uint32_t eff_hi(const Tabs& tb, uint32_t xh, uint32_t a, bool& tie) {
+  const uint4* r = reinterpret_cast<const uint4*>(tb.thhp + a * NA);
+  uint32_t t[NA];
+#pragma unroll
+  for (int q = 0; q < NA / 4; ++q) {
+    const uint4 v = r[q];
+    t[4 * q] = v.x; t[4 * q + 1] = v.y; t[4 * q + 2] = v.z; t[4 * q + 3] = v.w;
+  }
+  uint32_t c = 0;
+  bool eq = false;
+#pragma unroll
+  for (int j = 0; j + 1 < NA; ++j) {
+    c += xh > t[j] ? 1u : 0u;
+    eq |= xh == t[j];
+  }
+  tie = eq;
+  return c;
+}
+template <int NA>
+__device__ __forceinline__ uint32_t eff_full(const Tabs& tb, uint64_t x, uint32_t a) {
   const uint64_t* r = tb.thp + a * NA;
   uint32_t c = 0;
 #pragma unroll
@@ -254,27 +288,22 @@ __device__ __forceinline__ u128 jump_any(const Tabs& tb, u128 s, uint32_t n) {
   return pcg_jump(tb.jt64, s, n);
 }
 
-// Affine jumps compose: (j2 o j1)(s) = A2 (A1 s + C1) + C2.
-__device__ __forceinline__ PcgJump compose(const PcgJump& j2, const PcgJump& j1) {
-  const u128 a2 = mk128(j2.a_hi, j2.a_lo);
-  const u128 a = a2 * mk128(j1.a_hi, j1.a_lo);
-  const u128 c = a2 * mk128(j1.c_hi, j1.c_lo) + mk128(j2.c_hi, j2.c_lo);
-  return PcgJump{hi64(a), lo64(a), hi64(c), lo64(c)};
+// The full draw of window word j of a window with base state rw (word j = output of the base advanced by j).
+__device__ __forceinline__ uint64_t window_word(const Tabs& tb, const uint64_t (&rw)[2], uint32_t j) {
+  return pcg_output(jump_any(tb, mk128(rw[0], rw[1]), j));
 }
-// The jump by n draws as an affine map (the same tables as jump_any).
-__device__ __forceinline__ PcgJump jump_params(const Tabs& tb, uint32_t n) {
-  PcgJump j{0, 1, 0, 0};
-  if (n < 65536u) {
-    if (n & 255u) j = tb.jt8(n & 255u);
-    if (n >> 8) j = compose(tb.jt8(256u + (n >> 8)), j);
-    return j;
+
+// The base of the next step's window for block beta when the current step's choice() call uses `used` u64 draws:
+// the state whose next output is window word 0, from S(x_t) (jb = jblk[beta][0] folds in random(B) and E beta - H),
+// and heff = how many window words precede the block's first env word.
+__device__ __forceinline__ u128 rw_base(const Tabs& tb, const PcgJump& jb, u128 Sx, uint32_t used, int beta, int32_t H,
+                                        int32_t& heff) {
+  if (beta == 0) {
+    heff = min(H, (int32_t)used + 1);
+    return apply_jump(jb, jump_any(tb, Sx, used + 1u - (uint32_t)heff));
   }
-#pragma unroll
-  for (int L = 0; L < JT_LEVELS; ++L) {
-    const uint32_t d = (n >> (JT_RADIX_BITS * L)) & (JT_RADIX - 1);
-    if (d) j = compose(tb.jt64[L * JT_RADIX + d], j);
-  }
-  return j;
+  heff = H;
+  return apply_jump(jb, jump_any(tb, Sx, used + 1u));
 }
 
 __device__ __forceinline__ bool spin_give_up(const WgParams& P, uint32_t& spins) {
@@ -345,22 +374,23 @@ __device__ __forceinline__ uint32_t grej(uint64_t g) { return (uint32_t)(g >> 24
 #endif
 constexpr int NSTG = WG_NSTG;  // staging buffers: the store waves may trail the env waves by up to NSTG - 1 steps
 struct Lds {
+  uint32_t* W0;   // [2 step parities][E + 2H] window words (high halves)
   uint64_t* CS0;  // [2 step parities][512][2] coarse states (lo, hi)
   char* stg0;     // [NSTG][E] staged u32 per env: cell | term << 16 | trunc << 17 | wall bump << 18
-  uint32_t* NL0;  // [2 step parities][NCAP] goal-adjacent envs: slot | action index << 12 | goal-action mask << 16
+  uint32_t* NL0;  // [2 step parities][EW][NLW] goal-adjacent envs: slot | action index << 12 | goal-action mask << 16
+  int wlen;
   __device__ __forceinline__ Lds(char* dyn, const WgParams& P, int E)
-      : CS0(reinterpret_cast<uint64_t*>(dyn + P.lds.total)),
-        stg0(dyn + P.lds.total + 2 * 512 * 16),
-        NL0(reinterpret_cast<uint32_t*>(dyn + P.lds.total + 2 * 512 * 16 + (size_t)NSTG * E * 4)) {}
+      : W0(reinterpret_cast<uint32_t*>(dyn + P.lds.total)),
+        CS0(reinterpret_cast<uint64_t*>(dyn + P.lds.total + (size_t)2 * (E + 2 * P.halo) * 4)),
+        stg0(dyn + P.lds.total + (size_t)2 * (E + 2 * P.halo) * 4 + 2 * 512 * 16),
+        NL0(reinterpret_cast<uint32_t*>(dyn + P.lds.total + (size_t)2 * (E + 2 * P.halo) * 4 + 2 * 512 * 16 +
+                                        (size_t)NSTG * E * 4)),
+        wlen(E + 2 * P.halo) {}
+  __device__ __forceinline__ uint32_t* W(int k) const { return W0 + (size_t)(k & 1) * wlen; }
   __device__ __forceinline__ char* stg(int k, int E) const { return stg0 + (size_t)(k % NSTG) * E * 4; }
   __device__ __forceinline__ uint64_t* CS(int k) const { return CS0 + (size_t)(k & 1) * 1024; }
-  __device__ __forceinline__ uint32_t* NL(int k) const { return NL0 + (size_t)(k & 1) * NCAP; }
+  __device__ __forceinline__ uint32_t* NL(int k, int w) const { return NL0 + ((size_t)(k & 1) * EW + w) * NLW; }
 };
-
-__device__ __forceinline__ uint32_t mask_count(const WgShared& sh, int NS) {
-  const int lane = threadIdx.x & 63;
-  return wave_sum(lane < NS * EW ? popc(sh.mask[lane >> 3][lane & 7]) : 0u);
-}
 
 // Slow path, control wave: append the rejected half-word positions of choice-stream slice sigma (u64 draws
 // 62 sigma + 1 .. 62 sigma + 62 after random(B), both halves; with a buffered half (h) slice 0 also owns hw 0).
@@ -449,75 +479,55 @@ __device__ __forceinline__ uint32_t ctrl_slow(const WgParams& P, WgShared& sh, c
   return wtot;
 }
 
-// ------------------------------------------------------------------ the control wave ----
-// The early count of step k: the listed goal-adjacent envs' words (env slot i's word is the output of the block's
-// first-word state `base` advanced by i), counting those that reach the goal; truncated envs were never listed.
-template <int NA>
-__device__ __forceinline__ uint32_t ctrl_resolve(const Tabs& tb, const uint32_t* NLk, uint32_t nl, u128 base) {
-  const int lane = threadIdx.x & 63;
-  uint32_t goals = 0;
-  for (uint32_t i0 = 0; i0 < nl; i0 += 128) {  // two entries per lane and round, their jump chains interleaved
-    const uint32_t i1 = i0 + (uint32_t)lane, i2 = i1 + 64u;
-    const bool v1 = i1 < nl, v2 = i2 < nl;
-    const uint32_t e1 = v1 ? NLk[i1] : 0u, e2 = v2 ? NLk[i2] : 0u;
-    const uint64_t x1 = pcg_output(jump_any(tb, base, e1 & 0xFFFu));
-    const uint64_t x2 = pcg_output(jump_any(tb, base, e2 & 0xFFFu));
-    const uint32_t f1 = eff_action<NA>(tb, x1, (e1 >> 12) & 7u), f2 = eff_action<NA>(tb, x2, (e2 >> 12) & 7u);
-    goals += (v1 && ((e1 >> (16 + f1)) & 1u)) ? 1u : 0u;
-    goals += (v2 && ((e2 >> (16 + f2)) & 1u)) ? 1u : 0u;
+// Fill a window (high halves): word j = m * 512 + lg is the base state advanced by j (this lane: jump by lg, then
+// two interleaved chains of 1024-draw jumps).
+__device__ __forceinline__ void fill_window(uint32_t* RW, const PcgJump& jl, const PcgJump& j512, const PcgJump& j1024,
+                                            int nw, u128 base, int lg) {
+  u128 a = apply_jump(jl, base);
+  u128 c = apply_jump(j512, a);
+  int m = 0;
+  for (; m + 1 < nw; m += 2) {
+    RW[m * 512 + lg] = hi32(pcg_output(a));
+    RW[(m + 1) * 512 + lg] = hi32(pcg_output(c));
+    if (m + 2 < nw) {
+      a = apply_jump(j1024, a);
+      c = apply_jump(j1024, c);
+    }
   }
-  return wave_sum(goals);
+  if (m < nw) RW[m * 512 + lg] = hi32(pcg_output(a));
 }
 
-// Step k's resetters (cb <= CB_CTRL, no rejection): rank q takes half-word R + q; its cell goes to the staging
-// slot, and a resetter on a goal-adjacent cell is listed for step k + 1 (with its next action from r2s).
-template <int NS>
-__device__ __forceinline__ void ctrl_place(const WgParams& P, WgShared& sh, const Tabs& tb, const Lds& L, int k,
-                                           bool list_next, uint32_t cb, uint32_t R, uint32_t cbase, uint32_t h,
-                                           uint32_t u) {
-  constexpr int E = NS * 512;
+// ------------------------------------------------------------------ the control wave ----
+// Step k's resetters (cb <= CB_CTRL, no rejection): rank q takes half-word R + q; its cell (| goal-action mask)
+// goes to rc[q], where the env waves take it by rank.
+__device__ __forceinline__ void ctrl_place(const WgParams& P, WgShared& sh, const Tabs& tb, const uint64_t* CS,
+                                           uint32_t cb, uint32_t R, uint32_t cbase, uint32_t h, uint32_t u) {
   const int lane = threadIdx.x & 63;
   const uint32_t nag = (uint32_t)P.n_agent;
   const bool nocand = P.tmode & TM_NOCAND;
-  const uint64_t* CS = L.CS(k);
-  uint16_t* st = reinterpret_cast<uint16_t*>(L.stg(k, E));
-  uint32_t* NLn = L.NL(k + 1);
-  const uint32_t nlv = lds_load(&sh.nlc[(k + 1) & 1]);  // the env waves' entries of step k + 1 are all in
-  uint32_t nb = nlv & 0xFFFFu;
-  const uint32_t nb0 = nb;
-  for (uint32_t q0 = 0; q0 < cb; q0 += 64u) {
-    const uint32_t q = q0 + (uint32_t)lane;
-    uint32_t v = 0, ent = 0;
-    if (q < cb) {
-      ent = sh.r2s[q];
-      const uint32_t hw = R + q;
-      if (hw - cbase < (uint32_t)NCAND && !nocand) {  // (hw >= cbase >= h: never the buffered half)
-        v = sh.cand[hw - cbase];
+  for (uint32_t q = (uint32_t)lane; q < cb; q += 64u) {
+    const uint32_t hw = R + q;
+    uint32_t v;
+    if (hw - cbase < (uint32_t)NCAND && !nocand) {  // (hw >= cbase >= h: never the buffered half)
+      v = sh.cand[hw - cbase];
+    } else {
+      uint32_t word;
+      if (h && hw == 0) {
+        word = u;
       } else {
-        uint32_t word;
-        if (h && hw == 0) {
-          word = u;
-        } else {
-          const uint32_t hh = hw - h;
-          const uint64_t x = pcg_output(draw_state(tb, CS, hh >> 1));
-          word = (hh & 1u) ? (uint32_t)(x >> 32) : (uint32_t)x;
-        }
-        v = tb.avalid(lemire_value(word, nag));
+        const uint32_t hh = hw - h;
+        const uint64_t x = pcg_output(draw_state(tb, CS, hh >> 1));
+        word = (hh & 1u) ? (uint32_t)(x >> 32) : (uint32_t)x;
       }
-      st[2 * (ent & 0xFFFu)] = (uint16_t)v;  // the low half of the staged word: the new cell
+      v = tb.avalid(lemire_value(word, nag));
     }
-    const bool nr = list_next && (v >> 16) != 0u;
-    const uint64_t m = ballot(nr);
-    const uint32_t idx = nb + mbcnt(m);
-    if (nr && idx < (uint32_t)NCAP) NLn[idx] = ent | ((v >> 16) << 16);
-    nb += popc(m);
+    sh.rc[q] = v;
   }
-  if (lane == 0 && nb != nb0) lds_set(&sh.nlc[(k + 1) & 1], (nlv & 0xFFFF0000u) | nb);
 }
 
-// Per step: the early count (listed envs' words), granule published; while the granules travel S(y) and the
-// candidate cells; the all-gather; the resetters' cells, J_t = jump(B + used_t), S(x_{t+1}) (cells_done); the next
-// step's rejection-check slice and block base.
+// Per step: S(y) and the next window's base around the predicted used (sy_ready); the block's done count from the
+// env waves, granule published; the ranks; the candidate cells while the granules travel; the all-gather; the
+// resetters' cells, the next window's offset, S(x_{t+1}) (cells_done); the next step's rejection-check slice.
 template <int NS, int NA>
 __device__ __forceinline__ void wg_ctrl(const WgParams& P, WgShared& sh, const Tabs& tb, const Lds& L, int K) {
   const int lane = threadIdx.x & 63, beta = (int)blockIdx.x, G = (int)gridDim.x;
@@ -528,9 +538,11 @@ __device__ __forceinline__ void wg_ctrl(const WgParams& P, WgShared& sh, const T
   uint32_t Rprev = (uint32_t)(((uint64_t)bprev * (uint64_t)blockIdx.x) / (uint64_t)gridDim.x);  // a first guess
   const uint32_t ts0 = C->wstep + 1u;  // tag step of k = 0 (tags are never 0: the slots start zeroed)
   const PcgJump jr = P.jrej[(size_t)beta * 64 + lane];
-  const PcgJump jb = P.jblk[beta];
+  const PcgJump jb = P.jblk[2 * beta], jpro = P.jblk[2 * beta + 1];
   const PcgJump jB = P.jB;
-  const uint32_t nag = (uint32_t)P.n_agent, thra = P.thr_agent, tlim = (uint32_t)P.time_limit;
+  const uint32_t nag = (uint32_t)P.n_agent, thra = P.thr_agent;
+  const int32_t H = P.halo;
+  const uint32_t bias = (uint32_t)P.wg_bias;
   const int tmode = P.tmode;
   uint32_t* derr = &C->err;
   // Lemire check of a block's slice of the choice() stream (u64 draws 62 beta + 1 .. + 62 after random(B))
@@ -545,45 +557,61 @@ __device__ __forceinline__ void wg_ctrl(const WgParams& P, WgShared& sh, const T
     return wave_sum(rj);
   };
   uint32_t rejc = rej_check(Sx, h, u);
-  u128 base = apply_jump(jb, Sx);  // the state whose output is this block's first env word of the step
   lds_barrier();  // P1: tables staged, counters zeroed
-  if (lane == 0) {
+  if (lane == 0) {  // the first window: step 0's own random(B) words, exact: word 0 is S(x_0 + 1 + E beta - heff)
+    const u128 s = apply_jump(jpro, Sx);
+    sh.rw[0][0] = hi64(s);
+    sh.rw[0][1] = lo64(s);
+    sh.rw_off[0] = beta == 0 ? 1 : H;
     sh.sx[0][0] = hi64(Sx);
     sh.sx[0][1] = lo64(Sx);
     lds_release();
     lds_set(&sh.pro, 1u);
   }
   LSTAMP(P, 1);
-  uint32_t cbprev = 0;       // the previous step's resetters of this block (all truncate at the next step if tlim 0)
-  bool eplace_prev = false;  // the env waves placed the previous step's resetters
   for (int k = 0; k < K; ++k) {
     const uint32_t ts = ts0 + (uint32_t)k;
-    // ---- the step's reset count, early ----
-    lds_wait(&sh.trans_done, (uint32_t)EW * (uint32_t)(k + 1), derr);  // the env waves' lists of this step
-    if (eplace_prev) lds_wait(&sh.res_done, (uint32_t)EW * (uint32_t)k, derr);
-    WSTAMP(P, k, 5);
-    const uint32_t nlv = lds_load(&sh.nlc[k & 1]);
-    const uint32_t nl = nlv & 0xFFFFu;
-    uint32_t cnt;
-    if (nl <= (uint32_t)NCAP && !(tmode & TM_LATE)) {
-      cnt = (nlv >> 16) + (tlim == 0 ? cbprev : 0u) + ctrl_resolve<NA>(tb, L.NL(k), nl, base);
-    } else {  // too many listed envs: count the step's masks after the full transitions
-      lds_wait(&sh.trans_done, (uint32_t)EW * (uint32_t)(k + 2), derr);
-      cnt = mask_count(sh, NS);
-    }
-    uint64_t* slots = P.slots + (size_t)(ts & 1u) * 2 * G;
-    publish(P, slots, ts << 6, rejc, cnt);
-    WSTAMP(P, k, 6);
-    // ---- while the granules travel: S(y) and the cells of the choice() half-words around the block prefix
-    // predicted by the last step's (at a priority below the env waves': not urgent), so that the resetters' cells
-    // after the exchange are one LDS read each. Candidate i is half-word cbase + i; cbase = 2 d0 + h.
-    if (!(tmode & TM_CTRLHIGH)) __builtin_amdgcn_s_setprio(1);
+    // ---- S(y) and the next step's window base around the used predicted from the last b (the window's buffer and
+    // base slot are free once every env wave's transitions of step k - 1 are done) ----
+    lds_wait(&sh.trans_done, (uint32_t)EW * (uint32_t)k, derr);
     const u128 Sy = apply_jump(jB, Sx);
+    uint32_t used_p, hp;
+    words_to_draws(bprev + bias, h, used_p, hp);
+    int32_t heff_p;
+    const u128 Srw = rw_base(tb, jb, Sx, used_p, beta, H, heff_p);
     if (lane == 0) {
       sh.sy[k & 1][0] = hi64(Sy);
       sh.sy[k & 1][1] = lo64(Sy);
-      lds_set(&sh.nlc[k & 1], 0u);  // consumed (this parity's next entries come with step k + 1)
+      if (k + 1 < K) {
+        sh.rw[(k + 1) & 1][0] = hi64(Srw);
+        sh.rw[(k + 1) & 1][1] = lo64(Srw);
+      }
+      lds_release();
+      lds_set(&sh.sy_ready, (uint32_t)k + 1u);
     }
+    WSTAMP(P, k, 7);
+    // ---- the block's done count (early) ----
+    lds_wait(&sh.cnt_done, (uint32_t)EW * (uint32_t)(k + 1), derr);
+    WSTAMP(P, k, 5);
+    const uint32_t cnt = lds_load(&sh.cnt[k & 1]);
+    uint64_t* slots = P.slots + (size_t)(ts & 1u) * 2 * G;
+    publish(P, slots, ts << 6, rejc, cnt);
+    WSTAMP(P, k, 6);
+    // ---- while the granules travel: the ranks (resetters before each 64-env word of the done bitmap) ----
+    {
+      const uint64_t wd = lane < NS * EW ? sh.dmask[k & 1][lane] : 0ull;
+      const uint32_t c = popc(wd);
+      const uint32_t incl = wave_incl_scan(c);
+      if (lane < NS * EW) sh.pre[k & 1][lane] = incl - c;
+      if (lane == 0) {
+        lds_set(&sh.cnt[k & 1], 0u);  // (this parity's next adds come with step k + 2)
+        if (__builtin_amdgcn_readlane((int)incl, 63) != (int)cnt) atomicOr(derr, GP_DERR_LOGIC);
+      }
+    }
+    // the cells of the choice() half-words around the block prefix predicted by the last step's (at a priority below
+    // the env waves': not urgent), so that the resetters' cells after the exchange are one LDS read each. Candidate i
+    // is half-word cbase + i; cbase = 2 d0 + h.
+    if (!(tmode & TM_CTRLHIGH)) __builtin_amdgcn_s_setprio(1);
     const uint64_t* CS = L.CS(k);
     lds_wait(&sh.cs_done, (uint32_t)EW * (uint32_t)(k + 1), derr);
     const uint32_t d0 = min(Rprev > CAND_W + h ? (Rprev - CAND_W - h) >> 1 : 0u, 16384u - NCAND / 2);  // CS reach
@@ -618,17 +646,12 @@ __device__ __forceinline__ void wg_ctrl(const WgParams& P, WgShared& sh, const T
     const bool slow = rtot != 0 || b > 124u * (uint32_t)G;
     // ---- the step's resetters ----
     uint32_t used, h2;
-    if (!slow) words_to_draws(b, h, used, h2);
-    // J_t = jump by B + used_t (every env state's step) and S(x_{t+1}) = J_t(S(x_t)): the env waves' next words
-    PcgJump Jt = slow ? PcgJump{0, 1, 0, 0} : compose(jump_params(tb, used), jB);
-    lds_wait(&sh.r2s_done, (uint32_t)EW * (uint32_t)(k + 1), derr);  // every wave's masks and resetter listing
-    if (mask_count(sh, NS) != cnt && lane == 0) atomicOr(derr, GP_DERR_LOGIC);
-    if (slow) {
+    if (!slow) {
+      words_to_draws(b, h, used, h2);
+    } else {
       const uint32_t wtot = ctrl_slow(P, sh, tb, CS, Sy, h, u, b, ts, g);
       words_to_draws(wtot, h, used, h2);
-      Jt = compose(jump_params(tb, used), jB);
     }
-    const u128 Sxn = apply_jump(Jt, Sx);
     const bool eplace = slow || cnt > CB_CTRL || (tmode & TM_ENVPLACE);
     if (eplace) {
       if (lane == 0) {
@@ -638,16 +661,27 @@ __device__ __forceinline__ void wg_ctrl(const WgParams& P, WgShared& sh, const T
         if (!slow) sh.nrp = 0;
       }
     } else if (cnt) {
-      ctrl_place<NS>(P, sh, tb, L, k, k + 1 < K && tlim >= 1u, cnt, R, cbase, h, u);
+      ctrl_place(P, sh, tb, CS, cnt, R, cbase, h, u);
     }
+    // the next step's window offset; a window more than H off is regenerated exactly by the env waves
+    int32_t off = heff_p + (int32_t)used - (int32_t)used_p;
+    uint32_t fix = eplace ? 1u : 0u;
+    if (k + 1 < K && (off < 0 || off > 2 * H)) {
+      int32_t heff;
+      const u128 s = rw_base(tb, jb, Sx, used, beta, H, heff);
+      off = heff;
+      fix |= 2u;
+      if (lane == 0) {
+        sh.rw[(k + 1) & 1][0] = hi64(s);
+        sh.rw[(k + 1) & 1][1] = lo64(s);
+      }
+    }
+    const u128 Sxn = jump_any(tb, Sy, used);  // S(x_{t+1}) = S(y_t + used)
     if (lane == 0) {
       sh.sx[(k + 1) & 1][0] = hi64(Sxn);
       sh.sx[(k + 1) & 1][1] = lo64(Sxn);
-      sh.jst[k & 1][0] = Jt.a_hi;
-      sh.jst[k & 1][1] = Jt.a_lo;
-      sh.jst[k & 1][2] = Jt.c_hi;
-      sh.jst[k & 1][3] = Jt.c_lo;
-      sh.fix[(k + 1) & 1] = eplace ? 1u : 0u;
+      sh.rw_off[(k + 1) & 1] = off;
+      sh.fix[(k + 1) & 1] = fix;
       lds_release();
       lds_set(&sh.cells_done, (uint32_t)k + 1u);
     }
@@ -657,12 +691,7 @@ __device__ __forceinline__ void wg_ctrl(const WgParams& P, WgShared& sh, const T
     h = h2;
     bprev = b;
     Rprev = R;
-    cbprev = cnt;
-    eplace_prev = eplace;
-    if (k + 1 < K) {
-      rejc = rej_check(Sx, h, u);
-      base = apply_jump(jb, Sx);
-    }
+    if (k + 1 < K) rejc = rej_check(Sx, h, u);
     WSTAMP(P, k, 11);
   }
   LSTAMP(P, 3);
@@ -682,46 +711,31 @@ struct Acc {
   uint32_t eps = 0, ngoal = 0, nwall = 0, lens = 0;
 };
 
-// List this wave's goal-adjacent envs (bit s of nrm: entry ent[s]) and its truncation count for a step: one LDS
-// atomic per wave reserves the entries' places.
+// Append this wave's goal-adjacent envs (bit s of nrm: entry ent[s]) to its list of a step at position n (uniform);
+// returns the new length (entries past NLW are counted, not written: the wave then counts from its masks).
 template <int NS>
-__device__ __forceinline__ void append_near(uint32_t* NLp, uint32_t* nlcp, uint32_t nrm, const uint32_t (&ent)[NS],
-                                            uint32_t ntr) {
-  const int lane = threadIdx.x & 63;
-  uint32_t tot = 0, pos[NS];
+__device__ __forceinline__ uint32_t append_near(uint32_t* NLw, uint32_t n, uint32_t nrm, const uint32_t (&ent)[NS]) {
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     const uint64_t m = ballot((nrm >> s) & 1u);
-    pos[s] = tot + mbcnt(m);
-    tot += popc(m);
+    const uint32_t i = n + mbcnt(m);
+    if (((nrm >> s) & 1u) && i < (uint32_t)NLW) NLw[i] = ent[s];
+    n += popc(m);
   }
-  const uint32_t add = tot | (ntr << 16);
-  if (add) {
-    uint32_t base = 0;
-    if (lane == 0) base = __hip_atomic_fetch_add(nlcp, add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    base = (uint32_t)__builtin_amdgcn_readlane((int)base, 0) & 0xFFFFu;
-#pragma unroll
-    for (int s = 0; s < NS; ++s)
-      if (((nrm >> s) & 1u) && base + pos[s] < (uint32_t)NCAP) NLp[base + pos[s]] = ent[s];
-  }
+  return n;
 }
 
-// The previous step's (kp's) resetters: their cells from the staging area (placed by the control wave), or placed
-// here exactly (ranks -> positions past the listed rejections -> words), listing the goal-adjacent ones for step
-// kp + 1 when `list_next` (ai: the actions of step kp + 1).
+// The previous step's (kp's) resetters, by their block rank (the control wave's ranks of step kp + the slot's rank in
+// its 64-env word): the cell the control wave placed, or one placed here exactly (rank -> position past the listed
+// rejections -> word); the goal-adjacent ones appended to this wave's list of step kp + 1 when `list_next` (ai: the
+// actions of step kp + 1). Returns the list's new length.
 template <int NS, int NA>
-__device__ __forceinline__ void env_take(const WgParams& P, WgShared& sh, const Tabs& tb, const Lds& L, int kp,
-                                         bool eplace, bool list_next, uint32_t dn, const uint32_t (&pre)[NS],
-                                         const uint64_t (&bm)[NS], const uint32_t (&ai)[NS], uint32_t (&ae)[NS]) {
+__device__ __forceinline__ uint32_t env_take(const WgParams& P, WgShared& sh, const Tabs& tb, const Lds& L, int kp,
+                                             bool eplace, bool list_next, uint32_t nl, uint32_t dn,
+                                             const uint64_t (&bm)[NS], const uint32_t (&ai)[NS], uint32_t (&ae)[NS]) {
   constexpr int E = NS * 512;
-  const int lg = threadIdx.x;
+  const int lg = threadIdx.x, w = lg >> 6;
   uint16_t* st = reinterpret_cast<uint16_t*>(L.stg(kp, E));
-  if (!eplace) {
-#pragma unroll
-    for (int s = 0; s < NS; ++s)
-      if ((dn >> s) & 1u) ae[s] = st[2 * (s * 512 + lg)];
-    return;
-  }
   const u128 Sy = mk128(sh.sy[kp & 1][0], sh.sy[kp & 1][1]);
   const uint64_t* CS = L.CS(kp);
   const uint32_t R = sh.R, h = sh.h, u = sh.u, n = sh.nrp;
@@ -730,24 +744,50 @@ __device__ __forceinline__ void env_take(const WgParams& P, WgShared& sh, const 
   for (int s = 0; s < NS; ++s) {
     ent[s] = 0;
     if (!((dn >> s) & 1u)) continue;
-    uint32_t p = R + pre[s] + mbcnt(bm[s]);
-    for (uint32_t q = 0; q < n; ++q) p += sh.rp[q] <= p ? 1u : 0u;
-    uint32_t word;
-    if (h && p == 0) {
-      word = u;
+    const uint32_t q = sh.pre[kp & 1][s * EW + w] + mbcnt(bm[s]);
+    uint32_t v;
+    if (!eplace) {
+      v = sh.rc[q];
     } else {
-      const uint32_t hh = p - h, d = hh >> 1;
-      const u128 s2 = d < 16384u ? draw_state(tb, CS, d) : pcg_jump(tb.jt64, Sy, d + 1u);
-      const uint64_t x = pcg_output(s2);
-      word = (hh & 1u) ? (uint32_t)(x >> 32) : (uint32_t)x;
+      uint32_t p = R + q;
+      for (uint32_t r = 0; r < n; ++r) p += sh.rp[r] <= p ? 1u : 0u;
+      uint32_t word;
+      if (h && p == 0) {
+        word = u;
+      } else {
+        const uint32_t hh = p - h, d = hh >> 1;
+        const u128 s2 = d < 16384u ? draw_state(tb, CS, d) : pcg_jump(tb.jt64, Sy, d + 1u);
+        const uint64_t x = pcg_output(s2);
+        word = (hh & 1u) ? (uint32_t)(x >> 32) : (uint32_t)x;
+      }
+      v = tb.avalid(lemire_value(word, (uint32_t)P.n_agent));
     }
-    const uint32_t v = tb.avalid(lemire_value(word, (uint32_t)P.n_agent));
     st[2 * (s * 512 + lg)] = (uint16_t)v;
     ae[s] = v & 0xFFFFu;
     nrm |= (list_next && (v >> 16) != 0u) ? (1u << s) : 0u;
     ent[s] = (uint32_t)(s * 512 + lg) | (ai[s] << 12) | ((v >> 16) << 16);
   }
-  if (list_next) append_near<NS>(L.NL(kp + 1), &sh.nlc[(kp + 1) & 1], nrm, ent, 0u);
+  return list_next ? append_near<NS>(L.NL(kp + 1, w), nl, nrm, ent) : nl;
+}
+
+// The early count of step k for this wave: its listed goal-adjacent envs' window words (one entry per lane), each
+// goal hit OR-ed into the step's done bitmap; returns the wave's done count (its 64-env words' popcounts).
+template <int NS, int NA>
+__device__ __forceinline__ uint32_t env_resolve(WgShared& sh, const Tabs& tb, const Lds& L, int k, uint32_t nl,
+                                                bool exactw) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint64_t* dm = sh.dmask[k & 1];
+  if (lane < (int)nl) {
+    const uint32_t e = L.NL(k, w)[lane];
+    const uint32_t slot = e & 0xFFFu, j = slot + (uint32_t)sh.rw_off[k & 1];
+    bool tie;
+    uint32_t f = eff_hi<NA>(tb, L.W(k)[j], (e >> 12) & 7u, tie);
+    if (tie || exactw) f = eff_full<NA>(tb, window_word(tb, sh.rw[k & 1], j), (e >> 12) & 7u);
+    if ((e >> (16 + f)) & 1u)
+      __hip_atomic_fetch_or(&dm[slot >> 6], 1ull << (slot & 63u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  wave_sync_lds();
+  return wave_sum(lane < NS ? popc(dm[lane * EW + w]) : 0u);
 }
 
 template <int NS, int NA>
@@ -763,24 +803,25 @@ __device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Ta
   const uint32_t goal = (uint32_t)P.goal, tlim = (uint32_t)P.time_limit;
   uint32_t* derr = &P.ctl->err;
   uint32_t* aeg = P.ae;
+  const int nw = P.rw_words;
   const int tmode = P.tmode;
-  // per-lane constant jump by B + 32 lg + 1 (coarse state lg)
-  const PcgJump jcs = P.jlane[2 * lg + 1];
+  const bool exactw = tmode & TM_EXACTW;
+  const PcgJump j512 = P.j512, j1024 = P.j1024;
+  // per-lane constant jumps: by lg (window fill) and by B + 32 lg + 1 (coarse state)
+  const PcgJump jrw = P.jlane[2 * lg], jcs = P.jlane[2 * lg + 1];
   uint32_t ae[NS], ai[NS], an[NS];  // env state; action index of this step, of the next step
   int32_t a2[NS];                   // raw actions two steps ahead (loads in flight)
-  u128 sr[NS];                      // slot s's PCG64 state: its output is the slot's word of the current step
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     ae[s] = aeg[e0 + (size_t)s * 512 + lg];
     a2[s] = act[e0 + (size_t)s * 512 + lg];
     an[s] = K > 1 ? (uint32_t)act[B + e0 + (size_t)s * 512 + lg] : 0u;
   }
-  {  // step 0's states: S(x_0 + 1 + E beta + s 512 + lg)
+  // the first window, exact (word 0 = S(x_0 + 1 + E beta - heff)), filled from global data while the other waves
+  // stage the tables
+  {
     const GridCtl* C = P.ctl;
-    sr[0] = apply_jump(P.jlane[2 * lg], apply_jump(P.jblk[beta], mk128(C->s_hi, C->s_lo)));
-    const PcgJump j512 = P.j512;
-#pragma unroll
-    for (int s = 1; s < NS; ++s) sr[s] = apply_jump(j512, sr[s - 1]);
+    fill_window(L.W(0), jrw, j512, j1024, nw, apply_jump(P.jblk[2 * beta + 1], mk128(C->s_hi, C->s_lo)), lg);
   }
   lds_barrier();  // P1
 #pragma unroll
@@ -789,8 +830,9 @@ __device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Ta
     an[s] = K > 1 ? action_index<NA>((int32_t)an[s], derr) : 0u;
     acc.lens += ae[s] >> 16;  // episode lengths: + elapsed at the start - elapsed at the end + steps
   }
-  {  // step 0's truncations and goal-adjacent envs
-    uint32_t nrm = 0, trm = 0, ent[NS], ntr = 0;
+  uint32_t nl;  // this wave's goal-adjacent envs listed for the current step
+  {  // step 0's truncations (into its done bitmap) and goal-adjacent envs
+    uint32_t nrm = 0, trm = 0, ent[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       const uint32_t c = ae[s] & 0xFFFFu, el = (ae[s] >> 16) + 1u;
@@ -801,27 +843,37 @@ __device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Ta
       ent[s] = (uint32_t)(s * 512 + lg) | (ai[s] << 12) | (gm << 16);
     }
 #pragma unroll
-    for (int s = 0; s < NS; ++s) ntr += popc(ballot((trm >> s) & 1u));
-    append_near<NS>(L.NL(0), &sh.nlc[0], nrm, ent, ntr);
+    for (int s = 0; s < NS; ++s) {
+      const uint64_t m = ballot((trm >> s) & 1u);
+      if (lane == 0) sh.dmask[0][s * EW + w] = m;
+    }
+    nl = append_near<NS>(L.NL(0, w), 0u, nrm, ent);
   }
   lds_release();
-  if (lane == 0) lds_add(&sh.trans_done, 1u);
-  lds_wait(&sh.pro, 1u, derr);  // S(x_0)
+  lds_wait(&sh.pro, 1u, derr);  // the first window's offset, S(x_0)
+  if (lane == 0) lds_add(&sh.fill_done, 1u);
+  uint32_t fill_target = EW;
   uint64_t bm[NS];
-  uint32_t pre[NS];
   uint32_t dn = 0;
   for (int k = 0; k < K; ++k) {
     char* stg = L.stg(k, E);
-    if (k > 0) {  // the previous step's exchange is done: its resetters' cells, J_{k-1}
+    if (k > 0) {  // the previous step's exchange is done: its resetters' cells, this step's window offset
       lds_wait(&sh.cells_done, (uint32_t)k, derr);
       if (w == 0) WSTAMP(P, k, 16);
       const uint32_t fix = sh.fix[k & 1];
-      const PcgJump J{sh.jst[(k - 1) & 1][0], sh.jst[(k - 1) & 1][1], sh.jst[(k - 1) & 1][2], sh.jst[(k - 1) & 1][3]};
+      nl = env_take<NS, NA>(P, sh, tb, L, k - 1, fix & 1u, tlim >= 1u, nl, dn, bm, ai, ae);
+      if (tlim == 0 && lane == 0) {  // every resetter of step k - 1 truncates at step k
 #pragma unroll
-      for (int s = 0; s < NS; ++s) sr[s] = apply_jump(J, sr[s]);  // this step's words
-      env_take<NS, NA>(P, sh, tb, L, k - 1, fix & 1u, tlim >= 1u, dn, pre, bm, ai, ae);
+        for (int s = 0; s < NS; ++s) sh.dmask[k & 1][s * EW + w] |= bm[s];
+      }
       lds_release();
       if (lane == 0) lds_add(&sh.res_done, 1u);
+      if (fix & 2u) {  // the prediction missed the window: regenerate it exactly
+        fill_window(L.W(k), jrw, j512, j1024, nw, mk128(sh.rw[k & 1][0], sh.rw[k & 1][1]), lg);
+        lds_release();
+        if (lane == 0) lds_add(&sh.fill_done, 1u);
+        fill_target += EW;
+      }
     }
     if (w == 0) WSTAMP(P, k, 0);
     {  // this step's coarse states: S(x + B + 32 lg + 1)
@@ -830,20 +882,55 @@ __device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Ta
     }
     lds_release();
     if (lane == 0) lds_add(&sh.cs_done, 1u);
+    if (!(tmode & TM_NOPRIO)) __builtin_amdgcn_s_setprio(2);
+    lds_wait(&sh.fill_done, fill_target, derr);  // every env wave's part of this step's window
     if (w == 0) WSTAMP(P, k, 12);
+    // ---- the early count: this wave's done envs of the step ----
+    const bool early = nl <= (uint32_t)NLW && !(tmode & TM_LATE);
+    if (early) {
+      const uint32_t c = env_resolve<NS, NA>(sh, tb, L, k, nl, exactw);
+      if (lane == 0) lds_add(&sh.cnt[k & 1], c);
+      lds_release();
+      if (lane == 0) lds_add(&sh.cnt_done, 1u);
+    }
+    if (w == 0) WSTAMP(P, k, 1);
+    // ---- the next step's window (its base is published once every wave's transitions of step k - 1 are done) ----
+    auto fill_next = [&]() {
+      if (k + 1 < K) {
+        lds_wait(&sh.sy_ready, (uint32_t)k + 1u, derr);
+        const u128 Srw = mk128(sh.rw[(k + 1) & 1][0], sh.rw[(k + 1) & 1][1]);
+        if (!(tmode & TM_NOFILL)) fill_window(L.W(k + 1), jrw, j512, j1024, nw, Srw, lg);
+        lds_release();
+        if (lane == 0) lds_add(&sh.fill_done, 1u);
+        fill_target += EW;
+      }
+    };
+    if (!(tmode & TM_TRANSFIRST)) fill_next();
+    if (w == 0) WSTAMP(P, k, 3);
     // the actions two steps ahead
     if (k + 2 < K) {
 #pragma unroll
       for (int s = 0; s < NS; ++s) a2[s] = act[(size_t)(k + 2) * B + e0 + (size_t)s * 512 + lg];
     }
     if (k >= NSTG) lds_wait(&sh.st_done, (uint32_t)SW * (uint32_t)(k - NSTG + 1), derr);  // staging buffer copied out
-    if (!(tmode & TM_NOPRIO)) __builtin_amdgcn_s_setprio(2);
-    if (w == 0) WSTAMP(P, k, 1);
-    // ---- the full transitions (off the exchange's chain: the early count is already published) ----
+    // ---- the full transitions (off the exchange's chain: the early count is already in) ----
+    const int32_t off = sh.rw_off[k & 1];
+    const uint32_t* Wk = L.W(k);
+    uint32_t fe[NS], tie = 0;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      bool t;
+      fe[s] = eff_hi<NA>(tb, Wk[s * 512 + lg + off], ai[s], t);
+      tie |= (t || exactw) ? (1u << s) : 0u;
+    }
+    if (tie) {  // a word whose high half equals a threshold's (p ~ 2^-32 per compare): its full draw decides
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+        if ((tie >> s) & 1u) fe[s] = eff_full<NA>(tb, window_word(tb, sh.rw[k & 1], (uint32_t)(s * 512 + lg + off)), ai[s]);
+    }
     uint32_t mm[NS];
 #pragma unroll
-    for (int s = 0; s < NS; ++s)
-      mm[s] = tb.mvp[(ae[s] & 0xFFFFu) * NA + eff_action<NA>(tb, pcg_output(sr[s]), ai[s])];
+    for (int s = 0; s < NS; ++s) mm[s] = tb.mvp[(ae[s] & 0xFFFFu) * NA + fe[s]];
     // Per-slot outcomes as bits of VGPR words (bit s), not as live lane masks: eight slots' worth of 64-bit masks
     // would not fit the SGPRs and spill through v_writelane / v_readlane.
     uint32_t sv[NS], ent[NS], trm = 0, nrm = 0;
@@ -859,7 +946,7 @@ __device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Ta
       dn |= done << s;
       acc.ngoal += term;
       acc.nwall += blocked & (term ^ 1u);
-      // the next step: truncated for sure, or goal-adjacent (its word decides); resetters are the control's
+      // the next step: truncated for sure, or goal-adjacent (its word decides); resetters are listed at the take
       const uint32_t tr1 = (done ^ 1u) & (el + 1u > tlim ? 1u : 0u);
       trm |= tr1 << s;
       nrm |= ((done | tr1) ^ 1u) & (gmn != 0u ? 1u : 0u) ? (1u << s) : 0u;
@@ -867,36 +954,33 @@ __device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Ta
     }
 #pragma unroll
     for (int s = 0; s < NS; ++s) reinterpret_cast<uint32_t*>(stg)[s * 512 + lg] = sv[s];
-    uint32_t ntr = 0;
+    bool bad = false;
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       bm[s] = ballot((dn >> s) & 1u);
-      ntr += popc(ballot((trm >> s) & 1u));
+      const uint64_t mt = ballot((trm >> s) & 1u);
+      if (early) bad |= sh.dmask[k & 1][s * EW + w] != bm[s];  // the early count's bits == the step's outcome
+      if (lane == 0 && k + 1 < K) sh.dmask[(k + 1) & 1][s * EW + w] = mt;
     }
-    if (lane == 0) {
+    if (bad && lane == 0) atomicOr(derr, GP_DERR_LOGIC);
+    if (!early) {  // counted from the masks: this wave's part of the step's done bitmap and count
+      uint32_t c = 0;
 #pragma unroll
-      for (int s = 0; s < NS; ++s) sh.mask[s][w] = bm[s];
+      for (int s = 0; s < NS; ++s) {
+        c += popc(bm[s]);
+        if (lane == 0) sh.dmask[k & 1][s * EW + w] = bm[s];
+      }
+      if (lane == 0) lds_add(&sh.cnt[k & 1], c);
+      lds_release();
+      if (lane == 0) lds_add(&sh.cnt_done, 1u);
     }
-    if (k + 1 < K) append_near<NS>(L.NL(k + 1), &sh.nlc[(k + 1) & 1], nrm, ent, ntr);
+    nl = k + 1 < K ? append_near<NS>(L.NL(k + 1, w), 0u, nrm, ent) : 0u;
     acc.eps += (uint32_t)__builtin_popcount(dn);
     lds_release();
     if (lane == 0) lds_add(&sh.trans_done, 1u);
-    if (tmode & TM_ENVDROP) __builtin_amdgcn_s_setprio(0);
     if (w == 0) WSTAMP(P, k, 2);
-    // ---- the step's resetters listed in env order (rank -> slot | next action) ----
-    lds_wait(&sh.trans_done, (uint32_t)EW * (uint32_t)(k + 2), derr);  // every wave's masks
-    {
-      const uint32_t c = lane < NS * EW ? popc(sh.mask[lane >> 3][lane & 7]) : 0u;
-      const uint32_t ex = wave_incl_scan(c) - c;
-#pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        pre[s] = (uint32_t)__builtin_amdgcn_readlane((int)ex, s * EW + w);
-        if ((dn >> s) & 1u) sh.r2s[pre[s] + mbcnt(bm[s])] = (uint16_t)((uint32_t)(s * 512 + lg) | (an[s] << 12));
-      }
-    }
-    lds_release();
-    if (lane == 0) lds_add(&sh.r2s_done, 1u);
-    if (w == 0) WSTAMP(P, k, 3);
+    WSTAMP(P, k, 20 + w);
+    if (tmode & TM_TRANSFIRST) fill_next();
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       ai[s] = an[s];
@@ -906,7 +990,7 @@ __device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Ta
   }
   // the last step's resetters, then its outputs straight from the env waves
   lds_wait(&sh.cells_done, (uint32_t)K, derr);
-  env_take<NS, NA>(P, sh, tb, L, K - 1, sh.fix[K & 1] & 1u, false, dn, pre, bm, ai, ae);
+  env_take<NS, NA>(P, sh, tb, L, K - 1, sh.fix[K & 1] & 1u, false, 0u, dn, bm, ai, ae);
   if (!(tmode & TM_NOSTORE)) {
     const uint32_t* st = reinterpret_cast<const uint32_t*>(L.stg(K - 1, E));
     const size_t base = (size_t)(K - 1) * B + e0 + (size_t)lg;
@@ -950,7 +1034,7 @@ __device__ __forceinline__ void wg_store(const WgParams& P, WgShared& sh, const 
     lds_wait(&sh.res_done, (uint32_t)EW * (uint32_t)(k + 1), derr);  // every resetter's cell in place
     // out of the way of the next step's transitions, except for a launch's last steps, whose copies are the tail
     if (k + WG_EAGER_TAIL < K && !(tmode & TM_EAGERSTORE))
-      lds_wait(&sh.trans_done, (uint32_t)EW * (uint32_t)(k + 3), derr);
+      lds_wait(&sh.trans_done, (uint32_t)EW * (uint32_t)(k + 2), derr);
     if (sl < 64) WSTAMP(P, k, 13);
     const uint32_t* st = reinterpret_cast<const uint32_t*>(L.stg(k, E));
     const size_t base = (size_t)k * B + (size_t)beta * E;
@@ -1026,9 +1110,9 @@ __global__ __launch_bounds__(TPB) void wgrid_rollout(const WgParams* __restrict_
     }
   }
   if (tid == EW * 64) {
-    sh.trans_done = sh.cs_done = sh.r2s_done = sh.res_done = sh.st_done = 0;
-    sh.cells_done = sh.pro = 0;
-    sh.nlc[0] = sh.nlc[1] = 0;
+    sh.trans_done = sh.cnt_done = sh.cs_done = sh.fill_done = sh.res_done = sh.st_done = 0;
+    sh.sy_ready = sh.cells_done = sh.pro = 0;
+    sh.cnt[0] = sh.cnt[1] = 0;
     sh.fix[0] = sh.fix[1] = 0;
   }
   const Tabs tb(dyn, P);

@@ -7,8 +7,8 @@ drives them. Reference semantics: msrooms.py:369-413, rooms.py:177-222, action_u
 
 What each case forces:
 - block sizes E = 512 / 1024 / 2048 / 4096 envs (the strong-scaling shards of 1M envs over 8 / 4 / 2 GPUs);
-- launches of 1 to 128 steps back to back (the stream position and env states carried across launches);
-- most envs on goal-adjacent cells (the early count's list overflowing into the mask count, mass resets);
+- a window halo of 512 draws, and a prediction bias that puts every step's window outside its halo (the exact
+  regeneration after the exchange);
 - a Lemire rejection planted in the choice() stream inside a launch (the slow path: rejected positions listed,
   every resetter placed exactly);
 - ordinal actions (8 thresholds per row) and table obs (ROOMS layouts).
@@ -74,16 +74,19 @@ def test_wgrid_block_sizes_bit_exact(B, E, gpu_device):
     assert m["env_steps"] == B * 54
 
 
-@pytest.mark.parametrize("chunks", [(1, 1, 2, 3), (5, 64, 1), (127, 2)])
-def test_wgrid_launch_boundaries(chunks, gpu_device):
-    """Launches of every length carry the stream position, the buffered half-word, the last step's reset count
-    (the candidate cells' prediction) and the env states across launch boundaries exactly."""
+@pytest.mark.parametrize("knobs", [dict(wg_halo=512), dict(wg_bias=3000), dict(wg_bias=-600)])
+def test_wgrid_halo_and_forced_window_misses(knobs, gpu_device):
+    """wg_bias shifts every step's predicted reset count (3000 resets = ~1500 draws, far beyond the 256-draw
+    halo; -600 wraps to a huge count): each step's window is regenerated exactly after the exchange."""
+    from gym_po_amd._lib import debug_knobs
     B = 1 << 20
-    env = _fourrooms(B, gpu_device)
+    with debug_knobs(**knobs):
+        env = _fourrooms(B, gpu_device)
     assert env.query("wgrid") == 1
+    assert env.query("wgrid_halo") == knobs.get("wg_halo", 256)
     ora = gridworld.FourRoomsOracle(B, 1, obs_type="hansen")
     np.testing.assert_array_equal(_reset_obs(env, 5).astype(np.int64), np.asarray(ora.reset_seed(5)).astype(np.int64))
-    _check_chunks(env, ora, chunks, action_seed=9, n_act=4)
+    _check_chunks(env, ora, (12, 5), action_seed=9, n_act=4)
 
 
 def _rejected_word(n, k=1):
@@ -206,11 +209,12 @@ def test_wgrid_goal_crowd_bit_exact(B, frac, gpu_device):
     _check_chunks(env, ora, (6, 1, 9), action_seed=11, n_act=4)
 
 
-@pytest.mark.parametrize("tmode", [4, 128, 1024, 128 | 1024])
+@pytest.mark.parametrize("tmode", [4, 512, 1024, 512 | 1024, 2048, 128])
 def test_wgrid_schedule_variants_bit_exact(tmode, gpu_device):
-    """Test-only schedules of the windowed kernel (gp_debug_set wg_tmode): 4 = the count published from the masks
-    after the full transitions (no early count), 128 = no candidate cells (every resetter's word drawn after the
-    exchange), 1024 = the env waves place every step's resetters."""
+    """Test-only schedules of the windowed kernel (gp_debug_set wg_tmode): 4 = every env wave counts from its full
+    transitions (no early count), 512 = every window word re-derived from the window's base state (the path a
+    high-half tie takes), 1024 = the env waves place every step's resetters, 2048 = transitions before the next
+    window's fill, 128 = no candidate cells (every resetter's word drawn after the exchange)."""
     from gym_po_amd._lib import debug_knobs
     B = 1 << 18
     with debug_knobs(wg_tmode=tmode):

@@ -3,12 +3,12 @@
     python gym-po-taxi_amd/build.py --stamps && python tools/wstamps.py [B] [K]
 
 Stamps are s_memrealtime (100 MHz, synchronous across XCDs), kept in LDS, for the first 32 steps of a launch,
-per block and step k (round-5 schedule: early count, per-env PCG states):
-  env wave 0: 16 cells_done seen, 0 states advanced + resetter cells taken (step start), 12 coarse states done,
-              1 transitions start (after the staging wait), 2 transitions done (lists appended), 3 resetters listed,
-              18 next actions converted
-  control:    5 lists ready, 6 granule published (early count), 8 candidate cells done, 9 all-gather done,
-              10 cells placed / cells_done, 11 next rejection check + block base done
+per block and step k (round-5 schedule: windows, early count by the env waves, ranks):
+  env wave 0: 16 cells_done seen, 0 resetter cells taken (window regenerated if it missed), 12 window ready,
+              1 early count added, 3 next window filled, 2 transitions done, 18 next actions converted;
+              20 + w: env wave w's transitions done
+  control:    7 S(y) / next window base published, 5 block count ready, 6 granule published, 8 ranks + candidate
+              cells done, 9 all-gather done, 10 cells placed / cells_done, 11 next rejection check done
   store wave: 13 copy start, 14 copy issued
 Launch stamps per block: 0 entry, 1 P1 passed (control), 3 step loop done, 4 kernel end.
 """
@@ -77,23 +77,27 @@ def rep(name, d):
 
 
 rep("step (env wave 0 start -> next start)", nx[:, :, 0] - x[:, :, 0])
-rep("env: coarse states (0->12)", x[:, :, 12] - x[:, :, 0])
-rep("env: staging wait (12->1)", x[:, :, 1] - x[:, :, 12])
-rep("env: transitions + lists (1->2)", x[:, :, 2] - x[:, :, 1])
-rep("env: masks wait + resetter listing (2->3)", x[:, :, 3] - x[:, :, 2])
-rep("env: next actions converted (3->18)", x[:, :, 18] - x[:, :, 3])
+rep("env: window wait (0->12)", x[:, :, 12] - x[:, :, 0])
+rep("env: early count (12->1)", x[:, :, 1] - x[:, :, 12])
+rep("env: next window fill (1->3)", x[:, :, 3] - x[:, :, 1])
+rep("env: transitions (3->2)", x[:, :, 2] - x[:, :, 3])
+rep("env: next actions (2->18)", x[:, :, 18] - x[:, :, 2])
 rep("env: wait cells_done (18->next 16)", nx[:, :, 16] - x[:, :, 18])
-rep("env: advance + take cells (16->0)", x[:, :, 0] - x[:, :, 16])
-rep("ctrl: wait lists (prev 11 -> 5)", x[:, :, 5] - pv[:, :, 11])
-rep("ctrl: resolve + publish (5->6)", x[:, :, 6] - x[:, :, 5])
-rep("ctrl: S(y) + candidates (6->8)", x[:, :, 8] - x[:, :, 6])
+rep("env: take cells (16->0)", x[:, :, 0] - x[:, :, 16])
+rep("ctrl: trans wait + S(y) (prev 11 -> 7)", x[:, :, 7] - pv[:, :, 11])
+rep("ctrl: count wait (7 -> 5)", x[:, :, 5] - x[:, :, 7])
+rep("ctrl: publish (5->6)", x[:, :, 6] - x[:, :, 5])
+rep("ctrl: ranks + candidates (6->8)", x[:, :, 8] - x[:, :, 6])
 rep("ctrl: gather (8->9)", x[:, :, 9] - x[:, :, 8])
 rep("ctrl: publish -> gather done (6->9)", x[:, :, 9] - x[:, :, 6])
-rep("ctrl: J + r2s wait + cells (9->10)", x[:, :, 10] - x[:, :, 9])
-rep("ctrl: next rejection check + base (10->11)", x[:, :, 11] - x[:, :, 10])
+rep("ctrl: cells (9->10)", x[:, :, 10] - x[:, :, 9])
+rep("ctrl: next rejection check (10->11)", x[:, :, 11] - x[:, :, 10])
+rep("cells_done -> next count ready (10 -> next 5)", nx[:, :, 5] - x[:, :, 10])
 pub = x[:, :, 6]
 print(f"  publish spread across blocks (max-min)         median {np.median(pub.max(0) - pub.min(0)):.0f} ns")
 print(f"  gather done - last publish                     median {np.median(x[:, :, 9] - pub.max(0)[None]):.0f} ns")
-print(f"  cells_done -> env transitions done (10 -> next 2)  median {np.median(nx[:, :, 2] - x[:, :, 10]):.0f} ns")
 rep("store: copy issue (13->14)", x[:, :, 14] - x[:, :, 13])
+tw = x[:, :, 20:28] - x[:, :, 3][:, :, None]
+print("  transitions done per env wave (from wave 0's start), median:", [int(v) for v in np.median(tw, (0, 1))])
+print("  transitions done per env wave, p90:", [int(v) for v in np.percentile(tw, 90, (0, 1))])
 print("block 0, step 10 (ns from env start):", (a[0, 10] - a[0, 10, 0]).tolist())
