@@ -1182,7 +1182,7 @@ constexpr int XGT = 256;          // threads (positions / envs) per block of the
 constexpr int XGW = XGT / 64;     // waves (bitmap words) per block
 constexpr int XG_LOOK = 64;       // the halo of a normal call's block view (one wave)
 constexpr int XG_SPAN = 32;       // longest slow attempt (a 15-pair tail; else GP_DERR_STREAM)
-constexpr int XG_MIN_ENVS = 4096; // at or below: the one-workgroup kernel (fewer launches per step)
+constexpr int XG_MIN_ENVS = 1024; // at or below: the one-workgroup kernel (measured crossover)
 #ifndef XG_SPLIT_NORMALS
 #define XG_SPLIT_NORMALS 0        // 1: normal / choice calls as two launches each (count, then write; round 3's form)
 #endif
@@ -2268,7 +2268,8 @@ struct CRoomsBackend : EnvBackend {
   int xg_P = 0;                  // positions of a draw call (>= what normal(2B) needs)
   int xg_nbe = 0;                // env blocks
   int xg_slot = 0;               // the stream-state slot holding the current state (0 between API calls)
-  bool xg_on() const { return rng_mode == GP_RNG_NUMPY && B > XG_MIN_ENVS; }
+  int xg_min = XG_MIN_ENVS;       // at or below: the one-workgroup kernel (gp_debug_set xg_min_envs at create)
+  bool xg_on() const { return rng_mode == GP_RNG_NUMPY && B > xg_min; }
   bool xg_split = false;         // gp_debug_set("disable_fused", 1) at create: the two-launch draw calls (tests)
   bool xg_fused() const { return !XG_SPLIT_NORMALS && !xg_split && B <= XG_FUSE_MAX_ENVS; }  // one launch per call
   DevBuf xg_xend, xg_xinfo;      // the wall-noise extension of the action-noise call (XgCall::xinfo)
@@ -2872,7 +2873,8 @@ int CRoomsBackend::x_alloc() {
   xd.ai = x_ai.as<int32_t>();
   xd.rank = x_rank.as<int32_t>();
   xd.lemire_thr = lemire_threshold((uint32_t)d.n_valid);
-  if (B > XG_MIN_ENVS) {
+  if (gp_debug_knobs().xg_min_envs >= 0) xg_min = gp_debug_knobs().xg_min_envs;
+  if (B > xg_min) {
     // positions of a draw call: normal(2B) needs 2B + 2B / 16 + 4096 at most (xg_norm_need), rounded to blocks;
     // with the wall-noise extension (fused calls) up to 2B more normals
     const int64_t nmax = (xg_fused() ? 4 : 2) * b;

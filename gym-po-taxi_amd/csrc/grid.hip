@@ -2968,38 +2968,20 @@ int GridBackend::build_wgrid(const std::vector<uint16_t>& move, const std::vecto
   };
   put(L.j32, sizeof(PcgJump) * 32);
   put(L.jt8, sizeof(PcgJump) * 512);
-  put(L.move, (size_t)nc * na * 4);
+  put(L.move, (size_t)nc * na * 2);
   put(L.thr, (size_t)na * na * 8);
-  put(L.thh, (size_t)na * na * 4);
   put(L.ocell, (size_t)nc * 4);
-  put(L.avalid, agent_valid_h.size() * 4);
-  put(L.gmc, (size_t)nc);
+  put(L.avalid, agent_valid_h.size() * 2);
   L.total = off;
   const size_t lds = (size_t)wg_dyn_bytes(L.total, E, H);
   if (!wgrid_fits(E / 512, na, lds)) return GP_OK;
-  // goal-action masks (msrooms.py:401-407): bit a of gm[c] <=> effective action a moves an agent on c onto the goal
-  // (a blocked move stays on c). Only envs on cells with gm != 0 can terminate at a step: the early count.
-  const uint32_t goal = (uint32_t)d.fixed_goal;
-  std::vector<uint8_t> gm((size_t)nc, 0);
-  for (int c = 0; c < nc; ++c)
-    for (int a = 0; a < na; ++a)
-      if ((uint32_t)(move[(size_t)c * na + a] & 0x7FFFu) == goal) gm[(size_t)c] |= (uint8_t)(1u << a);
-  auto gm_of = [&](uint32_t c) -> uint32_t { return c < (uint32_t)nc ? gm[c] : 0u; };
-  std::vector<uint32_t> mv(move.size()), th_hi(thr.size()), av(agent_valid_h.size());
-  for (size_t i = 0; i < move.size(); ++i) mv[i] = (uint32_t)move[i] | (gm_of(move[i] & 0x7FFFu) << 16);
-  for (size_t i = 0; i < agent_valid_h.size(); ++i) av[i] = (uint32_t)agent_valid_h[i] | (gm_of(agent_valid_h[i]) << 16);
   wg_img.assign((size_t)L.total, 0);
-  memcpy(wg_img.data() + L.move, mv.data(), mv.size() * 4);
+  memcpy(wg_img.data() + L.move, move.data(), move.size() * 2);
   std::vector<uint64_t> th(thr.size());
-  for (size_t i = 0; i < thr.size(); ++i) {
-    th[i] = thr_on_u64(thr[i]);
-    th_hi[i] = (uint32_t)(th[i] >> 32);
-  }
+  for (size_t i = 0; i < thr.size(); ++i) th[i] = thr_on_u64(thr[i]);
   memcpy(wg_img.data() + L.thr, th.data(), th.size() * 8);
-  memcpy(wg_img.data() + L.thh, th_hi.data(), th_hi.size() * 4);
   memcpy(wg_img.data() + L.ocell, ocell.data(), ocell.size() * 4);
-  memcpy(wg_img.data() + L.avalid, av.data(), av.size() * 4);
-  memcpy(wg_img.data() + L.gmc, gm.data(), gm.size());
+  memcpy(wg_img.data() + L.avalid, agent_valid_h.data(), agent_valid_h.size() * 2);
   wg_G = (int)(B / E);
   wg_E = E;
   wg_NS = E / 512;
@@ -3078,7 +3060,6 @@ int GridBackend::upload_wgrid() {
   }
   w.jB = pcg_jump_params((u128)B, inc);
   w.j512 = pcg_jump_params((u128)512, inc);
-  w.j1024 = pcg_jump_params((u128)1024, inc);
   w.jt64 = d.jt;
   w.dbg = d.dbg;
   w.ctl = d.ctl;

@@ -27,13 +27,8 @@ struct alignas(32) MetricSlot {
 // device memory (WgParams, refreshed on every seed); the launch passes a pointer and the per-call buffers.
 constexpr int WG_HMAX = 512;  // largest halo (u64 draws on each side of a predicted window)
 
-constexpr int WG_NLW = 64;     // goal-adjacent envs per env wave and step the early count lists (more: its masks)
-
 struct WgLds {  // byte offsets of the tables in the LDS image (WgParams::limg, copied verbatim into LDS)
-  // move: u32 [ncells][NA] = new cell | blocked << 15 | goal-action mask of the new cell << 16
-  // thr: u64 [NA][NA] thresholds on the full draw; thh: u32 [NA][NA] their high halves
-  // avalid: u32 [n_agent] = valid agent cell | its goal-action mask << 16; gmc: u8 [ncells] goal-action masks
-  int32_t j32, jt8, move, thr, thh, ocell, avalid, gmc, total;
+  int32_t j32, jt8, move, thr, ocell, avalid, total;
 };
 
 struct WgParams {
@@ -55,7 +50,7 @@ struct WgParams {
   const PcgJump* jblk;          // [G][2]: by B + E beta - H (beta > 0; B for beta 0): the next window's base after
                                 //   the choice() draws; by E beta - H + 1 (beta > 0; 0 for beta 0): a launch's first
   const PcgJump* jt64;          // radix-64 general jump tables (JT_LEVELS x 64) for the rare paths
-  PcgJump jB, j512, j1024;      // jump by B (random(B)), by 512 / 1024 (a lane's next window words)
+  PcgJump jB, j512;             // jump by B (random(B)), by 512 (a lane's next window word)
   GridCtl* ctl;
   MetricSlot* mslot;            // [G]
   uint32_t* ae;                 // [B] agent cell | elapsed << 16
@@ -73,13 +68,12 @@ struct WgArgs {  // one launch: K steps, caller-owned action [K][B] and output [
   uint8_t* trunc;
 };
 
-// Dynamic LDS bytes of a launch (tables + two windows of high halves + coarse states + staging + the env waves'
-// near lists, 8 env waves).
+// Dynamic LDS bytes of a launch (tables + window + coarse states + staging).
 __host__ __device__ constexpr int wg_dyn_bytes(int tables, int E, int H) {
 #ifndef WG_NSTG
 #define WG_NSTG 3
 #endif
-  return tables + 2 * (E + 2 * H) * 4 + 2 * 512 * 16 + WG_NSTG * E * 4 + 2 * 8 * WG_NLW * 4;
+  return tables + (E + 2 * H) * 8 + 2 * 512 * 16 + WG_NSTG * E * 4;
 }
 // Launch on `s` (host; csrc/wgrid.hip). Returns hipError_t as int.
 int wgrid_launch(const WgArgs& a, int NS, int NA, int G, size_t dyn_lds, hipStream_t s);

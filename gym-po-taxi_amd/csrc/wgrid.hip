@@ -8,38 +8,27 @@
 //
 // Design (one workgroup of 11 waves per CU, block beta owns the E = 512 * NS consecutive envs [E beta, E beta + E);
 // env slot i = k * 512 + 64 w + l of env wave w, lane l, slot k):
-//  * WINDOWS. The random(B) words a block needs at step t+1 depend on the stream only through the position
-//    x_{t+1} = y_t + used_t (y_t = x_t + B). The env waves fill a window of E + 2H consecutive draws (their high 32
-//    bits) around the predicted position (used predicted from the previous step's b) while step t runs; env i then
-//    reads window word i + rw_off. Two windows (by step parity). A prediction more than H off regenerates the window
-//    exactly; a word whose high half equals a threshold's high half (p ~ 2^-32 per compare) is re-derived exactly.
-//  * EARLY COUNT. Only two things end an episode at step t (msrooms.py:405-412): truncation, elapsed + 1 >
-//    time_limit, known from the state alone, and reaching the goal, which needs the env's word, action and cell.
-//    An env can reach the goal only from a cell where some effective action lands on it (the goal-action mask
-//    gm[cell], from the move table; ~3% of the envs on FR_MAP). Each env wave lists its goal-adjacent envs for the
-//    next step during its transitions (and its resetters that land next to the goal when it takes their cells), so
-//    at a step's start it resolves only those (one compacted pass: window word, thresholds, gm) and adds its done
-//    count; the control wave publishes the block's count as soon as the 8 waves have, and the full transitions and
-//    the next window's fill run while the granules travel. A wave whose list overflows counts from its full
-//    transitions instead; every step checks each wave's done ballots against the step's done bitmap
-//    (GP_DERR_LOGIC).
-//  * RANKS. The step's done bitmap (truncations written by the env waves a step ahead, goal hits OR-ed in by the
-//    early count) gives every resetter its rank in the block before the exchange ends; the control wave places the
-//    cells by rank (rank q takes choice() half-word R + q) and each env wave takes its resetters' cells by rank.
+//  * The random(B) words a block needs at step t+1 depend on the stream only through the position x_{t+1} =
+//    y_t + used_t (y_t = x_t + B). The words themselves can be computed before used_t is known: while step t's
+//    exchange is in flight, the 8 env waves fill a WINDOW of E + 2H consecutive u64 draws around the predicted
+//    position (used predicted from the previous step's b). After the exchange env i reads window word
+//    i + rw_off, rw_off = H + used_t - used_pred; a prediction more than H off regenerates the window exactly
+//    (measured miss rate: tools/window_stats.py). So the step's critical path is only
+//      transitions (window word -> integer threshold compares -> LDS move table) -> granule publish ->
+//      all-gather of the G granules -> the block's resetter cells -> barrier,
+//    and the PCG64 work (~40 VALU per word) runs on the otherwise idle SIMDs during the exchange.
 //  * choice() words: 512 COARSE STATES S(y + 1 + 32 j) (one per env lane, a per-lane constant jump) cover the
 //    first 16384 draws after random(B); a resetter's word is one jump (<= 31 steps, LDS table) from a coarse state.
-//    During the exchange the control wave draws the cells of the 512 half-words around the predicted block prefix.
 //  * Lemire rejections (p ~ 2.4e-8 per word for 104 cells): each block checks a 62-draw slice of the choice
 //    stream before publishing (slices of all blocks cover 124 G half-words); the granule carries the count.
 //    Any rejection, or more resets than the slices cover, takes the exact slow path: coverage rounds (one more
-//    granule exchange each), the rejected positions listed, and every resetter's word placed exactly (by the env
-//    waves, which also do it when a block has more resetters than the control wave places quickly).
+//    granule exchange each), the rejected positions listed, and every resetter's word placed exactly.
 //  * Outputs: the env waves stage {cell, term, trunc, wall-bump} per env (4 B) in LDS; two store waves turn a
 //    step's staging into obs (per-cell obs table), reward, terminated and truncated with 16-B non-temporal
-//    stores while the next steps run.
-// Synchronisation: no workgroup barrier inside the step loop, monotone LDS counters; cross-block only the tagged
-// 8-B granules (agent-scope relaxed stores / polls, MI355X_MICROARCH.md "handoff" rows), each wait bounded by
-// spin_limit (GridCtl::err flags a grid that cannot make progress).
+//    stores while the next step runs (double-buffered staging).
+// Synchronisation: one workgroup barrier per step (B2, after the exchange) plus LDS counters; cross-block only
+// the tagged 8-B granules (agent-scope relaxed stores / polls, MI355X_MICROARCH.md "handoff" rows), each wait
+// bounded by spin_limit (GridCtl::err flags a grid that cannot make progress).
 #include <stdint.h>
 
 #include "gp_internal.h"
@@ -48,15 +37,13 @@
 namespace {
 
 // GP_STAMPS diagnostic builds (tools/wstamps.py): s_memrealtime (100 MHz, chip-synchronous) stamps by one lane.
-// Step stamps go to LDS (WgShared::stp; copied out at the kernel's end): a global store per stamp would sit in the
-// stamping wave's vmcnt and stretch every later vmcnt wait of that wave.
 #ifdef GP_STAMPS
 #define WSTAMP(P, k, i)                                                                                  \
   do {                                                                                                   \
-    if ((threadIdx.x & 63) == 0 && (k) < 32) {                                                           \
+    if ((threadIdx.x & 63) == 0 && (k) < 64) {                                                           \
       unsigned long long t_;                                                                             \
       asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                     \
-      sh.stp[(k)][(i)] = t_;                                                                             \
+      (P).dbg[((size_t)blockIdx.x * 64 + (k)) * 16 + (i)] = t_;                                          \
     }                                                                                                    \
   } while (0)
 #define LSTAMP(P, i)                                                                                     \
@@ -76,64 +63,52 @@ namespace {
   } while (0)
 #endif
 
-// Timing-study and test variants (WgParams::tmode, gp_debug_set "wg_tmode"; 0 in production). TM_NOSTORE and
-// TM_NOFILL drop work (results invalid: measurement only); the others give exact results.
-constexpr int TM_NOSTORE = 1;     // store waves skip the output copy
-constexpr int TM_NOFILL = 2;      // env waves skip the window fill (stale words)
-constexpr int TM_LATE = 4;        // every env wave counts from its full transitions (no early count)
-constexpr int TM_THROTTLE = 8;    // store waves drain their stores after every 16-env chunk (vmcnt(0))
-constexpr int TM_BUSYPOLL = 16;   // the all-gather polls without s_sleep
-constexpr int TM_NOPRIO = 32;     // env waves keep priority 0 (default: 2, above the store waves)
+// Timing-study variants (WgParams::tmode, gp_debug_set "wg_tmode"; never set in production). TM_NOSTORE and TM_NOFILL
+// drop work (results invalid: measurement only); the others are alternative schedules with exact results.
+constexpr int TM_NOSTORE = 1;   // store waves skip the output copy
+constexpr int TM_NOFILL = 2;    // env waves skip the window fill (stale words)
+constexpr int TM_LATEACT = 4;   // env waves load the next step's actions after the transitions (default: before)
+constexpr int TM_THROTTLE = 8;  // store waves drain their stores after every 16-env chunk (vmcnt(0))
+constexpr int TM_BUSYPOLL = 16; // the all-gather polls without s_sleep
+constexpr int TM_NOPRIO = 32;   // env waves keep priority 0 through their transitions (default: 2, above the store waves)
 constexpr int TM_EAGERSTORE = 64; // store waves copy a step as soon as it is final (default: after the next transitions)
-constexpr int TM_NOCAND = 128;    // no candidate cells during the all-gather (every resetter's cell drawn after it)
-constexpr int TM_STORELOW = 256;  // store waves at priority 0 (default 1)
-constexpr int TM_EXACTW = 512;    // every window word re-derived from the base state (the tie path, for parity tests)
-constexpr int TM_ENVPLACE = 1024; // the env waves place every step's resetters (the slow-path placement, for tests)
-constexpr int TM_TRANSFIRST = 2048; // env waves run the transitions before the next window's fill (default: after)
-constexpr int TM_CTRLHIGH = 4096; // the control wave stays at priority 3 while it draws candidates (default: 1)
+constexpr int TM_NOCAND = 128;  // no candidate cells during the all-gather (every resetter's cell drawn after it)
+constexpr int TM_STORELOW = 256; // store waves at priority 0 (default 1)
+constexpr int TM_ENVHIGH = 512; // env waves at priority 2 throughout (default: 2 for the transitions, 0 otherwise)
 
 constexpr int EW = 8;                 // env waves
 constexpr int SW = 2;                 // store waves
 constexpr int CWAVE = EW;             // the control wave
 constexpr int NWAVES = EW + 1 + SW;
 constexpr int TPB = NWAVES * 64;      // 704 threads
+constexpr int NL = EW * 64;           // env lanes (512)
 constexpr int SLICE = 62;             // u64 draws per rejection-check slice (124 half-words)
 constexpr int MAXRP = 512;            // rejected half-word positions the slow path lists
 constexpr int NCAND = 512;            // candidate resetter cells drawn during the all-gather (256 u64 draws)
 constexpr uint32_t CAND_W = 192;      // half-words of them before the predicted block prefix
-constexpr uint32_t CB_CTRL = 256;     // resetters per block the control wave places itself (more: the env waves)
-constexpr int NLW = WG_NLW;           // goal-adjacent envs per env wave and step the early count lists
 
 struct WgShared {
-  // Per step parity, one 64-bit word per (env slot k, env wave w) = 64 env slots: dmask = the step's done envs
-  // (truncations written a step ahead, goal hits OR-ed in by the early count), pre = the block's resetters before
-  // each word (the ranks).
-  uint64_t dmask[2][64];
-  uint32_t pre[2][64];
+  uint64_t mask[8][EW];      // this step's resetter ballots by (slot k, env wave w)
   // monotone LDS counters: the waves never meet at a workgroup barrier inside the step loop
-  uint32_t trans_done;       // env waves done with a step's full transitions
-  uint32_t cnt_done;         // env waves done adding a step's done count (EW per step)
+  uint32_t trans_done;       // env waves done with a step's transitions (EW per step)
   uint32_t cs_done;          // env waves done with a step's coarse states
+  uint32_t r2s_done;         // env waves done listing a step's resetters in r2s
   uint32_t fill_done;        // env-wave window fills (and exact regenerations) completed
-  uint32_t res_done;         // env waves done taking (or placing) the previous step's resetter cells
+  uint32_t res_done;         // env waves done taking a step's resetter cells (the staging is final)
   uint32_t st_done;          // store-wave step copies completed (SW per step)
+  uint32_t sx_ready;         // control wave: step k's S(x) published (k + 1)
   uint32_t sy_ready;         // control wave: step k's S(y) and step k+1's window base published (k + 1)
-  uint32_t cells_done;       // control wave: step k's exchange done, cells placed, S(x_{k+1}), rw_off, fix (k + 1)
-  uint32_t pro;              // prologue: the first window's base and S(x_0) are published
-  uint32_t cnt[2];           // by step parity: the block's done count (the env waves' adds)
+  uint32_t cells_done;       // control wave: step k's exchange finished, its resetters' cells staged (k + 1)
+  uint32_t pro;              // prologue: the first window's base is published
   uint64_t sx[2][2];         // by step parity: S(x_t) (hi, lo), the state at the step's start
   uint64_t sy[2][2];         // by step parity: S(y_t) (hi, lo), the state after the step's random(B)
   uint64_t rw[2][2];         // by parity of the step a window serves: its base state (hi, lo)
   int32_t rw_off[2];         // by step parity: env i of that step reads window word i + rw_off
-  uint32_t fix[2];           // by step parity, acted on at the step's start: bit 0 the env waves place the previous
-                             // step's resetters (slow path / many resetters), bit 1 regenerate the step's window
-  uint32_t R, h, u, nrp;     // env placement: block prefix, has_uint32 / uinteger at the step start, # positions
+  uint32_t fix[2];           // by step parity: bit 0 slow path, bit 1 window regeneration
+  uint32_t R, h, u, nrp;     // slow path: block prefix, has_uint32 / uinteger at the step start, # positions
   uint32_t rp[MAXRP];        // slow path: rejected half-word positions, ascending
-  uint32_t rc[CB_CTRL];      // the control wave's placement: cell of resetter rank q | its goal-action mask << 16
-  uint32_t cand[NCAND];      // half-words cbase .. cbase + NCAND - 1: candidate cell | its goal-action mask << 16
-#ifdef GP_STAMPS
-  unsigned long long stp[32][32];  // step stamps of the first 32 steps (GP_STAMPS builds)
-#endif
+  uint16_t r2s[4096];        // resetter rank in the block -> env slot
+  uint16_t cand[NCAND];      // the cells of choice() half-words cbase .. cbase + NCAND - 1 (predicted block prefix)
 };
 
 // ------------------------------------------------------------------ small helpers ----
@@ -150,9 +125,6 @@ __device__ __forceinline__ uint32_t lds_load(const uint32_t* p) {
 __device__ __forceinline__ void lds_add(uint32_t* p, uint32_t v) {
   __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-__device__ __forceinline__ void lds_set(uint32_t* p, uint32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
 // Wait (one wave) until an LDS counter reaches `want`. Every wave of the block is resident, so this ends; the
 // bound (~2^26 polls) only turns a logic error into a flagged launch (GP_DERR_TIMEOUT) instead of a hung GPU.
 __device__ __forceinline__ void lds_wait(const uint32_t* p, uint32_t want, uint32_t* err) {
@@ -165,11 +137,6 @@ __device__ __forceinline__ void lds_wait(const uint32_t* p, uint32_t want, uint3
     }
   }
   lds_acquire();
-}
-__device__ __forceinline__ void wave_sync_lds() {  // this wave's LDS writes visible to its own later reads
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
 }
 
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {  // DPP row shifts + broadcasts
@@ -188,8 +155,6 @@ __device__ __forceinline__ uint32_t mbcnt(uint64_t m) {  // set bits of m below 
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot((int)p); }
-__device__ __forceinline__ uint32_t popc(uint64_t m) { return (uint32_t)__builtin_popcountll(m); }
-__device__ __forceinline__ uint32_t hi32(uint64_t x) { return (uint32_t)(x >> 32); }
 
 // numpy next_uint32 bookkeeping after `wtot` 32-bit words: u64 draws used and the new buffer flag.
 __device__ __forceinline__ void words_to_draws(uint32_t wtot, uint32_t h0, uint32_t& used, uint32_t& h) {
@@ -207,66 +172,31 @@ __host__ __device__ __forceinline__ uint64_t thr_on_u64(uint64_t t) {
   return t >= (1ull << 53) ? ~0ull : ((t << 11) | 0x7FFull);
 }
 
-// Action -> row index (numpy negative indexing; out-of-range actions, an IndexError in the reference
-// (msrooms.py:400 action_matrix[action]), set GP_DERR_ACTION and are clamped).
+// Action -> byte offset of its threshold row (numpy negative indexing; out-of-range actions, an IndexError in
+// the reference (msrooms.py:400 action_matrix[action]), set GP_DERR_ACTION and are clamped).
 template <int NA>
-__device__ __forceinline__ uint32_t action_index(int32_t a, uint32_t* derr) {
+__device__ __forceinline__ int32_t action_row(int32_t a, uint32_t* derr) {
   if (action_out_of_range(a, NA)) flag_bad_action(derr);
   if (a < 0) a += NA;
-  return (uint32_t)min(max(a, 0), NA - 1);
+  return min(max(a, 0), NA - 1) * NA * 8;
 }
 
 struct Tabs {  // the LDS copy of the tables (pointers resolved once per role)
   const PcgJump* j32p;   // [32] jump by d
   const PcgJump* jt8p;   // [2][256] jump by d, by 256 d
-  const uint32_t* mvp;   // [ncells][NA] new cell | blocked << 15 | goal-action mask of the new cell << 16
-  const uint64_t* thp;   // [NA][NA] thresholds on the full draw
-  const uint32_t* thhp;  // [NA][NA] their high halves
   const int32_t* ocp;    // [ncells] obs of the agent cell (fixed goal)
-  const uint32_t* avp;   // [n_agent] valid agent cell | goal-action mask << 16
-  const uint8_t* gmp;    // [ncells] goal-action masks
+  const uint16_t* avp;   // [n_agent] valid agent cells
   const PcgJump* jt64;   // global radix-64 tables
+  int32_t halo;
   __device__ __forceinline__ Tabs(const char* d, const WgParams& P)
       : j32p(reinterpret_cast<const PcgJump*>(d + P.lds.j32)), jt8p(reinterpret_cast<const PcgJump*>(d + P.lds.jt8)),
-        mvp(reinterpret_cast<const uint32_t*>(d + P.lds.move)), thp(reinterpret_cast<const uint64_t*>(d + P.lds.thr)),
-        thhp(reinterpret_cast<const uint32_t*>(d + P.lds.thh)), ocp(reinterpret_cast<const int32_t*>(d + P.lds.ocell)),
-        avp(reinterpret_cast<const uint32_t*>(d + P.lds.avalid)), gmp(reinterpret_cast<const uint8_t*>(d + P.lds.gmc)),
-        jt64(P.jt64) {}
+        ocp(reinterpret_cast<const int32_t*>(d + P.lds.ocell)), avp(reinterpret_cast<const uint16_t*>(d + P.lds.avalid)),
+        jt64(P.jt64), halo(P.halo) {}
   __device__ __forceinline__ const PcgJump& j32(uint32_t i) const { return j32p[i]; }
   __device__ __forceinline__ const PcgJump& jt8(uint32_t i) const { return jt8p[i]; }
   __device__ __forceinline__ int32_t ocell(uint32_t c) const { return ocp[c]; }
   __device__ __forceinline__ uint32_t avalid(uint32_t v) const { return avp[v]; }
 };
-
-// Effective action (action_utils.py:84-90 in integer form: #{j : x > thr[a][j]}) from the high half of the draw;
-// `tie` when the high half equals a threshold's (then only the full draw decides).
-template <int NA>
-__device__ __forceinline__ uint32_t eff_hi(const Tabs& tb, uint32_t xh, uint32_t a, bool& tie) {
-  const uint4* r = reinterpret_cast<const uint4*>(tb.thhp + a * NA);
-  uint32_t t[NA];
-#pragma unroll
-  for (int q = 0; q < NA / 4; ++q) {
-    const uint4 v = r[q];
-    t[4 * q] = v.x; t[4 * q + 1] = v.y; t[4 * q + 2] = v.z; t[4 * q + 3] = v.w;
-  }
-  uint32_t c = 0;
-  bool eq = false;
-#pragma unroll
-  for (int j = 0; j + 1 < NA; ++j) {
-    c += xh > t[j] ? 1u : 0u;
-    eq |= xh == t[j];
-  }
-  tie = eq;
-  return c;
-}
-template <int NA>
-__device__ __forceinline__ uint32_t eff_full(const Tabs& tb, uint64_t x, uint32_t a) {
-  const uint64_t* r = tb.thp + a * NA;
-  uint32_t c = 0;
-#pragma unroll
-  for (int j = 0; j + 1 < NA; ++j) c += x > r[j] ? 1u : 0u;
-  return c;
-}
 
 // Coarse state j (S(y + 1 + 32 j)) from its LDS slot (lo, hi).
 __device__ __forceinline__ u128 load_cs(const uint64_t* CS, uint32_t j) {
@@ -288,16 +218,12 @@ __device__ __forceinline__ u128 jump_any(const Tabs& tb, u128 s, uint32_t n) {
   return pcg_jump(tb.jt64, s, n);
 }
 
-// The full draw of window word j of a window with base state rw (word j = output of the base advanced by j).
-__device__ __forceinline__ uint64_t window_word(const Tabs& tb, const uint64_t (&rw)[2], uint32_t j) {
-  return pcg_output(jump_any(tb, mk128(rw[0], rw[1]), j));
-}
-
 // The base of the next step's window for block beta when the current step's choice() call uses `used` u64 draws:
 // the state whose next output is window word 0, from S(x_t) (jb = jblk[beta][0] folds in random(B) and E beta - H),
 // and heff = how many window words precede the block's first env word.
-__device__ __forceinline__ u128 rw_base(const Tabs& tb, const PcgJump& jb, u128 Sx, uint32_t used, int beta, int32_t H,
+__device__ __forceinline__ u128 rw_base(const Tabs& tb, const PcgJump& jb, u128 Sx, uint32_t used, int beta,
                                         int32_t& heff) {
+  const int32_t H = tb.halo;
   if (beta == 0) {
     heff = min(H, (int32_t)used + 1);
     return apply_jump(jb, jump_any(tb, Sx, used + 1u - (uint32_t)heff));
@@ -363,6 +289,7 @@ __device__ __forceinline__ void exchange(const WgParams& P, uint64_t* slots, uin
 __device__ __forceinline__ uint32_t gcnt(uint64_t g) { return (uint32_t)g & 0xFFFFFFu; }
 __device__ __forceinline__ uint32_t grej(uint64_t g) { return (uint32_t)(g >> 24) & 0xFFu; }
 
+// Per-launch view of the dynamic LDS (pointers resolved once) and the block geometry.
 #ifndef WG_NSTG
 #define WG_NSTG 3
 #endif
@@ -374,22 +301,15 @@ __device__ __forceinline__ uint32_t grej(uint64_t g) { return (uint32_t)(g >> 24
 #endif
 constexpr int NSTG = WG_NSTG;  // staging buffers: the store waves may trail the env waves by up to NSTG - 1 steps
 struct Lds {
-  uint32_t* W0;   // [2 step parities][E + 2H] window words (high halves)
+  uint64_t* RW;   // [E + 2H] window words
   uint64_t* CS0;  // [2 step parities][512][2] coarse states (lo, hi)
   char* stg0;     // [NSTG][E] staged u32 per env: cell | term << 16 | trunc << 17 | wall bump << 18
-  uint32_t* NL0;  // [2 step parities][EW][NLW] goal-adjacent envs: slot | action index << 12 | goal-action mask << 16
-  int wlen;
   __device__ __forceinline__ Lds(char* dyn, const WgParams& P, int E)
-      : W0(reinterpret_cast<uint32_t*>(dyn + P.lds.total)),
-        CS0(reinterpret_cast<uint64_t*>(dyn + P.lds.total + (size_t)2 * (E + 2 * P.halo) * 4)),
-        stg0(dyn + P.lds.total + (size_t)2 * (E + 2 * P.halo) * 4 + 2 * 512 * 16),
-        NL0(reinterpret_cast<uint32_t*>(dyn + P.lds.total + (size_t)2 * (E + 2 * P.halo) * 4 + 2 * 512 * 16 +
-                                        (size_t)NSTG * E * 4)),
-        wlen(E + 2 * P.halo) {}
-  __device__ __forceinline__ uint32_t* W(int k) const { return W0 + (size_t)(k & 1) * wlen; }
+      : RW(reinterpret_cast<uint64_t*>(dyn + P.lds.total)),
+        CS0(reinterpret_cast<uint64_t*>(dyn + P.lds.total + (size_t)(E + 2 * P.halo) * 8)),
+        stg0(dyn + P.lds.total + (size_t)(E + 2 * P.halo) * 8 + 2 * 512 * 16) {}
   __device__ __forceinline__ char* stg(int k, int E) const { return stg0 + (size_t)(k % NSTG) * E * 4; }
   __device__ __forceinline__ uint64_t* CS(int k) const { return CS0 + (size_t)(k & 1) * 1024; }
-  __device__ __forceinline__ uint32_t* NL(int k, int w) const { return NL0 + ((size_t)(k & 1) * EW + w) * NLW; }
 };
 
 // Slow path, control wave: append the rejected half-word positions of choice-stream slice sigma (u64 draws
@@ -414,13 +334,16 @@ __device__ __forceinline__ void list_slice(const WgParams& P, WgShared& sh, cons
   if (rb && n0 < (uint32_t)MAXRP) sh.rp[n0] = 0;
   if (rlo && base + ex < (uint32_t)MAXRP) sh.rp[base + ex] = pos;
   if (rhi && base + ex + (rlo ? 1u : 0u) < (uint32_t)MAXRP) sh.rp[base + ex + (rlo ? 1u : 0u)] = pos + 1u;
-  const uint32_t n1 = base + popc(mlo) + popc(mhi);
-  wave_sync_lds();
+  const uint32_t n1 = base + (uint32_t)__builtin_popcountll(mlo) + (uint32_t)__builtin_popcountll(mhi);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+  __builtin_amdgcn_wave_barrier();
   if (lane == 0) {
     if (n1 > (uint32_t)MAXRP) atomicOr(&P.ctl->err, GP_DERR_OVERFLOW);
     sh.nrp = min(n1, (uint32_t)MAXRP);
   }
-  wave_sync_lds();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
 }
 
 // The slices with rejections among the gathered granules (lane l holds blocks 4l..4l+3 of round r), ascending.
@@ -449,7 +372,8 @@ __device__ __forceinline__ uint32_t ctrl_slow(const WgParams& P, WgShared& sh, c
                                               uint32_t h, uint32_t u, uint32_t b, uint32_t ts, const uint64_t (&g0)[4]) {
   const int lane = threadIdx.x & 63, G = (int)gridDim.x, beta = (int)blockIdx.x;
   if (lane == 0) sh.nrp = 0;
-  wave_sync_lds();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+  __builtin_amdgcn_wave_barrier();
   uint32_t rtot = list_flagged(P, sh, tb, CS, g0, 0u, Sy, h, u);
   // coverage rounds: slices sigma = r G + beta of the half-words beyond the first 124 G
   uint32_t covered = 124u * (uint32_t)G;
@@ -479,58 +403,16 @@ __device__ __forceinline__ uint32_t ctrl_slow(const WgParams& P, WgShared& sh, c
   return wtot;
 }
 
-// Fill a window (high halves): word j = m * 512 + lg is the base state advanced by j (this lane: jump by lg, then
-// two interleaved chains of 1024-draw jumps).
-__device__ __forceinline__ void fill_window(uint32_t* RW, const PcgJump& jl, const PcgJump& j512, const PcgJump& j1024,
-                                            int nw, u128 base, int lg) {
-  u128 a = apply_jump(jl, base);
-  u128 c = apply_jump(j512, a);
-  int m = 0;
-  for (; m + 1 < nw; m += 2) {
-    RW[m * 512 + lg] = hi32(pcg_output(a));
-    RW[(m + 1) * 512 + lg] = hi32(pcg_output(c));
-    if (m + 2 < nw) {
-      a = apply_jump(j1024, a);
-      c = apply_jump(j1024, c);
-    }
-  }
-  if (m < nw) RW[m * 512 + lg] = hi32(pcg_output(a));
-}
-
 // ------------------------------------------------------------------ the control wave ----
-// Step k's resetters (cb <= CB_CTRL, no rejection): rank q takes half-word R + q; its cell (| goal-action mask)
-// goes to rc[q], where the env waves take it by rank.
-__device__ __forceinline__ void ctrl_place(const WgParams& P, WgShared& sh, const Tabs& tb, const uint64_t* CS,
-                                           uint32_t cb, uint32_t R, uint32_t cbase, uint32_t h, uint32_t u) {
-  const int lane = threadIdx.x & 63;
-  const uint32_t nag = (uint32_t)P.n_agent;
-  const bool nocand = P.tmode & TM_NOCAND;
-  for (uint32_t q = (uint32_t)lane; q < cb; q += 64u) {
-    const uint32_t hw = R + q;
-    uint32_t v;
-    if (hw - cbase < (uint32_t)NCAND && !nocand) {  // (hw >= cbase >= h: never the buffered half)
-      v = sh.cand[hw - cbase];
-    } else {
-      uint32_t word;
-      if (h && hw == 0) {
-        word = u;
-      } else {
-        const uint32_t hh = hw - h;
-        const uint64_t x = pcg_output(draw_state(tb, CS, hh >> 1));
-        word = (hh & 1u) ? (uint32_t)(x >> 32) : (uint32_t)x;
-      }
-      v = tb.avalid(lemire_value(word, nag));
-    }
-    sh.rc[q] = v;
-  }
-}
-
-// Per step: S(y) and the next window's base around the predicted used (sy_ready); the block's done count from the
-// env waves, granule published; the ranks; the candidate cells while the granules travel; the all-gather; the
-// resetters' cells, the next window's offset, S(x_{t+1}) (cells_done); the next step's rejection-check slice.
+// Per step: S(x) published (sx_ready: the env waves' coarse states), the rejection check of its slice, the block's
+// reset count once the env waves' transitions are in, the granule published, S(y) and the next window's base
+// (sy_ready), the all-gather, the resetters' cells (cells_done), then the next step's S(x) = J_used(S(y)). Every
+// constant part of a jump (random(B), the block and lane offsets) is folded into per-lane / per-block tables, so
+// the chain from one exchange to the next publish is two table jumps and one per-lane jump.
 template <int NS, int NA>
 __device__ __forceinline__ void wg_ctrl(const WgParams& P, WgShared& sh, const Tabs& tb, const Lds& L, int K) {
   const int lane = threadIdx.x & 63, beta = (int)blockIdx.x, G = (int)gridDim.x;
+  constexpr int E = NS * 512;
   GridCtl* C = P.ctl;
   u128 Sx = mk128(C->s_hi, C->s_lo);
   uint32_t h = C->has_u32, u = C->uinteger;
@@ -543,91 +425,76 @@ __device__ __forceinline__ void wg_ctrl(const WgParams& P, WgShared& sh, const T
   const uint32_t nag = (uint32_t)P.n_agent, thra = P.thr_agent;
   const int32_t H = P.halo;
   const uint32_t bias = (uint32_t)P.wg_bias;
-  const int tmode = P.tmode;
   uint32_t* derr = &C->err;
-  // Lemire check of a block's slice of the choice() stream (u64 draws 62 beta + 1 .. + 62 after random(B))
-  auto rej_check = [&](u128 S, uint32_t hh, uint32_t uu) -> uint32_t {
-    uint32_t rj = 0;
-    if (lane < SLICE) {
-      const uint64_t x = pcg_output(apply_jump(jr, S));
-      rj = (lemire_rejected((uint32_t)x, nag, thra) ? 1u : 0u) + (lemire_rejected((uint32_t)(x >> 32), nag, thra) ? 1u : 0u);
-    } else if (lane == SLICE && beta == 0 && hh) {
-      rj = lemire_rejected(uu, nag, thra) ? 1u : 0u;  // the buffered half is hw 0
-    }
-    return wave_sum(rj);
-  };
-  uint32_t rejc = rej_check(Sx, h, u);
   lds_barrier();  // P1: tables staged, counters zeroed
-  if (lane == 0) {  // the first window: step 0's own random(B) words, exact: word 0 is S(x_0 + 1 + E beta - heff)
+  // the first window: step 0's own random(B) words, exact: word 0 is S(x_0 + 1 + E beta - heff)
+  if (lane == 0) {
     const u128 s = apply_jump(jpro, Sx);
     sh.rw[0][0] = hi64(s);
     sh.rw[0][1] = lo64(s);
     sh.rw_off[0] = beta == 0 ? 1 : H;
-    sh.sx[0][0] = hi64(Sx);
-    sh.sx[0][1] = lo64(Sx);
     lds_release();
-    lds_set(&sh.pro, 1u);
+    __hip_atomic_store(&sh.pro, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   LSTAMP(P, 1);
   for (int k = 0; k < K; ++k) {
     const uint32_t ts = ts0 + (uint32_t)k;
-    // ---- S(y) and the next step's window base around the used predicted from the last b (the window's buffer and
-    // base slot are free once every env wave's transitions of step k - 1 are done) ----
-    lds_wait(&sh.trans_done, (uint32_t)EW * (uint32_t)k, derr);
+    if (lane == 0) {
+      sh.sx[k & 1][0] = hi64(Sx);
+      sh.sx[k & 1][1] = lo64(Sx);
+      lds_release();
+      __hip_atomic_store(&sh.sx_ready, (uint32_t)k + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    // Lemire check of this block's slice of the choice() stream (u64 draws 62 beta + 1 .. + 62 after random(B))
+    uint32_t rj = 0;
+    if (lane < SLICE) {
+      const uint64_t x = pcg_output(apply_jump(jr, Sx));
+      rj = (lemire_rejected((uint32_t)x, nag, thra) ? 1u : 0u) + (lemire_rejected((uint32_t)(x >> 32), nag, thra) ? 1u : 0u);
+    } else if (lane == SLICE && beta == 0 && h) {
+      rj = lemire_rejected(u, nag, thra) ? 1u : 0u;  // the buffered half is hw 0
+    }
+    const uint32_t rejc = wave_sum(rj);
+    WSTAMP(P, k, 6);
+    // this block's reset count, published
+    lds_wait(&sh.trans_done, (uint32_t)EW * (uint32_t)(k + 1), derr);
+    WSTAMP(P, k, 7);
+    const uint32_t cb = wave_sum(lane < NS * EW ? (uint32_t)__builtin_popcountll(sh.mask[lane >> 3][lane & 7]) : 0u);
+    uint64_t* slots = P.slots + (size_t)(ts & 1u) * 2 * G;
+    publish(P, slots, ts << 6, rejc, cb);
+    WSTAMP(P, k, 8);
+    // while the granules travel: S(y) and the next step's window, around the used predicted from the last b
     const u128 Sy = apply_jump(jB, Sx);
     uint32_t used_p, hp;
     words_to_draws(bprev + bias, h, used_p, hp);
     int32_t heff_p;
-    const u128 Srw = rw_base(tb, jb, Sx, used_p, beta, H, heff_p);
+    const u128 Srw = rw_base(tb, jb, Sx, used_p, beta, heff_p);
     if (lane == 0) {
       sh.sy[k & 1][0] = hi64(Sy);
       sh.sy[k & 1][1] = lo64(Sy);
-      if (k + 1 < K) {
-        sh.rw[(k + 1) & 1][0] = hi64(Srw);
-        sh.rw[(k + 1) & 1][1] = lo64(Srw);
-      }
+      sh.rw[(k + 1) & 1][0] = hi64(Srw);
+      sh.rw[(k + 1) & 1][1] = lo64(Srw);
       lds_release();
-      lds_set(&sh.sy_ready, (uint32_t)k + 1u);
+      __hip_atomic_store(&sh.sy_ready, (uint32_t)k + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    WSTAMP(P, k, 7);
-    // ---- the block's done count (early) ----
-    lds_wait(&sh.cnt_done, (uint32_t)EW * (uint32_t)(k + 1), derr);
-    WSTAMP(P, k, 5);
-    const uint32_t cnt = lds_load(&sh.cnt[k & 1]);
-    uint64_t* slots = P.slots + (size_t)(ts & 1u) * 2 * G;
-    publish(P, slots, ts << 6, rejc, cnt);
-    WSTAMP(P, k, 6);
-    // ---- while the granules travel: the ranks (resetters before each 64-env word of the done bitmap) ----
-    {
-      const uint64_t wd = lane < NS * EW ? sh.dmask[k & 1][lane] : 0ull;
-      const uint32_t c = popc(wd);
-      const uint32_t incl = wave_incl_scan(c);
-      if (lane < NS * EW) sh.pre[k & 1][lane] = incl - c;
-      if (lane == 0) {
-        lds_set(&sh.cnt[k & 1], 0u);  // (this parity's next adds come with step k + 2)
-        if (__builtin_amdgcn_readlane((int)incl, 63) != (int)cnt) atomicOr(derr, GP_DERR_LOGIC);
-      }
-    }
-    // the cells of the choice() half-words around the block prefix predicted by the last step's (at a priority below
-    // the env waves': not urgent), so that the resetters' cells after the exchange are one LDS read each. Candidate i
-    // is half-word cbase + i; cbase = 2 d0 + h.
-    if (!(tmode & TM_CTRLHIGH)) __builtin_amdgcn_s_setprio(1);
+    // While the granules travel (the longest wait of a step): the cells of the choice() half-words around the block
+    // prefix predicted by the last step's, so that the resetters' cells after the exchange are one LDS read each.
+    // Candidate i is half-word cbase + i; cbase = 2 d0 + h, draws d0 .. d0 + NCAND / 2 - 1 (both halves each).
     const uint64_t* CS = L.CS(k);
     lds_wait(&sh.cs_done, (uint32_t)EW * (uint32_t)(k + 1), derr);
     const uint32_t d0 = min(Rprev > CAND_W + h ? (Rprev - CAND_W - h) >> 1 : 0u, 16384u - NCAND / 2);  // CS reach
     const uint32_t cbase = 2u * d0 + h;
-    if (!(tmode & TM_NOCAND)) {
+    if (!(P.tmode & TM_NOCAND)) {
 #pragma unroll
       for (int m = 0; m < NCAND / 128; ++m) {
         const uint32_t j = (uint32_t)(lane + 64 * m);
         const uint64_t x = pcg_output(draw_state(tb, CS, d0 + j));
-        sh.cand[2 * j] = tb.avalid(lemire_value((uint32_t)x, nag));
-        sh.cand[2 * j + 1] = tb.avalid(lemire_value((uint32_t)(x >> 32), nag));
+        sh.cand[2 * j] = (uint16_t)tb.avalid(lemire_value((uint32_t)x, nag));
+        sh.cand[2 * j + 1] = (uint16_t)tb.avalid(lemire_value((uint32_t)(x >> 32), nag));
       }
     }
-    wave_sync_lds();
-    __builtin_amdgcn_s_setprio(3);
-    WSTAMP(P, k, 8);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
     uint64_t g[4];
     gather(P, slots, ts << 6, g);
     WSTAMP(P, k, 9);
@@ -644,31 +511,48 @@ __device__ __forceinline__ void wg_ctrl(const WgParams& P, WgShared& sh, const T
     }
     const uint32_t rtot = wave_sum(grej(g[0]) + grej(g[1]) + grej(g[2]) + grej(g[3]));
     const bool slow = rtot != 0 || b > 124u * (uint32_t)G;
-    // ---- the step's resetters ----
     uint32_t used, h2;
+    // (also before cells_done when nothing is drawn: every env wave has read this step's masks)
+    lds_wait(&sh.r2s_done, (uint32_t)EW * (uint32_t)(k + 1), derr);
     if (!slow) {
       words_to_draws(b, h, used, h2);
+      if (cb) {  // this block's resetters' cells: rank q takes half-word R + q
+        uint16_t* st = reinterpret_cast<uint16_t*>(L.stg(k, E));
+        for (uint32_t q = (uint32_t)lane; q < cb; q += 64u) {
+          const uint32_t hw = R + q;
+          const uint32_t slot = sh.r2s[q];
+          uint32_t cell;
+          if (hw - cbase < (uint32_t)NCAND && !(P.tmode & TM_NOCAND)) {  // (hw >= cbase >= h: never the buffered half)
+            cell = sh.cand[hw - cbase];
+          } else {
+            uint32_t word;
+            if (h && hw == 0) {
+              word = u;
+            } else {
+              const uint32_t hh = hw - h;
+              const uint64_t x = pcg_output(draw_state(tb, CS, hh >> 1));
+              word = (hh & 1u) ? (uint32_t)(x >> 32) : (uint32_t)x;
+            }
+            cell = tb.avalid(lemire_value(word, nag));
+          }
+          st[2 * slot] = (uint16_t)cell;  // the low half of the staged word
+        }
+      }
     } else {
       const uint32_t wtot = ctrl_slow(P, sh, tb, CS, Sy, h, u, b, ts, g);
       words_to_draws(wtot, h, used, h2);
-    }
-    const bool eplace = slow || cnt > CB_CTRL || (tmode & TM_ENVPLACE);
-    if (eplace) {
       if (lane == 0) {
         sh.R = R;
         sh.h = h;
         sh.u = u;
-        if (!slow) sh.nrp = 0;
       }
-    } else if (cnt) {
-      ctrl_place(P, sh, tb, CS, cnt, R, cbase, h, u);
     }
     // the next step's window offset; a window more than H off is regenerated exactly by the env waves
     int32_t off = heff_p + (int32_t)used - (int32_t)used_p;
-    uint32_t fix = eplace ? 1u : 0u;
+    uint32_t fix = slow ? 1u : 0u;
     if (k + 1 < K && (off < 0 || off > 2 * H)) {
       int32_t heff;
-      const u128 s = rw_base(tb, jb, Sx, used, beta, H, heff);
+      const u128 s = rw_base(tb, jb, Sx, used, beta, heff);
       off = heff;
       fix |= 2u;
       if (lane == 0) {
@@ -676,23 +560,20 @@ __device__ __forceinline__ void wg_ctrl(const WgParams& P, WgShared& sh, const T
         sh.rw[(k + 1) & 1][1] = lo64(s);
       }
     }
-    const u128 Sxn = jump_any(tb, Sy, used);  // S(x_{t+1}) = S(y_t + used)
     if (lane == 0) {
-      sh.sx[(k + 1) & 1][0] = hi64(Sxn);
-      sh.sx[(k + 1) & 1][1] = lo64(Sxn);
       sh.rw_off[(k + 1) & 1] = off;
-      sh.fix[(k + 1) & 1] = fix;
+      sh.fix[k & 1] = fix;
       lds_release();
-      lds_set(&sh.cells_done, (uint32_t)k + 1u);
+      __hip_atomic_store(&sh.cells_done, (uint32_t)k + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     WSTAMP(P, k, 10);
-    Sx = Sxn;
+    // the next step's state S(x_{t+1}) = S(y_t + used)
+    Sx = jump_any(tb, Sy, used);
     if (used) u = (uint32_t)(pcg_output(Sx) >> 32);  // numpy keeps the last drawn high half in uinteger
     h = h2;
     bprev = b;
     Rprev = R;
-    if (k + 1 < K) rejc = rej_check(Sx, h, u);
-    WSTAMP(P, k, 11);
+    WSTAMP(P, k, 12);
   }
   LSTAMP(P, 3);
   if (beta == 0 && lane == 0) {
@@ -711,87 +592,45 @@ struct Acc {
   uint32_t eps = 0, ngoal = 0, nwall = 0, lens = 0;
 };
 
-// Append this wave's goal-adjacent envs (bit s of nrm: entry ent[s]) to its list of a step at position n (uniform);
-// returns the new length (entries past NLW are counted, not written: the wave then counts from its masks).
+// Slow path: place this lane's resetters exactly (ranks -> positions past the listed rejections -> words).
 template <int NS>
-__device__ __forceinline__ uint32_t append_near(uint32_t* NLw, uint32_t n, uint32_t nrm, const uint32_t (&ent)[NS]) {
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    const uint64_t m = ballot((nrm >> s) & 1u);
-    const uint32_t i = n + mbcnt(m);
-    if (((nrm >> s) & 1u) && i < (uint32_t)NLW) NLw[i] = ent[s];
-    n += popc(m);
-  }
-  return n;
-}
-
-// The previous step's (kp's) resetters, by their block rank (the control wave's ranks of step kp + the slot's rank in
-// its 64-env word): the cell the control wave placed, or one placed here exactly (rank -> position past the listed
-// rejections -> word); the goal-adjacent ones appended to this wave's list of step kp + 1 when `list_next` (ai: the
-// actions of step kp + 1). Returns the list's new length.
-template <int NS, int NA>
-__device__ __forceinline__ uint32_t env_take(const WgParams& P, WgShared& sh, const Tabs& tb, const Lds& L, int kp,
-                                             bool eplace, bool list_next, uint32_t nl, uint32_t dn,
-                                             const uint64_t (&bm)[NS], const uint32_t (&ai)[NS], uint32_t (&ae)[NS]) {
-  constexpr int E = NS * 512;
-  const int lg = threadIdx.x, w = lg >> 6;
-  uint16_t* st = reinterpret_cast<uint16_t*>(L.stg(kp, E));
-  const u128 Sy = mk128(sh.sy[kp & 1][0], sh.sy[kp & 1][1]);
-  const uint64_t* CS = L.CS(kp);
+__device__ __forceinline__ void wg_env_slow(const WgParams& P, WgShared& sh, const Tabs& tb, const uint64_t* CS,
+                                            int k, char* stg, uint32_t dn, const uint32_t (&pre)[NS],
+                                            const uint64_t (&bm)[NS], uint32_t (&ae)[NS]) {
+  const int lg = threadIdx.x;
+  const u128 Sy = mk128(sh.sy[k & 1][0], sh.sy[k & 1][1]);
   const uint32_t R = sh.R, h = sh.h, u = sh.u, n = sh.nrp;
-  uint32_t nrm = 0, ent[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
-    ent[s] = 0;
     if (!((dn >> s) & 1u)) continue;
-    const uint32_t q = sh.pre[kp & 1][s * EW + w] + mbcnt(bm[s]);
-    uint32_t v;
-    if (!eplace) {
-      v = sh.rc[q];
+    uint32_t p = R + pre[s] + mbcnt(bm[s]);
+    for (uint32_t q = 0; q < n; ++q) p += sh.rp[q] <= p ? 1u : 0u;
+    uint32_t word;
+    if (h && p == 0) {
+      word = u;
     } else {
-      uint32_t p = R + q;
-      for (uint32_t r = 0; r < n; ++r) p += sh.rp[r] <= p ? 1u : 0u;
-      uint32_t word;
-      if (h && p == 0) {
-        word = u;
-      } else {
-        const uint32_t hh = p - h, d = hh >> 1;
-        const u128 s2 = d < 16384u ? draw_state(tb, CS, d) : pcg_jump(tb.jt64, Sy, d + 1u);
-        const uint64_t x = pcg_output(s2);
-        word = (hh & 1u) ? (uint32_t)(x >> 32) : (uint32_t)x;
-      }
-      v = tb.avalid(lemire_value(word, (uint32_t)P.n_agent));
+      const uint32_t hh = p - h, d = hh >> 1;
+      const u128 st = d < 16384u ? draw_state(tb, CS, d) : pcg_jump(tb.jt64, Sy, d + 1u);
+      const uint64_t x = pcg_output(st);
+      word = (hh & 1u) ? (uint32_t)(x >> 32) : (uint32_t)x;
     }
-    st[2 * (s * 512 + lg)] = (uint16_t)v;
-    ae[s] = v & 0xFFFFu;
-    nrm |= (list_next && (v >> 16) != 0u) ? (1u << s) : 0u;
-    ent[s] = (uint32_t)(s * 512 + lg) | (ai[s] << 12) | ((v >> 16) << 16);
+    const uint32_t cell = tb.avalid(lemire_value(word, (uint32_t)P.n_agent));
+    reinterpret_cast<uint16_t*>(stg)[2 * (s * 512 + lg)] = (uint16_t)cell;
+    ae[s] = cell;
   }
-  return list_next ? append_near<NS>(L.NL(kp + 1, w), nl, nrm, ent) : nl;
 }
 
-// The early count of step k for this wave: its listed goal-adjacent envs' window words (one entry per lane), each
-// goal hit OR-ed into the step's done bitmap; returns the wave's done count (its 64-env words' popcounts).
-template <int NS, int NA>
-__device__ __forceinline__ uint32_t env_resolve(WgShared& sh, const Tabs& tb, const Lds& L, int k, uint32_t nl,
-                                                bool exactw) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  uint64_t* dm = sh.dmask[k & 1];
-  if (lane < (int)nl) {
-    const uint32_t e = L.NL(k, w)[lane];
-    const uint32_t slot = e & 0xFFFu, j = slot + (uint32_t)sh.rw_off[k & 1];
-    bool tie;
-    uint32_t f = eff_hi<NA>(tb, L.W(k)[j], (e >> 12) & 7u, tie);
-    if (tie || exactw) f = eff_full<NA>(tb, window_word(tb, sh.rw[k & 1], j), (e >> 12) & 7u);
-    if ((e >> (16 + f)) & 1u)
-      __hip_atomic_fetch_or(&dm[slot >> 6], 1ull << (slot & 63u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+// Fill the window: word j = m * 512 + lg is the base state advanced by j (this lane: jump by lg, then by 512).
+__device__ __forceinline__ void fill_window(uint64_t* RW, const PcgJump& jl, const PcgJump& j512, int nw, u128 base, int lg) {
+  u128 s = apply_jump(jl, base);
+  for (int m = 0; m < nw; ++m) {
+    RW[m * 512 + lg] = pcg_output(s);
+    s = apply_jump(j512, s);
   }
-  wave_sync_lds();
-  return wave_sum(lane < NS ? popc(dm[lane * EW + w]) : 0u);
 }
 
 template <int NS, int NA>
-__device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Tabs& tb, const Lds& L,
+__device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Tabs& tb, const Lds& L, const char* dyn,
                                        const int32_t* __restrict__ act, int K, Acc& acc, int32_t* __restrict__ obs,
                                        float* __restrict__ rew, uint8_t* __restrict__ term,
                                        uint8_t* __restrict__ trunc) {
@@ -800,214 +639,175 @@ __device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Ta
   constexpr int E = NS * 512;
   const size_t B = (size_t)E * (size_t)G;
   const size_t e0 = (size_t)beta * E;
+  const char* thr = dyn + P.lds.thr;
+  const char* mv = dyn + P.lds.move;
   const uint32_t goal = (uint32_t)P.goal, tlim = (uint32_t)P.time_limit;
   uint32_t* derr = &P.ctl->err;
   uint32_t* aeg = P.ae;
   const int nw = P.rw_words;
   const int tmode = P.tmode;
-  const bool exactw = tmode & TM_EXACTW;
-  const PcgJump j512 = P.j512, j1024 = P.j1024;
-  // per-lane constant jumps: by lg (window fill) and by B + 32 lg + 1 (coarse state)
+  const PcgJump j512 = P.j512;
+  // per-lane constant jumps: by lg (window fill) and by 32 lg + 1 (coarse state)
   const PcgJump jrw = P.jlane[2 * lg], jcs = P.jlane[2 * lg + 1];
-  uint32_t ae[NS], ai[NS], an[NS];  // env state; action index of this step, of the next step
-  int32_t a2[NS];                   // raw actions two steps ahead (loads in flight)
+  uint32_t ae[NS];
+  int32_t arow[NS], anext[NS];
 #pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    ae[s] = aeg[e0 + (size_t)s * 512 + lg];
-    a2[s] = act[e0 + (size_t)s * 512 + lg];
-    an[s] = K > 1 ? (uint32_t)act[B + e0 + (size_t)s * 512 + lg] : 0u;
+  for (int k = 0; k < NS; ++k) {
+    ae[k] = aeg[e0 + (size_t)k * 512 + lg];
+    anext[k] = act[e0 + (size_t)k * 512 + lg];
   }
   // the first window, exact (word 0 = S(x_0 + 1 + E beta - heff)), filled from global data while the other waves
-  // stage the tables
+  // stage the tables (it lies behind them in LDS)
   {
     const GridCtl* C = P.ctl;
-    fill_window(L.W(0), jrw, j512, j1024, nw, apply_jump(P.jblk[2 * beta + 1], mk128(C->s_hi, C->s_lo)), lg);
+    fill_window(L.RW, jrw, j512, nw, apply_jump(P.jblk[2 * beta + 1], mk128(C->s_hi, C->s_lo)), lg);
   }
   lds_barrier();  // P1
 #pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    ai[s] = action_index<NA>(a2[s], derr);
-    an[s] = K > 1 ? action_index<NA>((int32_t)an[s], derr) : 0u;
-    acc.lens += ae[s] >> 16;  // episode lengths: + elapsed at the start - elapsed at the end + steps
+  for (int k = 0; k < NS; ++k) {
+    arow[k] = action_row<NA>(anext[k], derr);
+    acc.lens += ae[k] >> 16;  // episode lengths: + elapsed at the start - elapsed at the end + steps
   }
-  uint32_t nl;  // this wave's goal-adjacent envs listed for the current step
-  {  // step 0's truncations (into its done bitmap) and goal-adjacent envs
-    uint32_t nrm = 0, trm = 0, ent[NS];
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const uint32_t c = ae[s] & 0xFFFFu, el = (ae[s] >> 16) + 1u;
-      const uint32_t tr = el > tlim ? 1u : 0u;
-      const uint32_t gm = tb.gmp[c];
-      trm |= tr << s;
-      nrm |= (!tr && gm != 0u) ? (1u << s) : 0u;
-      ent[s] = (uint32_t)(s * 512 + lg) | (ai[s] << 12) | (gm << 16);
-    }
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const uint64_t m = ballot((trm >> s) & 1u);
-      if (lane == 0) sh.dmask[0][s * EW + w] = m;
-    }
-    nl = append_near<NS>(L.NL(0, w), 0u, nrm, ent);
-  }
-  lds_release();
-  lds_wait(&sh.pro, 1u, derr);  // the first window's offset, S(x_0)
+  lds_wait(&sh.pro, 1u, derr);  // the first window's offset
   if (lane == 0) lds_add(&sh.fill_done, 1u);
   uint32_t fill_target = EW;
   uint64_t bm[NS];
-  uint32_t dn = 0;
+  uint32_t pre[NS];
   for (int k = 0; k < K; ++k) {
     char* stg = L.stg(k, E);
-    if (k > 0) {  // the previous step's exchange is done: its resetters' cells, this step's window offset
-      lds_wait(&sh.cells_done, (uint32_t)k, derr);
-      if (w == 0) WSTAMP(P, k, 16);
-      const uint32_t fix = sh.fix[k & 1];
-      nl = env_take<NS, NA>(P, sh, tb, L, k - 1, fix & 1u, tlim >= 1u, nl, dn, bm, ai, ae);
-      if (tlim == 0 && lane == 0) {  // every resetter of step k - 1 truncates at step k
+    if (k + 1 < K && !(tmode & TM_LATEACT)) {
 #pragma unroll
-        for (int s = 0; s < NS; ++s) sh.dmask[k & 1][s * EW + w] |= bm[s];
-      }
-      lds_release();
-      if (lane == 0) lds_add(&sh.res_done, 1u);
-      if (fix & 2u) {  // the prediction missed the window: regenerate it exactly
-        fill_window(L.W(k), jrw, j512, j1024, nw, mk128(sh.rw[k & 1][0], sh.rw[k & 1][1]), lg);
-        lds_release();
-        if (lane == 0) lds_add(&sh.fill_done, 1u);
-        fill_target += EW;
-      }
+      for (int s = 0; s < NS; ++s) anext[s] = act[(size_t)(k + 1) * B + e0 + (size_t)s * 512 + lg];
     }
+    lds_wait(&sh.fill_done, fill_target, derr);                  // every env wave's part of this step's window
+    if (k >= NSTG) lds_wait(&sh.st_done, (uint32_t)SW * (uint32_t)(k - NSTG + 1), derr);  // this staging buffer copied out
+    if (!(tmode & TM_NOPRIO)) __builtin_amdgcn_s_setprio(2);  // the transitions are on the critical path
     if (w == 0) WSTAMP(P, k, 0);
-    {  // this step's coarse states: S(x + B + 32 lg + 1)
-      const u128 cs = apply_jump(jcs, mk128(sh.sx[k & 1][0], sh.sx[k & 1][1]));
+    // ---- transitions (the critical path) ----
+    // Phased over the env slots so that their LDS round trips overlap: every slot's window word and threshold
+    // row first, then the effective actions, the move-table entries, and the staged outputs last (a store to
+    // the staging area between two slots' loads would order them: all of it is one LDS array to the compiler).
+    const int32_t off = sh.rw_off[k & 1];
+    uint32_t dn = 0;
+    uint32_t mvo[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const uint64_t x = L.RW[s * 512 + lg + off];
+      const char* t = thr + arow[s];
+      uint32_t eb = 0;  // 2 x effective action: #{j : x > thr[a][j]} (integer form of action_utils.py:84-90)
+#pragma unroll
+      for (int j = 0; j + 1 < NA; j += 2) {
+        const ulonglong2 tt = *reinterpret_cast<const ulonglong2*>(t + 8 * j);
+        eb = x > tt.x ? (uint32_t)(2 * (j + 1)) : eb;
+        if (j + 2 < NA) eb = x > tt.y ? (uint32_t)(2 * (j + 2)) : eb;
+      }
+      mvo[s] = (ae[s] & 0xFFFFu) * (2 * NA) + eb;
+    }
+    uint32_t mm[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) mm[s] = *reinterpret_cast<const uint16_t*>(mv + mvo[s]);
+    uint32_t sv[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const uint32_t m = mm[s];
+      const uint32_t nc = m & 0x7FFFu, blocked = m >> 15;
+      const uint32_t el = (ae[s] >> 16) + 1u;
+      const bool term = nc == goal, trunc = el > tlim, done = term || trunc;
+      sv[s] = nc | ((uint32_t)term << 16) | ((uint32_t)trunc << 17) | (blocked << 18);
+      ae[s] = done ? nc : (nc | (el << 16));
+      bm[s] = ballot(done);
+      dn |= (uint32_t)done << s;
+      acc.ngoal += term ? 1u : 0u;
+      acc.nwall += (blocked && !term) ? 1u : 0u;
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s) sh.mask[s][w] = bm[s];
+    }
+#pragma unroll
+    for (int s = 0; s < NS; ++s) reinterpret_cast<uint32_t*>(stg)[s * 512 + lg] = sv[s];
+    acc.eps += (uint32_t)__builtin_popcount(dn);
+    lds_release();
+    if (lane == 0) lds_add(&sh.trans_done, 1u);
+    if (!(tmode & TM_NOPRIO) && !(tmode & TM_ENVHIGH)) __builtin_amdgcn_s_setprio(0);
+    if (w == 0) WSTAMP(P, k, 1);
+    // the next step's actions (one step ahead)
+    if (k + 1 < K && (tmode & TM_LATEACT)) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s) anext[s] = act[(size_t)(k + 1) * B + e0 + (size_t)s * 512 + lg];
+    }
+    // ---- while the exchange runs: coarse states, resetter listing, the next step's window ----
+    lds_wait(&sh.sx_ready, (uint32_t)k + 1u, derr);
+    if (w == 0) WSTAMP(P, k, 2);
+    {
+      const u128 cs = apply_jump(jcs, mk128(sh.sx[k & 1][0], sh.sx[k & 1][1]));  // S(x + B + 32 lg + 1)
       reinterpret_cast<ulonglong2*>(L.CS(k))[lg] = ulonglong2{lo64(cs), hi64(cs)};
     }
     lds_release();
     if (lane == 0) lds_add(&sh.cs_done, 1u);
-    if (!(tmode & TM_NOPRIO)) __builtin_amdgcn_s_setprio(2);
-    lds_wait(&sh.fill_done, fill_target, derr);  // every env wave's part of this step's window
-    if (w == 0) WSTAMP(P, k, 12);
-    // ---- the early count: this wave's done envs of the step ----
-    const bool early = nl <= (uint32_t)NLW && !(tmode & TM_LATE);
-    if (early) {
-      const uint32_t c = env_resolve<NS, NA>(sh, tb, L, k, nl, exactw);
-      if (lane == 0) lds_add(&sh.cnt[k & 1], c);
-      lds_release();
-      if (lane == 0) lds_add(&sh.cnt_done, 1u);
-    }
-    if (w == 0) WSTAMP(P, k, 1);
-    // ---- the next step's window (its base is published once every wave's transitions of step k - 1 are done) ----
-    auto fill_next = [&]() {
-      if (k + 1 < K) {
-        lds_wait(&sh.sy_ready, (uint32_t)k + 1u, derr);
-        const u128 Srw = mk128(sh.rw[(k + 1) & 1][0], sh.rw[(k + 1) & 1][1]);
-        if (!(tmode & TM_NOFILL)) fill_window(L.W(k + 1), jrw, j512, j1024, nw, Srw, lg);
-        lds_release();
-        if (lane == 0) lds_add(&sh.fill_done, 1u);
-        fill_target += EW;
-      }
-    };
-    if (!(tmode & TM_TRANSFIRST)) fill_next();
     if (w == 0) WSTAMP(P, k, 3);
-    // the actions two steps ahead
-    if (k + 2 < K) {
-#pragma unroll
-      for (int s = 0; s < NS; ++s) a2[s] = act[(size_t)(k + 2) * B + e0 + (size_t)s * 512 + lg];
-    }
-    if (k >= NSTG) lds_wait(&sh.st_done, (uint32_t)SW * (uint32_t)(k - NSTG + 1), derr);  // staging buffer copied out
-    // ---- the full transitions (off the exchange's chain: the early count is already in) ----
-    const int32_t off = sh.rw_off[k & 1];
-    const uint32_t* Wk = L.W(k);
-    uint32_t fe[NS], tie = 0;
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      bool t;
-      fe[s] = eff_hi<NA>(tb, Wk[s * 512 + lg + off], ai[s], t);
-      tie |= (t || exactw) ? (1u << s) : 0u;
-    }
-    if (tie) {  // a word whose high half equals a threshold's (p ~ 2^-32 per compare): its full draw decides
-#pragma unroll
-      for (int s = 0; s < NS; ++s)
-        if ((tie >> s) & 1u) fe[s] = eff_full<NA>(tb, window_word(tb, sh.rw[k & 1], (uint32_t)(s * 512 + lg + off)), ai[s]);
-    }
-    uint32_t mm[NS];
-#pragma unroll
-    for (int s = 0; s < NS; ++s) mm[s] = tb.mvp[(ae[s] & 0xFFFFu) * NA + fe[s]];
-    // Per-slot outcomes as bits of VGPR words (bit s), not as live lane masks: eight slots' worth of 64-bit masks
-    // would not fit the SGPRs and spill through v_writelane / v_readlane.
-    uint32_t sv[NS], ent[NS], trm = 0, nrm = 0;
-    dn = 0;
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const uint32_t m = mm[s];
-      const uint32_t nc = m & 0x7FFFu, blocked = (m >> 15) & 1u, gmn = m >> 16;
-      const uint32_t el = (ae[s] >> 16) + 1u;
-      const uint32_t term = nc == goal ? 1u : 0u, trunc = el > tlim ? 1u : 0u, done = term | trunc;
-      sv[s] = nc | (term << 16) | (trunc << 17) | (blocked << 18);
-      ae[s] = done ? nc : (nc | (el << 16));
-      dn |= done << s;
-      acc.ngoal += term;
-      acc.nwall += blocked & (term ^ 1u);
-      // the next step: truncated for sure, or goal-adjacent (its word decides); resetters are listed at the take
-      const uint32_t tr1 = (done ^ 1u) & (el + 1u > tlim ? 1u : 0u);
-      trm |= tr1 << s;
-      nrm |= ((done | tr1) ^ 1u) & (gmn != 0u ? 1u : 0u) ? (1u << s) : 0u;
-      ent[s] = (uint32_t)(s * 512 + lg) | (an[s] << 12) | (gmn << 16);
-    }
-#pragma unroll
-    for (int s = 0; s < NS; ++s) reinterpret_cast<uint32_t*>(stg)[s * 512 + lg] = sv[s];
-    bool bad = false;
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      bm[s] = ballot((dn >> s) & 1u);
-      const uint64_t mt = ballot((trm >> s) & 1u);
-      if (early) bad |= sh.dmask[k & 1][s * EW + w] != bm[s];  // the early count's bits == the step's outcome
-      if (lane == 0 && k + 1 < K) sh.dmask[(k + 1) & 1][s * EW + w] = mt;
-    }
-    if (bad && lane == 0) atomicOr(derr, GP_DERR_LOGIC);
-    if (!early) {  // counted from the masks: this wave's part of the step's done bitmap and count
-      uint32_t c = 0;
+    lds_wait(&sh.trans_done, (uint32_t)EW * (uint32_t)(k + 1), derr);  // every wave's masks; nobody reads the window now
+    {
+      const uint32_t c = lane < NS * EW ? (uint32_t)__builtin_popcountll(sh.mask[lane >> 3][lane & 7]) : 0u;
+      const uint32_t ex = wave_incl_scan(c) - c;
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
-        c += popc(bm[s]);
-        if (lane == 0) sh.dmask[k & 1][s * EW + w] = bm[s];
+        pre[s] = (uint32_t)__builtin_amdgcn_readlane((int)ex, s * EW + w);
+        if ((dn >> s) & 1u) sh.r2s[pre[s] + mbcnt(bm[s])] = (uint16_t)(s * 512 + lg);
       }
-      if (lane == 0) lds_add(&sh.cnt[k & 1], c);
-      lds_release();
-      if (lane == 0) lds_add(&sh.cnt_done, 1u);
     }
-    nl = k + 1 < K ? append_near<NS>(L.NL(k + 1, w), 0u, nrm, ent) : 0u;
-    acc.eps += (uint32_t)__builtin_popcount(dn);
     lds_release();
-    if (lane == 0) lds_add(&sh.trans_done, 1u);
-    if (w == 0) WSTAMP(P, k, 2);
-    WSTAMP(P, k, 20 + w);
-    if (tmode & TM_TRANSFIRST) fill_next();
+    if (lane == 0) lds_add(&sh.r2s_done, 1u);
+    if (w == 0) WSTAMP(P, k, 4);
+    if (k + 1 < K) {
+      lds_wait(&sh.sy_ready, (uint32_t)k + 1u, derr);
+      const u128 Srw = mk128(sh.rw[(k + 1) & 1][0], sh.rw[(k + 1) & 1][1]);
+      if (!(tmode & TM_NOFILL)) fill_window(L.RW, jrw, j512, nw, Srw, lg);
+      lds_release();
+      if (lane == 0) lds_add(&sh.fill_done, 1u);
+      fill_target += EW;
 #pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      ai[s] = an[s];
-      if (k + 2 < K) an[s] = action_index<NA>(a2[s], derr);
+      for (int s = 0; s < NS; ++s) arow[s] = action_row<NA>(anext[s], derr);
     }
-    if (w == 0) WSTAMP(P, k, 18);
-  }
-  // the last step's resetters, then its outputs straight from the env waves
-  lds_wait(&sh.cells_done, (uint32_t)K, derr);
-  env_take<NS, NA>(P, sh, tb, L, K - 1, sh.fix[K & 1] & 1u, false, 0u, dn, bm, ai, ae);
-  if (!(tmode & TM_NOSTORE)) {
-    const uint32_t* st = reinterpret_cast<const uint32_t*>(L.stg(K - 1, E));
-    const size_t base = (size_t)(K - 1) * B + e0 + (size_t)lg;
+    if (w == 0) WSTAMP(P, k, 5);
+    if (w == EW - 1) WSTAMP(P, k, 15);
+    // ---- the exchange's outcome: the resetters' cells ----
+    lds_wait(&sh.cells_done, (uint32_t)k + 1u, derr);
+    if (w == 0) WSTAMP(P, k, 11);
+    const uint32_t fix = sh.fix[k & 1];
+    if (fix & 1u) {
+      wg_env_slow<NS>(P, sh, tb, L.CS(k), k, stg, dn, pre, bm, ae);
+    } else {
 #pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const uint32_t v = st[s * 512 + lg];
-      const size_t e = base + (size_t)s * 512;
-      obs[e] = tb.ocell(v & 0xFFFFu);
-      rew[e] = (v & 0x10000u) ? P.r_goal : ((v & 0x40000u) ? P.r_wall : P.r_step);
-      term[e] = (uint8_t)((v >> 16) & 1u);
-      trunc[e] = (uint8_t)((v >> 17) & 1u);
+      for (int s = 0; s < NS; ++s)
+        if ((dn >> s) & 1u) ae[s] = reinterpret_cast<const uint16_t*>(stg)[2 * (s * 512 + lg)];
+    }
+    lds_release();
+    if (lane == 0) lds_add(&sh.res_done, 1u);
+    if (k == K - 1 && !(tmode & TM_NOSTORE)) {  // the launch's last step: its outputs straight from the env waves
+      const uint32_t* st = reinterpret_cast<const uint32_t*>(stg);
+      const size_t base = (size_t)k * B + e0 + (size_t)lg;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        const uint32_t v = st[s * 512 + lg];
+        const size_t e = base + (size_t)s * 512;
+        obs[e] = tb.ocell(v & 0xFFFFu);
+        rew[e] = (v & 0x10000u) ? P.r_goal : ((v & 0x40000u) ? P.r_wall : P.r_step);
+        term[e] = (uint8_t)((v >> 16) & 1u);
+        trunc[e] = (uint8_t)((v >> 17) & 1u);
+      }
+    }
+    if ((fix & 2u) && k + 1 < K) {  // the prediction missed the window: regenerate it exactly
+      fill_window(L.RW, jrw, j512, nw, mk128(sh.rw[(k + 1) & 1][0], sh.rw[(k + 1) & 1][1]), lg);
+      lds_release();
+      if (lane == 0) lds_add(&sh.fill_done, 1u);
+      fill_target += EW;
     }
   }
 #pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    aeg[e0 + (size_t)s * 512 + lg] = ae[s];
-    acc.lens -= ae[s] >> 16;
+  for (int k = 0; k < NS; ++k) {
+    aeg[e0 + (size_t)k * 512 + lg] = ae[k];
+    acc.lens -= ae[k] >> 16;
   }
 }
 
@@ -1015,8 +815,8 @@ __device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Ta
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void nt_store(void* p, u32x4 v) { __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p)); }
 
-// Step k's staging (final once every env wave has taken or placed its resetters' cells) -> obs, reward, terminated,
-// truncated in HBM, 4 envs per lane and chunk, while the env waves run the next steps.
+// Step k's staging (final once every env wave has taken its resetters' cells) -> obs, reward, terminated,
+// truncated in HBM, 16 envs per lane and chunk, while the env waves run the next steps.
 template <int NS>
 __device__ __forceinline__ void wg_store(const WgParams& P, WgShared& sh, const Tabs& tb, const Lds& L, int K,
                                          int32_t* __restrict__ obs, float* __restrict__ rew, uint8_t* __restrict__ term,
@@ -1031,15 +831,17 @@ __device__ __forceinline__ void wg_store(const WgParams& P, WgShared& sh, const 
   uint32_t* derr = &P.ctl->err;
   lds_barrier();  // P1
   for (int k = 0; k + 1 < K; ++k) {  // (the env waves write the last step themselves)
-    lds_wait(&sh.res_done, (uint32_t)EW * (uint32_t)(k + 1), derr);  // every resetter's cell in place
-    // out of the way of the next step's transitions, except for a launch's last steps, whose copies are the tail
+    lds_wait(&sh.res_done, (uint32_t)EW * (uint32_t)(k + 1), derr);
+    // and out of the way of the next step's transitions (the critical path): start once they are done, except for
+    // a launch's last steps, whose copies are the launch's tail
     if (k + WG_EAGER_TAIL < K && !(tmode & TM_EAGERSTORE))
       lds_wait(&sh.trans_done, (uint32_t)EW * (uint32_t)(k + 2), derr);
     if (sl < 64) WSTAMP(P, k, 13);
     const uint32_t* st = reinterpret_cast<const uint32_t*>(L.stg(k, E));
     const size_t base = (size_t)k * B + (size_t)beta * E;
     // Lane-contiguous: in every store instruction consecutive lanes write consecutive 16 B (obs, reward) or 4 B
-    // (terminated, truncated) of 4 envs each, whole cache lines per instruction.
+    // (terminated, truncated) of 4 envs each, whole cache lines per instruction (a lane-strided pattern left the
+    // lines to be merged from partial writes and ran the output stream at a fraction of the HBM rate).
 #if WG_SUNROLL == 4
 #pragma unroll 4
 #elif WG_SUNROLL == 1
@@ -1089,7 +891,7 @@ __global__ __launch_bounds__(TPB) void wgrid_rollout(const WgParams* __restrict_
   constexpr int E = NS * 512;
   if (tid == 0) LSTAMP(P, 0);
   // stage the table image (each thread's 16-B loads in flight before its LDS stores)
-  // (the control and store waves; the env waves compute their first states meanwhile)
+  // (the control and store waves; the env waves fill their first window meanwhile)
   if (wid >= EW) {
     constexpr int CT = (NWAVES - EW) * 64;
     const int t = tid - EW * 64;
@@ -1110,9 +912,8 @@ __global__ __launch_bounds__(TPB) void wgrid_rollout(const WgParams* __restrict_
     }
   }
   if (tid == EW * 64) {
-    sh.trans_done = sh.cnt_done = sh.cs_done = sh.fill_done = sh.res_done = sh.st_done = 0;
-    sh.sy_ready = sh.cells_done = sh.pro = 0;
-    sh.cnt[0] = sh.cnt[1] = 0;
+    sh.trans_done = sh.cs_done = sh.r2s_done = sh.fill_done = sh.res_done = sh.st_done = 0;
+    sh.sx_ready = sh.sy_ready = sh.cells_done = sh.pro = 0;
     sh.fix[0] = sh.fix[1] = 0;
   }
   const Tabs tb(dyn, P);
@@ -1126,7 +927,7 @@ __global__ __launch_bounds__(TPB) void wgrid_rollout(const WgParams* __restrict_
     else __builtin_amdgcn_s_setprio(1);
     wg_store<NS>(P, sh, tb, L, K, obs, rew, term, trunc);
   } else {
-    wg_env<NS, NA>(P, sh, tb, L, act, K, acc, obs, rew, term, trunc);
+    wg_env<NS, NA>(P, sh, tb, L, dyn, act, K, acc, obs, rew, term, trunc);
   }
   // episode statistics of the launch (env waves; the others contribute zeros)
   float rsum = 0.f;
@@ -1153,9 +954,6 @@ __global__ __launch_bounds__(TPB) void wgrid_rollout(const WgParams* __restrict_
     m_n[wid] = nst;
   }
   __syncthreads();
-#ifdef GP_STAMPS
-  for (int i = tid; i < 32 * 32; i += TPB) P.dbg[(size_t)blockIdx.x * 32 * 32 + i] = (&sh.stp[0][0])[i];
-#endif
   if (tid == 0) {
     float rr = 0;
     uint32_t e = 0, l = 0, n = 0;

@@ -1,5 +1,6 @@
-"""GPU parity of C-ROOMS exact mode (rng_mode="numpy", csrc/crooms.hip: crooms_numpy_rollout for B <= 4096, the
-multi-workgroup xg_* draw-call kernels above).
+"""GPU parity of C-ROOMS exact mode (rng_mode="numpy", csrc/crooms.hip: crooms_numpy_rollout for B <= 1024
+(XG_MIN_ENVS, the measured crossover), the multi-workgroup xg_* draw-call kernels above; both paths are also
+forced on the other side of the crossover).
 
 The device draws the reference's own PCG64 stream word for word — rng.random / rng.normal (numpy's
 256-layer ziggurat, a data-dependent number of words per normal) / rng.choice (buffered 32-bit Lemire) in
@@ -78,7 +79,7 @@ ORACLE_CASES = [
     ({"obs_type": "hansen8", "action_type": "ordinal", "layout": "16", "goal_xy": None, "time_limit": 20}, 1500, 45, 1),
     ({"obs_type": "grid", "action_type": "cardinal", "action_std": 0.0, "time_limit": 15}, 999, 40, 40),
     ({"obs_type": "goal_room", "layout": "8b", "goal_xy": None, "time_limit": 12}, 4099, 30, 5),
-    # B > 4096: the multi-workgroup path (grid-wide draw calls, cluster-resolved ziggurat chains)
+    # larger: the multi-workgroup path (grid-wide draw calls, cluster-resolved ziggurat chains) at scale
     ({"obs_type": "vector_mdp", "action_std": 0.5, "time_limit": 6}, 65536, 12, 6),
     ({"obs_type": "vector_goal_mdp", "goal_xy": None, "use_velocity": True, "time_limit": 25}, 30001, 30, 3),
     ({"obs_type": "hansen8", "action_type": "ordinal", "layout": "16", "goal_xy": None, "time_limit": 20}, 20000, 25, 5),
@@ -98,6 +99,19 @@ def test_numpy_mode_two_launch_calls_vs_oracle(kw, B, steps, K, gpu_device):
     from gym_po_amd._lib import debug_knobs
     with debug_knobs(disable_fused=1):
         test_numpy_mode_vs_oracle(kw, B, steps, K, gpu_device)
+
+
+# each path on the other side of the crossover (gp_debug_set xg_min_envs at create): the one-workgroup kernel up to
+# its 4096-env limit, the grid-wide calls down to a single partial block
+CROSS_CASES = [(ORACLE_CASES[0], 4096), (ORACLE_CASES[1], 4096), (ORACLE_CASES[3], 0),
+               (({"obs_type": "vector_mdp", "action_std": 0.5, "time_limit": 6}, 64, 20, 4), 0)]
+
+
+@pytest.mark.parametrize("case,xg_min", CROSS_CASES)
+def test_numpy_mode_both_paths_across_crossover(case, xg_min, gpu_device):
+    from gym_po_amd._lib import debug_knobs
+    with debug_knobs(xg_min_envs=xg_min):
+        test_numpy_mode_vs_oracle(*case, gpu_device)
 
 
 @pytest.mark.parametrize("kw,B,steps,K", ORACLE_CASES)

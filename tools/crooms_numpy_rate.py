@@ -1,7 +1,8 @@
 """Throughput of C-ROOMS exact mode (rng_mode='numpy': one workgroup up to 4096 envs, the multi-workgroup draw
 calls above) beside philox mode, same config.
 
-Usage (GPU box): python tools/crooms_numpy_rate.py  -> one JSON line per (mode, B).
+Usage (GPU box): python tools/crooms_numpy_rate.py [B ...] -> one JSON line per (mode, B). XG_MIN=n: the
+one-workgroup kernel only up to n envs (gp_debug_set xg_min_envs; crossover measurements). MODES=numpy: one mode.
 """
 import json
 import os
@@ -17,7 +18,10 @@ from gym_po_amd import CRoomsEnv  # noqa: E402
 
 def rate(mode, B, K=None, reps=3):
     K = K or (50 if B <= 65536 else 8)
-    env = CRoomsEnv(B, obs_type="vector_mdp", rng_mode=mode)
+    from gym_po_amd._lib import debug_knobs
+    knobs = {"xg_min_envs": int(os.environ["XG_MIN"])} if os.environ.get("XG_MIN") else {}
+    with debug_knobs(**knobs):
+        env = CRoomsEnv(B, obs_type="vector_mdp", rng_mode=mode)
     env.reset(seed=0)
     a = torch.rand((K, B, 2), device=env.device) * 2 - 1
     env.rollout(a)
@@ -28,10 +32,10 @@ def rate(mode, B, K=None, reps=3):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     return {"mode": mode, "num_envs": B, "steps": K * reps, "us_per_step": dt / (K * reps) * 1e6,
-            "env_steps_per_s": B * K * reps / dt}
+            "env_steps_per_s": B * K * reps / dt, "xg_min_envs": knobs.get("xg_min_envs", 4096)}
 
 
 if __name__ == "__main__":
     for B in [int(x) for x in sys.argv[1:]] or (1024, 4096, 65536, 1 << 21):
-        for mode in ("numpy", "philox"):
+        for mode in os.environ.get("MODES", "numpy philox").split():
             print(json.dumps(rate(mode, B)), flush=True)
