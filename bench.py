@@ -469,7 +469,9 @@ def main():
 
     kernel_name = None
     if args.workload == "fourrooms" and args.mode == "numpy" and env.query("wgrid"):
-        kernel_name = f"wgrid_rollout<{env.query('wgrid_block_envs') // 512},{W['n_actions']}>"
+        # launches of up to wgrid_kmax steps run the windowed kernel, longer ones the fused kernel (grid.hip)
+        kernel_name = (f"wgrid_rollout<{env.query('wgrid_block_envs') // 512},{W['n_actions']}>"
+                       if steps_per_launch <= env.query("wgrid_kmax") else "grid_rollout_numpy<GP_OBS_HANSEN,2,4,true>")
     total_steps = (args.envs if args.strong else B * world) * args.steps
     cfg_key = (f"fourrooms_hansen4_B{B}_{args.mode}" if args.workload == "fourrooms" else
                f"{args.workload}_B{B}_{args.mode}")

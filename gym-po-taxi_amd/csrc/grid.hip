@@ -35,6 +35,11 @@ constexpr int EPT = 4;
 constexpr int EPB = TPB * EPT;
 constexpr uint32_t SPIN_LIMIT = 1u << 24;  // default polls before a persistent wait gives up (GP_SPIN_LIMIT)
 constexpr int MAX_TPB2 = 1024;  // max tiles per K2 block (B <= 256 * 1024 * EPB)
+// Longest launch on the windowed kernel (wgrid.hip); longer launches run the fused kernel (grid_rollout_numpy).
+// In-call A/Bs on MI355X (profiles/r05_ab_kernel_by_K.txt).
+#ifndef WG_KMAX
+#define WG_KMAX 24
+#endif
 
 struct GridLdsTab {
   int32_t off, bytes;
@@ -2705,6 +2710,7 @@ struct GridBackend : EnvBackend {
   int fused_G = 0, fused_qpt = 0;  // fused numpy rollout geometry (0 = not eligible)
   // windowed numpy rollout (wgrid.hip): G blocks of E = 512 * NS envs; 0 = not eligible
   int wg_G = 0, wg_E = 0, wg_NS = 0, wg_H = 0;
+  int wg_kmax = WG_KMAX;  // launches of more steps go to the fused kernel when it can take them (gp_debug_set wg_kmax)
   size_t wg_lds = 0;
   WgParams wg{};
   std::vector<char> wg_img;        // LDS image of its tables (the PCG jump parts rebuilt on every seed)
@@ -2744,6 +2750,7 @@ struct GridBackend : EnvBackend {
     else if (!strcmp(key, "wgrid_blocks")) *v = wg_G;
     else if (!strcmp(key, "wgrid_block_envs")) *v = wg_E;
     else if (!strcmp(key, "wgrid_halo")) *v = wg_H;
+    else if (!strcmp(key, "wgrid_kmax")) *v = wg_kmax;
     else return EnvBackend::query(key, v);
     return GP_OK;
   }
@@ -2791,6 +2798,12 @@ struct GridBackend : EnvBackend {
   bool wgrid_ok(const void* act, const void* obs, const void* rew, const void* term, const void* trunc) const {
     auto al = [](const void* x, uintptr_t m) { return ((uintptr_t)x & (m - 1)) == 0; };
     return wg_G && al(act, 4) && al(obs, 16) && al(rew, 16) && al(term, 16) && al(trunc, 16);
+  }
+  // The windowed kernel for launches of up to wg_kmax steps, the fused kernel (same stream, same state) for longer
+  // ones when it can take them.
+  bool wgrid_pick(int K, const void* act, const void* obs, const void* rew, const void* term, const void* trunc) const {
+    if (!wgrid_ok(act, obs, rew, term, trunc)) return false;
+    return K <= wg_kmax || !(fused_ok(act, obs, rew, term, trunc) && B % 4 == 0);
   }
   int launch_wgrid(int K, const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc, hipStream_t s) {
     const WgArgs a{b_wgp.as<WgParams>(), K, (const int32_t*)act, (int32_t*)obs, rew, term, trunc};
@@ -3165,7 +3178,7 @@ int GridBackend::step(const void* act, void* obs, float* rew, uint8_t* term, uin
   int e = dispatch_obs(d.obs_kind, [&](auto okc) -> int {
     constexpr int OK = decltype(okc)::value;
     if (rng_mode == GP_RNG_NUMPY) {
-      if (wgrid_ok(act, obs, rew, term, trunc)) return launch_wgrid(1, act, obs, rew, term, trunc, s);
+      if (wgrid_pick(1, act, obs, rew, term, trunc)) return launch_wgrid(1, act, obs, rew, term, trunc, s);
       if (fused_ok(act, obs, rew, term, trunc)) return launch_fused<OK>(1, act, obs, rew, term, trunc, s);
       timer.begin(s);
       hipLaunchKernelGGL(grid_step_numpy<OK>, dim3(d.nblk), dim3(TPB), 0, s, d, (const int32_t*)act, obs, rew, term,
@@ -3200,7 +3213,7 @@ int GridBackend::step(const void* act, void* obs, float* rew, uint8_t* term, uin
 
 int GridBackend::rollout(int K, const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc,
                          hipStream_t s) {
-  if (rng_mode == GP_RNG_NUMPY && wgrid_ok(act, obs, rew, term, trunc)) {
+  if (rng_mode == GP_RNG_NUMPY && wgrid_pick(K, act, obs, rew, term, trunc)) {
     if (!has_reset) {
       gp_set_error("rollout() before reset()");
       return GP_E_STATE;
@@ -3578,6 +3591,7 @@ int GridBackend::build(const gp_grid_config* cfg) {
   // function of the agent cell (Hansen with the goal multiplier folded in, or table[agent] + table2[goal])
   if (rng_mode == GP_RNG_NUMPY && d.fixed_goal >= 0 && d.fixed_agent < 0 && d.n_agent_valid >= 2 &&
       (cfg->obs_kind == GP_OBS_HANSEN || cfg->obs_kind == GP_OBS_TABLE) && !dbg.no_wgrid && !dbg.disable_fused) {
+    if (dbg.wg_kmax >= 0) wg_kmax = dbg.wg_kmax;
     std::vector<int32_t> ocell(nc);
     for (int c = 0; c < nc; ++c)
       ocell[c] = cfg->obs_kind == GP_OBS_HANSEN ? ofix[c] : t1[c] + (t2.empty() ? 0 : t2[d.fixed_goal]);

@@ -11,7 +11,9 @@ What each case forces:
   regeneration after the exchange);
 - a Lemire rejection planted in the choice() stream inside a launch (the slow path: rejected positions listed,
   every resetter placed exactly);
-- ordinal actions (8 thresholds per row) and table obs (ROOMS layouts).
+- ordinal actions (8 thresholds per row) and table obs (ROOMS layouts);
+- the kernel choice by launch length (launches of more than wg_kmax steps run the fused kernel on the same stream
+  and state): every launch on either kernel, and the default split, over mixed launch lengths.
 """
 import numpy as np
 import pytest
@@ -60,6 +62,19 @@ def _check_chunks(env, ora, chunks, action_seed, n_act, before_chunk=None):
 def _fourrooms(B, device, **kw):
     from gym_po_amd import MultistoryFourRoomsEnv
     return MultistoryFourRoomsEnv(B, grid_z=1, obs_type="hansen", device=device, **kw)
+
+
+@pytest.mark.parametrize("kmax", [0, 24, 1000])
+def test_kernel_choice_by_launch_length_bit_exact(kmax, gpu_device):
+    from gym_po_amd._lib import debug_knobs
+    B = 1 << 18
+    with debug_knobs(wg_kmax=kmax):
+        env = _fourrooms(B, gpu_device)
+    assert env.query("wgrid") == 1
+    ora = gridworld.FourRoomsOracle(B, 1, obs_type="hansen")
+    np.testing.assert_array_equal(_reset_obs(env, 41).astype(np.int64), np.asarray(ora.reset_seed(41)).astype(np.int64))
+    _check_chunks(env, ora, (1, 20, 33, 2, 64, 24, 25), action_seed=8, n_act=4)
+    assert env.metrics()["env_steps"] == B * 169
 
 
 @pytest.mark.parametrize("B,E", [(1 << 17, 512), (1 << 18, 1024), (1 << 19, 2048), (3 << 17, 2048), (8192, 512)])
@@ -188,10 +203,10 @@ def _goal_adjacent_cells(ora):
 
 @pytest.mark.parametrize("B,frac", [(1 << 20, 0.9), (1 << 20, 0.2), (1 << 20, 0.05), (1 << 17, 0.5)])
 def test_wgrid_goal_crowd_bit_exact(B, frac, gpu_device):
-    """Most (or many) envs put on goal-adjacent cells with set_state: the early reset count lists every such env.
-    frac 0.9 overflows the per-block list (the count falls back to the step's masks) and resets hundreds of
-    thousands of envs at once (slow path, env-wave placement); 0.2 / 0.05 keep the list under its cap with a few
-    hundred / tens of resetters per block (control- and env-wave placement). Every later step is bit-exact too."""
+    """Most (or many) envs put on goal-adjacent cells with set_state, so that hundreds of thousands (0.9) down to
+    a few hundred per block (0.05) reach the goal in the same step: the step's reset count, the rank-ordered
+    resetter lists and the window regeneration (the count lands far outside the predicted window) stay exact, and
+    every later step is bit-exact too."""
     env = _fourrooms(B, gpu_device)
     assert env.query("wgrid") == 1
     ora = gridworld.FourRoomsOracle(B, 1, obs_type="hansen")
@@ -209,12 +224,12 @@ def test_wgrid_goal_crowd_bit_exact(B, frac, gpu_device):
     _check_chunks(env, ora, (6, 1, 9), action_seed=11, n_act=4)
 
 
-@pytest.mark.parametrize("tmode", [4, 512, 1024, 512 | 1024, 2048, 128])
+@pytest.mark.parametrize("tmode", [4, 64, 128, 32 | 512, 8 | 16])
 def test_wgrid_schedule_variants_bit_exact(tmode, gpu_device):
-    """Test-only schedules of the windowed kernel (gp_debug_set wg_tmode): 4 = every env wave counts from its full
-    transitions (no early count), 512 = every window word re-derived from the window's base state (the path a
-    high-half tie takes), 1024 = the env waves place every step's resetters, 2048 = transitions before the next
-    window's fill, 128 = no candidate cells (every resetter's word drawn after the exchange)."""
+    """Test-only schedules of the windowed kernel (gp_debug_set wg_tmode, wgrid.hip TM_*): 4 = next actions loaded
+    after the transitions, 64 = store waves copy a step as soon as it is final, 128 = no candidate cells (every
+    resetter's word drawn after the exchange), 32|512 = env-wave priority off / always high, 8|16 = throttled
+    stores and busy polling. Results must not depend on the schedule."""
     from gym_po_amd._lib import debug_knobs
     B = 1 << 18
     with debug_knobs(wg_tmode=tmode):
