@@ -662,6 +662,7 @@ __device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Ta
     const GridCtl* C = P.ctl;
     fill_window(L.RW, jrw, j512, nw, apply_jump(P.jblk[2 * beta + 1], mk128(C->s_hi, C->s_lo)), lg);
   }
+  if (w == 0) LSTAMP(P, 2);
   lds_barrier();  // P1
 #pragma unroll
   for (int k = 0; k < NS; ++k) {
@@ -669,6 +670,7 @@ __device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Ta
     acc.lens += ae[k] >> 16;  // episode lengths: + elapsed at the start - elapsed at the end + steps
   }
   lds_wait(&sh.pro, 1u, derr);  // the first window's offset
+  if (w == 0) LSTAMP(P, 7);
   if (lane == 0) lds_add(&sh.fill_done, 1u);
   uint32_t fill_target = EW;
   uint64_t bm[NS];
@@ -910,6 +912,8 @@ __global__ __launch_bounds__(TPB) void wgrid_rollout(const WgParams* __restrict_
       if (a2) d[i0 + 2 * CT] = v2;
       if (a3) d[i0 + 3 * CT] = v3;
     }
+    if (wid == EW) LSTAMP(P, 5);
+    if (wid == EW + 1) LSTAMP(P, 6);
   }
   if (tid == EW * 64) {
     sh.trans_done = sh.cs_done = sh.r2s_done = sh.fill_done = sh.res_done = sh.st_done = 0;

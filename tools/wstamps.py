@@ -8,7 +8,9 @@ Stamps are s_memrealtime (100 MHz, synchronous across XCDs), per block and step 
   control:    6 S(y) + rejection check + window base published, 7 transitions seen, 8 granule publish,
               9 all-gather done, 10 cells drawn (before B2), 11 after B2, 12 next state done
   store wave: 13 copy start (after B2), 14 copy issued
-Launch stamps per block: 0 entry, 1 P1 passed (control), 3 control step loop done, 4 kernel end (slot 2 unused).
+Launch stamps per block: 0 entry, 1 P1 passed (control), 2 env wave 0's first window filled, 3 control step loop
+done, 4 kernel end, 5 / 6 table staging done (control wave / store wave 0), 7 env wave 0 has the first
+window's offset.
 """
 import ctypes
 import os
@@ -27,6 +29,7 @@ B = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
 K = int(sys.argv[2]) if len(sys.argv) > 2 else 64
 from gym_po_amd._lib import debug_knobs  # noqa: E402
 knobs = dict((kv.split("=")[0], int(kv.split("=")[1])) for kv in os.environ.get("GP_KNOBS", "").split(",") if kv)
+knobs.setdefault("wg_kmax", 1 << 20)  # every launch on the windowed kernel (longer ones would run the fused kernel)
 with debug_knobs(**knobs):
     env = MultistoryFourRoomsEnv(B, 1, obs_type="hansen")
 print(f"knobs {knobs}")
@@ -51,6 +54,13 @@ t0 = ls[:, 0].min()
 print(f"B={B} K={K} G={G} E={env.query('wgrid_block_envs')} H={env.query('wgrid_halo')}")
 print(f"launch: entry spread {ls[:, 0].max() - t0} ns; P1 passed (control, max) {ls[:, 1].max() - t0}; "
       f"control loop done (max) {ls[:, 3].max() - t0}; kernel end (max) {ls[:, 4].max() - t0} ns")
+e0 = ls[:, 0]
+print("prologue per block (median/max ns from the block's entry): env first window filled "
+      f"{np.median(ls[:, 2] - e0):.0f}/{(ls[:, 2] - e0).max()}; table staging done: control wave "
+      f"{np.median(ls[:, 5] - e0):.0f}/{(ls[:, 5] - e0).max()}, store wave 0 {np.median(ls[:, 6] - e0):.0f}/"
+      f"{(ls[:, 6] - e0).max()}; control past P1, first window published {np.median(ls[:, 1] - e0):.0f}/"
+      f"{(ls[:, 1] - e0).max()}; env wave 0 sees it {np.median(ls[:, 7] - e0):.0f}/{(ls[:, 7] - e0).max()}; "
+      f"env wave 0 starts step 0 {np.median(a[:, 0, 0] - e0):.0f}/{(a[:, 0, 0] - e0).max()}")
 
 
 def at(k, i):  # stamp i of step k over blocks, ns from the first block's entry
