@@ -793,6 +793,263 @@ __global__ __launch_bounds__(NP_TPB) void taxi_np_kernel(TaxiDev p, TaxiNpDev q,
   if (K > 0) taxi_metrics<NP_WAVES>(p, rsum, eps, lens, nst);
 }
 
+// ---- numpy mode, grid-wide (B > NPG_MIN_ENVS): the same step as three launches ----
+// Only the draws walk the stream (one workgroup, np_draws as above); both env passes run over every CU:
+//   taxi_npg_pass1  one 1024-env tile per block: transitions, rewards / flags, and each env's rank among its
+//                   tile's task completions (tc) and episode resets (rs) in env order; the tile's two counts;
+//   taxi_npg_draws  the tiles' counts -> per-tile prefixes and the step's b1 / b2, then the draws;
+//   taxi_npg_pass2  one tile per block: resets applied (rank = tile prefix + rank in the tile), observations.
+// (reset(): pass 1 flags every env a reset, pass 2 writes the obs.)
+constexpr int NPG_MIN_ENVS = 1024;  // at or below: the one-workgroup kernel (K steps per launch; measured crossover)
+
+struct NpgDev {
+  uint32_t* bcnt;   // [ntiles] tile counts: tc | rs << 16
+  uint64_t* bpre;   // [ntiles] tile prefixes: tc | rs << 32
+  int32_t grid;     // metric slots (p.mslot)
+};
+
+// Exclusive block scan of a u64 per thread (256 threads); the block total in tot.
+__device__ __forceinline__ uint64_t npg_scan64(uint64_t x, uint64_t& tot) {
+  __shared__ uint64_t ws[WAVES];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint64_t v = x;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t y = __shfl_up(v, d, 64);
+    if (lane >= d) v += y;
+  }
+  if (lane == 63) ws[w] = v;
+  __syncthreads();
+  uint64_t base = 0;
+  tot = 0;
+#pragma unroll
+  for (int i = 0; i < WAVES; ++i) {
+    base += i < w ? ws[i] : 0ull;
+    tot += ws[i];
+  }
+  __syncthreads();
+  return base + v - x;
+}
+
+// Metrics of a block into slot (block mod slots), atomically (more blocks than slots).
+__device__ void npg_metrics(const TaxiDev& p, int slots, float rsum, uint32_t eps, uint32_t lens, uint32_t nst) {
+  __shared__ float s_r[WAVES];
+  __shared__ uint32_t s_e[WAVES], s_l[WAVES], s_n[WAVES];
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    rsum += __shfl_xor(rsum, d, 64);
+    eps += __shfl_xor(eps, d, 64);
+    lens += __shfl_xor(lens, d, 64);
+    nst += __shfl_xor(nst, d, 64);
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) { s_r[wid] = rsum; s_e[wid] = eps; s_l[wid] = lens; s_n[wid] = nst; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float r = 0.f;
+    unsigned long long e = 0, l = 0, n = 0;
+    for (int w = 0; w < WAVES; ++w) { r += s_r[w]; e += s_e[w]; l += s_l[w]; n += s_n[w]; }
+    TaxiSlot& m = p.mslot[blockIdx.x % (unsigned)slots];
+    atomicAdd(&m.return_sum, (double)r);
+    atomicAdd(&m.episodes, e);
+    atomicAdd(&m.length_sum, l);
+    atomicAdd(&m.env_steps, n);
+  }
+}
+
+// Pass 1 of step k (RESET: reset(), every env flagged a reset).
+template <bool RESET>
+__global__ __launch_bounds__(TPB) void taxi_npg_pass1(TaxiDev p, TaxiNpDev q, NpgDev g, size_t off,
+                                                      const int32_t* __restrict__ act, float* __restrict__ rew,
+                                                      uint8_t* __restrict__ term, uint8_t* __restrict__ trunc) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  if (!RESET) stage_tables(p, lds);
+  __syncthreads();
+  const int tile = blockIdx.x, env0 = tile * EPB + threadIdx.x * EPT;
+  float rsum = 0.f;
+  uint32_t eps = 0, lens = 0, nst = 0;
+  bool ftc[EPT], frs[EPT];
+  if (RESET) {
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+      ftc[i] = false;
+      frs[i] = env0 + i < p.B;
+    }
+  } else {
+    uint32_t u[4], a4[4];
+    ld4_u32(p.st, env0, p.B, u);
+    ld4_u32(reinterpret_cast<const uint32_t*>(act + off), env0, p.B, a4);
+    float r[4];
+    uint8_t tm[4], tr[4];
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+      const bool live = env0 + i < p.B;
+      ftc[i] = frs[i] = false;
+      r[i] = 0.f;
+      tm[i] = tr[i] = 0;
+      if (!live) continue;
+      uint32_t s = u[i] & 0xFFFu, nd = (u[i] >> 12) & 0xFu, el = (u[i] >> 16) + 1u;
+      int a = (int)a4[i];  // extended_taxi.py:344-364 (as taxi_np_kernel's pass 1)
+      if (action_out_of_range(a, NACT)) flag_bad_action(p.derr);
+      a = a < 0 ? (a == -1 ? NACT : max(a + NACT, 0)) : min(a, NACT - 1);
+      const uint32_t t = l_trans(lds, p)[s * TCOL + (uint32_t)a];
+      s = t & 0xFFFu;
+      const uint32_t goal = (t >> 12) & 1u, bad = (t >> 13) & 1u;
+      nd += goal;
+      r[i] = goal ? p.r_goal : (bad ? p.r_bad : p.r_any);
+      const bool dterm = nd == (uint32_t)p.num_passengers, dtrunc = el > (uint32_t)p.time_limit;
+      tm[i] = dterm ? 1 : 0;
+      tr[i] = dtrunc ? 1 : 0;
+      rsum += r[i];
+      nst += 1u;
+      ftc[i] = goal && !(dterm || dtrunc);
+      frs[i] = dterm || dtrunc;
+      if (frs[i]) {
+        eps += 1u;
+        lens += el;
+      }
+      u[i] = s | (nd << 12) | (min(el, 0xFFFFu) << 16);
+    }
+    st4_u32(reinterpret_cast<uint32_t*>(rew + off), env0, p.B,
+            {__float_as_uint(r[0]), __float_as_uint(r[1]), __float_as_uint(r[2]), __float_as_uint(r[3])});
+    st4_u8(term + off, env0, p.B, tm);
+    st4_u8(trunc + off, env0, p.B, tr);
+    st4_u32(p.st, env0, p.B, u);
+  }
+  // ranks in env order within the tile (env0 + i: thread-major, then i)
+  uint32_t ctc = 0, crs = 0;
+#pragma unroll
+  for (int i = 0; i < EPT; ++i) {
+    ctc += ftc[i] ? 1u : 0u;
+    crs += frs[i] ? 1u : 0u;
+  }
+  uint64_t tot;
+  const uint64_t base = npg_scan64((uint64_t)ctc | ((uint64_t)crs << 32), tot);
+  uint32_t rtc = (uint32_t)base, rrs = (uint32_t)(base >> 32);
+  int32_t rk[4];
+#pragma unroll
+  for (int i = 0; i < EPT; ++i) {
+    rk[i] = ftc[i] ? (int32_t)rtc : (frs[i] ? (int32_t)(rrs | (1u << 30)) : -1);
+    rtc += ftc[i] ? 1u : 0u;
+    rrs += frs[i] ? 1u : 0u;
+  }
+  st4_u32(reinterpret_cast<uint32_t*>(q.rk), env0, p.B,
+          {(uint32_t)rk[0], (uint32_t)rk[1], (uint32_t)rk[2], (uint32_t)rk[3]});
+  if (threadIdx.x == 0) g.bcnt[tile] = (uint32_t)tot | ((uint32_t)(tot >> 32) << 16);
+  if (!RESET) npg_metrics(p, g.grid, rsum, eps, lens, nst);
+}
+
+// The draws of one step (one workgroup of NP_TPB threads): tile prefixes, b1 / b2, then np_draws.
+__global__ __launch_bounds__(NP_TPB) void taxi_npg_draws(TaxiDev p, TaxiNpDev q, NpgDev g, int ntiles) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  __shared__ NpShared sh;
+  __shared__ uint64_t etab[256];
+  __shared__ uint64_t wsum[NP_WAVES];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  {
+    const uint4* s2 = (const uint4*)q.mtab;
+    uint4* d2 = (uint4*)lds;
+    for (int i = t; i < q.mtab_bytes / 16; i += NP_TPB) d2[i] = s2[i];
+    for (int i = t; i < 256; i += NP_TPB) etab[i] = gp_libm::kExpTab[i];
+    if (t == 0) {
+      sh.S[0] = q.rng[0];
+      sh.S[1] = q.rng[1];
+      sh.has = (uint32_t)q.rng[4];
+      sh.uval = (uint32_t)q.rng[5];
+    }
+  }
+  // per-tile prefixes: thread t sums tiles [t * per, (t + 1) * per), a block scan, then the tiles' own
+  const int per = (ntiles + NP_TPB - 1) / NP_TPB;
+  uint64_t x = 0;
+  for (int j = 0; j < per; ++j) {
+    const int tl = t * per + j;
+    if (tl < ntiles) {
+      const uint32_t c = g.bcnt[tl];
+      x += (uint64_t)(c & 0xFFFFu) | ((uint64_t)(c >> 16) << 32);
+    }
+  }
+  uint64_t v = x;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t y = __shfl_up(v, d, 64);
+    if (lane >= d) v += y;
+  }
+  if (lane == 63) wsum[w] = v;
+  __syncthreads();
+  uint64_t base = 0, tot = 0;
+  for (int i = 0; i < NP_WAVES; ++i) {
+    base += i < w ? wsum[i] : 0ull;
+    tot += wsum[i];
+  }
+  base += v - x;
+  for (int j = 0; j < per; ++j) {
+    const int tl = t * per + j;
+    if (tl < ntiles) {
+      g.bpre[tl] = base;
+      const uint32_t c = g.bcnt[tl];
+      base += (uint64_t)(c & 0xFFFFu) | ((uint64_t)(c >> 16) << 32);
+    }
+  }
+  if (t == 0) {
+    sh.b1 = (uint32_t)tot;
+    sh.b2 = (uint32_t)(tot >> 32);
+  }
+  __syncthreads();
+  const NpCats c{(const double*)(lds + q.off_pp), (const double*)(lds + q.off_q), (const double*)(lds + q.off_lq),
+                 (const uint16_t*)(lds + q.off_cat), lds + q.off_flip, etab};
+  np_draws(p, q, c, sh);
+  __syncthreads();
+  if (t == 0) {
+    q.rng[0] = sh.S[0];
+    q.rng[1] = sh.S[1];
+    q.rng[4] = sh.has;
+    q.rng[5] = sh.uval;
+  }
+}
+
+// Pass 2 of step k: the draws applied, the observations (OH as taxi_rollout: 0 scalar, CS one-hot chunks).
+template <int OH>
+__global__ __launch_bounds__(TPB) void taxi_npg_pass2(TaxiDev p, TaxiNpDev q, NpgDev g, size_t off,
+                                                      void* __restrict__ obs) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  __shared__ uint16_t s_hot[WAVES][256];
+  stage_tables(p, lds);
+  __syncthreads();
+  const int tile = blockIdx.x, env0 = tile * EPB + threadIdx.x * EPT;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint64_t pre = g.bpre[tile];
+  const uint32_t ptc = (uint32_t)pre, prs = (uint32_t)(pre >> 32);
+  uint32_t u[4], rk[4], h[4];
+  ld4_u32(p.st, env0, p.B, u);
+  ld4_u32(reinterpret_cast<const uint32_t*>(q.rk), env0, p.B, rk);
+  const uint16_t* obs_of = l_obs(lds, p);
+#pragma unroll
+  for (int i = 0; i < EPT; ++i) {
+    const int32_t r = (int32_t)rk[i];
+    if (env0 + i < p.B && r >= 0) {
+      if (r & (1 << 30)) {
+        u[i] = q.vrs[prs + (uint32_t)(r & ~(1 << 30))];  // _reset_mask: new start state, elapsed 0, dropoffs 0
+      } else {
+        const int32_t v = q.vtc[ptc + (uint32_t)r];  // encode(r, c, p, d): taxi cell kept
+        const uint32_t s = u[i] & 0xFFFu;
+        const uint32_t s2 = (s / (uint32_t)p.lpl) * (uint32_t)p.lpl + (uint32_t)(v >> 16) * (uint32_t)p.nlocs +
+                            (uint32_t)(v & 0xFFFF);
+        u[i] = (u[i] & ~0xFFFu) | s2;
+      }
+    }
+    h[i] = obs_of[u[i] & 0xFFFu];
+  }
+  st4_u32(p.st, env0, p.B, u);
+  if constexpr (OH == 0) {
+    st4_u32(reinterpret_cast<uint32_t*>(obs) + off, env0, p.B, h);
+  } else {
+    const int we0 = tile * EPB + wid * 256;
+    const int n = min(256, p.B - we0);
+    if (n > 0)
+      write_onehot_wave<OH>((uint8_t*)obs + (off + (size_t)we0) * (size_t)p.n_obs, n, p.n_obs, s_hot[wid], h, lane);
+  }
+}
+
 // ------------------------------------------------------------------ host backend ----
 struct TaxiBackend : EnvBackend {
   TaxiDev d{};
@@ -859,7 +1116,39 @@ struct TaxiBackend : EnvBackend {
     r->uinteger = (uint32_t)r6[5];
     return check();
   }
+  // grid-wide numpy mode (B > npg_min): per step pass 1, the draws, pass 2 (K = 0: reset())
+  NpgDev npg{};
+  DevBuf b_bcnt, b_bpre;
+  int npg_min = NPG_MIN_ENVS;
+  template <int OH>
+  void launch_npg_pass2(size_t off, void* obs, hipStream_t s) {
+    hipLaunchKernelGGL((taxi_npg_pass2<OH>), dim3((unsigned)d.ntiles), dim3(TPB), (size_t)d.tab_bytes, s, d, np, npg,
+                       off, obs);
+  }
+  void launch_npg(int K, const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc, hipStream_t s) {
+    const int cs = one_hot ? chunk_size(obs, K > 0 ? K : 1) : 0;
+    for (int k = 0; k < (K > 0 ? K : 1); ++k) {
+      const size_t off = (size_t)k * (size_t)B;
+      if (K == 0)
+        hipLaunchKernelGGL((taxi_npg_pass1<true>), dim3((unsigned)d.ntiles), dim3(TPB), (size_t)d.tab_bytes, s, d, np,
+                           npg, off, (const int32_t*)act, rew, term, trunc);
+      else
+        hipLaunchKernelGGL((taxi_npg_pass1<false>), dim3((unsigned)d.ntiles), dim3(TPB), (size_t)d.tab_bytes, s, d, np,
+                           npg, off, (const int32_t*)act, rew, term, trunc);
+      hipLaunchKernelGGL(taxi_npg_draws, dim3(1), dim3(NP_TPB), (size_t)np.mtab_bytes, s, d, np, npg, d.ntiles);
+      switch (cs) {
+        case 0: launch_npg_pass2<0>(off, obs, s); break;
+        case 16: launch_npg_pass2<16>(off, obs, s); break;
+        case 4: launch_npg_pass2<4>(off, obs, s); break;
+        default: launch_npg_pass2<1>(off, obs, s); break;
+      }
+    }
+  }
   void launch_np(int K, const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc, hipStream_t s) {
+    if (B > npg_min) {
+      launch_npg(K, act, obs, rew, term, trunc, s);
+      return;
+    }
     const size_t lds = (size_t)d.tab_bytes + (size_t)np.mtab_bytes;
     if (one_hot)
       hipLaunchKernelGGL((taxi_np_kernel<true>), dim3(1), dim3(NP_TPB), lds, s, d, np, K, (const int32_t*)act, obs,
@@ -1254,6 +1543,13 @@ int TaxiBackend::np_build(const std::vector<uint16_t>& valid) {
   np.rk = b_rk.as<int32_t>();
   np.vtc = b_vtc.as<int32_t>();
   np.vrs = b_vrs.as<uint16_t>();
+  if (gp_debug_knobs().taxi_npg_min >= 0) npg_min = gp_debug_knobs().taxi_npg_min;
+  if ((e = b_bcnt.alloc(sizeof(uint32_t) * (size_t)d.ntiles + 16)) ||
+      (e = b_bpre.alloc(sizeof(uint64_t) * (size_t)d.ntiles + 16)))
+    return e;
+  npg.bcnt = b_bcnt.as<uint32_t>();
+  npg.bpre = b_bpre.as<uint64_t>();
+  npg.grid = grid;
   return np_upload_rng();
 }
 

@@ -1,4 +1,5 @@
-"""Seed-identical Taxi (rng_mode="numpy", csrc/taxi.hip taxi_np_kernel) against the reference's fixtures and numpy.
+"""Seed-identical Taxi (rng_mode="numpy", csrc/taxi.hip: taxi_np_kernel up to 1024 envs, the grid-wide taxi_npg_*
+launches above) against the reference's fixtures and numpy.
 
 The fixtures were recorded from the reference's TaxiVecEnv (tests/golden/make_golden.py): reset(seed) and every
 step's obs / reward / terminated / truncated, the final env state and the final np_random PCG64 state. Here the
@@ -126,3 +127,51 @@ def test_numpy_mode_rng_state_roundtrip(gpu_device):
     for x, y in zip(a, b):
         assert torch.equal(x, y)
     assert e1.rng_state == e2.rng_state
+
+
+@pytest.mark.parametrize("name", ["taxi_hansen_b64", "taxi_ext_3pass_rew"])
+def test_numpy_mode_grid_wide_path_on_fixtures(name, gpu_device):
+    """The grid-wide form (pass 1 / draws / pass 2 launches per step, taxi.hip taxi_npg_*) forced on the fixtures'
+    small batches (one partial tile), from the seed, as test_numpy_mode_replays_reference_fixture_from_seed."""
+    from gym_po_amd._lib import debug_knobs
+    with debug_knobs(taxi_npg_min=0):
+        test_numpy_mode_replays_reference_fixture_from_seed(name, gpu_device)
+
+
+@pytest.mark.parametrize("one_hot", [False, True])
+def test_numpy_mode_grid_wide_65536_envs_burst(one_hot, gpu_device):
+    """65,536 envs (64 tiles on the grid-wide path): every env truncates together at step 16 (a 65,536-row
+    multinomial burst), task completions redraw p / d, against the oracle on numpy's Generator; Hansen obs as
+    int32 or as one-hot uint8 rows (checked as argmax + row sums on the device)."""
+    import torch
+    from gym_po_amd import HansenTaxiVecEnv
+    from oracle.taxi import TaxiOracle
+    B, T, kw = 65536, 24, {"time_limit": 15}
+    env = HansenTaxiVecEnv(B, **kw, rng_mode="numpy", one_hot=one_hot, device=gpu_device)
+    ora = TaxiOracle(B, hansen_obs=True, **kw)
+
+    def idx(o):
+        if not one_hot:
+            return o.cpu().numpy().astype(np.int64)
+        assert bool((o.sum(-1) == 1).all())
+        return o.argmax(-1).cpu().numpy().astype(np.int64)
+
+    o0, _ = env.reset(seed=21)
+    np.testing.assert_array_equal(idx(o0), np.asarray(ora.reset_seed(21)).astype(np.int64))
+    acts = np.random.default_rng(4).integers(0, 5, (T, B))
+    eps, t = 0, 0
+    for K in (1, 13, 10):
+        o, r, d, tr = env.rollout(torch.as_tensor(acts[t:t + K].astype(np.int32), device=gpu_device))
+        for j in range(K):
+            ro, rr, rd, rt = ora.step_seeded(acts[t + j])
+            np.testing.assert_array_equal(idx(o[j]), np.asarray(ro).astype(np.int64), err_msg=f"obs t={t + j}")
+            np.testing.assert_array_equal(r[j].cpu().numpy(), rr, err_msg=f"rew t={t + j}")
+            np.testing.assert_array_equal(d[j].cpu().numpy().astype(bool), rd, err_msg=f"term t={t + j}")
+            np.testing.assert_array_equal(tr[j].cpu().numpy().astype(bool), rt, err_msg=f"trunc t={t + j}")
+            eps += int((rd | rt).sum())
+        t += K
+    assert eps >= B
+    env.check()
+    assert _rng6(env.rng_state) == _rng6(ora.gen.bit_generator.state)
+    m = env.metrics()
+    assert m["episodes"] == eps and m["env_steps"] == T * B
