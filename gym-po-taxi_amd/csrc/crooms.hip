@@ -1446,20 +1446,25 @@ __device__ __forceinline__ ZigTabs xg_zig() {
 
 // A block's view of positions [q0 - XG_LOOK, q0 + XGT) (the halo: the slow attempts that can reach into the
 // block): slow bits, spans, flags (bit 0 on-chain, bit 1 accepted) in LDS. Index i = position - (q0 - XG_LOOK).
-constexpr int XGH = XG_LOOK + XGT;
-struct XgView {
-  uint64_t bits[XGH / 64];
-  uint16_t span[XGH];
-  uint8_t flag[XGH];
+template <int NP>  // a view of NP block positions and the XG_LOOK halo before them
+struct XgViewT {
+  static constexpr int H = XG_LOOK + NP;
+  uint64_t bits[H / 64];
+  uint16_t span[H];
+  uint8_t flag[H];
 };
-__device__ __forceinline__ bool xv_slow(const XgView& v, int i) { return (v.bits[i >> 6] >> (i & 63)) & 1ull; }
+using XgView = XgViewT<XGT>;
+constexpr int XGH = XgView::H;
+template <class V>
+__device__ __forceinline__ bool xv_slow(const V& v, int i) { return (v.bits[i >> 6] >> (i & 63)) & 1ull; }
 // The slow positions of view indices [lo, hi) (hi - lo <= 128) as up to three bit words from (lo & ~63).
-__device__ __forceinline__ void xv_window(const XgView& v, int lo, int hi, uint64_t (&m)[3], int& base) {
+template <class V>
+__device__ __forceinline__ void xv_window(const V& v, int lo, int hi, uint64_t (&m)[3], int& base) {
   base = lo & ~63;
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     const int b0 = base + 64 * k;
-    uint64_t w = (b0 < hi && b0 < XGH) ? v.bits[b0 >> 6] : 0ull;
+    uint64_t w = (b0 < hi && b0 < V::H) ? v.bits[b0 >> 6] : 0ull;
     if (b0 < lo) w &= ~0ull << (lo - b0);
     if (b0 + 64 > hi) w &= (hi - b0) <= 0 ? 0ull : ((hi - b0) >= 64 ? ~0ull : ((1ull << (hi - b0)) - 1ull));
     m[k] = w;
@@ -1467,9 +1472,10 @@ __device__ __forceinline__ void xv_window(const XgView& v, int lo, int hi, uint6
 }
 // Whether the slow attempt at view index i is on the chain: back to its cluster's start, then forward. -1: the
 // cluster may reach before the view (never when the view starts before position 0), for xg_on_chain_abs.
-__device__ __forceinline__ int xv_on_chain(const XgView& v, int i, bool at0) {
+template <class V>
+__device__ __forceinline__ int xv_on_chain(const V& v, int i, bool at0) {
   int c = i;
-  for (int hop = 0; hop < XGH; ++hop) {
+  for (int hop = 0; hop < V::H; ++hop) {
     if (c - XG_SPAN < 0 && !at0) return -1;
     uint64_t m[3];
     int base;
@@ -1508,12 +1514,13 @@ __device__ __forceinline__ int xv_on_chain(const XgView& v, int i, bool at0) {
 // The same walk in stream positions for a cluster that reaches before the block's view (a chain of overlapping
 // slow attempts longer than the halo's spare XG_LOOK - XG_SPAN words: rare): positions outside the view are
 // evaluated on the spot (their own jump), inside it read from the view.
-__device__ __noinline__ int xg_on_chain_abs(const XgCall& a, const XgView& v, int q0, const CrRng& s0, int qi) {
+template <class V>
+__device__ __noinline__ int xg_on_chain_abs(const XgCall& a, const V& v, int q0, const CrRng& s0, int qi) {
   const ZigTabs zt = xg_zig();
   const u128 S = mk128(s0.s_hi, s0.s_lo), inc = xg_inc(s0);
   auto slow_at = [&](int p, int& span) -> bool {
     const int i = p - (q0 - XG_LOOK);
-    if (i >= 0 && i < XGH) {
+    if (i >= 0 && i < V::H) {
       if (!xv_slow(v, i)) return false;
       span = v.span[i];
       return true;
@@ -1693,7 +1700,15 @@ __device__ __forceinline__ uint32_t xg_tprefix(const XgCall& a, int bid, int nbl
   return xg_block_sum(x);
 }
 
+// The fused call's blocks cover XG_PPT positions per thread (XGN per block): the per-block fixed latency (entry
+// loads, base states, the publish and the prefix wait, ~20 us) is paid once per XGN positions. At 2^21 envs a call
+// of ~4.7M positions was ~21,800 blocks of 256 whose lifetimes, ~4.5 resident per CU, serialised into ~470 us.
+// (XG_PPT = 1 below XG_PPT_MIN_BLOCKS blocks of XGT positions: small calls keep their parallelism.)
+constexpr int XG_PPT_MIN_BLOCKS = 1024;
+
+template <int XG_PPT>
 __global__ __launch_bounds__(XGT) void xg_norm_fused(XgCall a) {
+  constexpr int XGN = XGT * XG_PPT;
   const int xty = a.nsrc.gs ? 2 : 0;
   XSTAMP(xty, 0);
   const PcgJump myj = a.wj[threadIdx.x + 1];  // (independent of everything: issued first)
@@ -1701,97 +1716,125 @@ __global__ __launch_bounds__(XGT) void xg_norm_fused(XgCall a) {
   const int64_t want = a.xinfo ? (int64_t)xg_vload(a.xinfo + 1) : 0;
   const int64_t n = xg_n(a);
   XSTAMP(xty, 1);
-  const int bid = blockIdx.x, q0 = bid * XGT;
+  const int bid = blockIdx.x, q0 = bid * XGN;
   // the extension's normals past n (the next call's, xg_wall_one)
   const int64_t X = a.xinfo ? min((int64_t)a.xmax, want + want / 4 + 1024) : 0;
-  const int need = min(xg_norm_need(a, n + X), (int)(gridDim.x * XGT));  // (the launch may cap the extension)
+  const int need = min(xg_norm_need(a, n + X), (int)(gridDim.x * XGN));  // (the launch may cap the extension)
   if (n == 0) {  // nothing drawn: the state carries over
     if (bid == 0 && threadIdx.x == 0) a.st[a.wr] = s0;
     return;
   }
   if (q0 >= need) return;
-  __shared__ XgView v;
+  using View = XgViewT<XGN>;
+  __shared__ View v;
   __shared__ uint64_t hb[2];
-  __shared__ uint64_t pmw[XGW];
+  __shared__ uint64_t bb[XG_PPT][2];
+  __shared__ uint64_t pmw[XGN / 64];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  if (t == 64) {  // the halo's base state (wave 1) beside the block's (thread 0, in xg_base_state)
+  {
     const u128 S = mk128(s0.s_hi, s0.s_lo);
-    const u128 h = q0 < XG_LOOK ? (u128)0
-                   : a.hj  ? apply_jump(a.hj[blockIdx.x], S)
-                           : pcg_jump_ilp(a.jt, S, (uint32_t)(q0 - XG_LOOK));
-    hb[0] = hi64(h);
-    hb[1] = lo64(h);
+    if (t == 64) {  // the halo's base state (wave 1) beside the sub-blocks' (threads 0 .. XG_PPT - 1)
+      const u128 h = q0 < XG_LOOK ? (u128)0
+                     : a.hj  ? apply_jump(a.hj[bid * XG_PPT], S)
+                             : pcg_jump_ilp(a.jt, S, (uint32_t)(q0 - XG_LOOK));
+      hb[0] = hi64(h);
+      hb[1] = lo64(h);
+    }
+    if (t < XG_PPT) {  // sub-block m = t: positions q0 + XGT m .. (bj[k] = k XGT steps)
+      const u128 b = a.bj ? apply_jump(a.bj[bid * XG_PPT + t], S) : pcg_jump_ilp(a.jt, S, (uint32_t)(q0 + XGT * t));
+      bb[t][0] = hi64(b);
+      bb[t][1] = lo64(b);
+    }
   }
-  const u128 sb = xg_base_state(a, s0, q0, nullptr);
+  __syncthreads();
   XSTAMP(xty, 2);
   const ZigTabs zt = xg_zig();
   const u128 inc = xg_inc(s0);
-  double val = 0.0, zf = 0.0;
-  int span = 1;
+  double val[XG_PPT], zf[XG_PPT];
+  int span[XG_PPT];
+  // own positions: view index XG_LOOK + XGT m + t; then (t < XG_LOOK) the halo's, view index t
 #pragma unroll
-  for (int part = 0; part < 2; ++part) {
-    if (part == 1 && t >= XG_LOOK) break;  // wave-uniform (XG_LOOK = one wave)
-    const int i = part == 0 ? XG_LOOK + t : t;
+  for (int part = 0; part <= XG_PPT; ++part) {
+    if (part == XG_PPT && t >= XG_LOOK) break;  // wave-uniform (XG_LOOK = one wave)
+    const bool halo = part == XG_PPT;
+    const int i = halo ? t : XG_LOOK + XGT * part + t;
     const int q = q0 - XG_LOOK + i;
     const bool live = q >= 0 && q < need;
-    const u128 X = apply_jump(myj, part == 0 ? sb : mk128(hb[0], hb[1]));
+    const u128 Xs = apply_jump(myj, halo ? mk128(hb[0], hb[1]) : mk128(bb[part][0], bb[part][1]));
     double z;
-    const bool slow = live && !zig_fast(zt, pcg_output(X), z);
-    if (part == 0) zf = z;
+    const bool slow = live && !zig_fast(zt, pcg_output(Xs), z);
+    if (!halo) {
+      zf[part] = z;
+      val[part] = 0.0;
+      span[part] = 1;
+    }
     const uint64_t m = __ballot(slow);
     if (lane == 0) v.bits[i >> 6] = m;
     if (slow) {
       int u = 1;
       double vv = 0.0;
-      const int r = xg_attempt(zt, X, inc, u, vv);
+      const int r = xg_attempt(zt, Xs, inc, u, vv);
       if (r < 0) atomicOr(a.err, GP_DERR_STREAM);
       v.span[i] = (uint16_t)u;
       v.flag[i] = (uint8_t)(r > 0 ? 2u : 0u);
-      if (part == 0) {
-        val = vv;
-        span = u;
+      if (!halo) {
+        val[part] = vv;
+        span[part] = u;
       }
     }
   }
   __syncthreads();
   XSTAMP(xty, 3);
-  const int i = XG_LOOK + t, q = q0 + t;
-  const bool slow = xv_slow(v, i);
-  int on = 0;
-  if (slow && (on = xv_on_chain(v, i, q0 == 0)) < 0) on = xg_on_chain_abs(a, v, q0, s0, q);
+  bool slow[XG_PPT];
+  int on[XG_PPT];
+#pragma unroll
+  for (int m = 0; m < XG_PPT; ++m) {
+    const int i = XG_LOOK + XGT * m + t;
+    slow[m] = xv_slow(v, i);
+    on[m] = 0;
+    if (slow[m] && (on[m] = xv_on_chain(v, i, q0 == 0)) < 0) on[m] = xg_on_chain_abs(a, v, q0, s0, q0 + XGT * m + t);
+  }
   const int ih = XG_SPAN + t;
   int onh = 0;
   const bool slowh = t < XG_LOOK - XG_SPAN && xv_slow(v, ih);
   if (slowh && (onh = xv_on_chain(v, ih, q0 == 0)) < 0) onh = xg_on_chain_abs(a, v, q0, s0, q0 - XG_LOOK + ih);
   __syncthreads();
-  if (slow && on) v.flag[i] |= 1u;
+#pragma unroll
+  for (int m = 0; m < XG_PPT; ++m)
+    if (slow[m] && on[m]) v.flag[XG_LOOK + XGT * m + t] |= 1u;
   if (slowh && onh) v.flag[ih] |= 1u;
   __syncthreads();
   XSTAMP(xty, 4);
-  bool prod;
-  if (q >= need) {
-    prod = false;
-  } else if (slow) {
-    prod = (v.flag[i] & 3u) == 3u;
-  } else {
-    prod = true;
-    uint64_t m[3];
-    int base;
-    xv_window(v, i - XG_SPAN, i, m, base);
+  bool prod[XG_PPT];
+  uint32_t mycnt = 0;
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      uint64_t w = m[k];
-      while (w) {
-        const int p = base + 64 * k + __builtin_ctzll(w);
-        w &= w - 1;
-        if ((v.flag[p] & 1u) && p + (int)v.span[p] > i) prod = false;
+  for (int m = 0; m < XG_PPT; ++m) {
+    const int i = XG_LOOK + XGT * m + t, q = q0 + XGT * m + t;
+    if (q >= need) {
+      prod[m] = false;
+    } else if (slow[m]) {
+      prod[m] = (v.flag[i] & 3u) == 3u;
+    } else {
+      prod[m] = true;
+      uint64_t mw[3];
+      int base;
+      xv_window(v, i - XG_SPAN, i, mw, base);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        uint64_t w = mw[k];
+        while (w) {
+          const int p = base + 64 * k + __builtin_ctzll(w);
+          w &= w - 1;
+          if ((v.flag[p] & 1u) && p + (int)v.span[p] > i) prod[m] = false;
+        }
       }
     }
+    const uint64_t pm = __ballot(prod[m]);
+    if (lane == 0) pmw[(XGT / 64) * m + wv] = pm;
+    mycnt += lane == 0 ? (uint32_t)__builtin_popcountll(pm) : 0u;
   }
-  const uint64_t pm = __ballot(prod);
-  if (lane == 0) pmw[wv] = pm;
-  const uint32_t cnt = xg_block_sum(lane == 0 ? (uint32_t)__builtin_popcountll(pm) : 0u);  // (syncs pmw too)
-  const int nb = (need + XGT - 1) / XGT;
+  const uint32_t cnt = xg_block_sum(mycnt);  // (syncs pmw too)
+  const int nb = (need + XGN - 1) / XGN;
   if (t == 0) xg_tpublish(a, bid, nb, cnt);
   XSTAMP(xty, 5);
   const int64_t pre = xg_tprefix(a, bid, nb);
@@ -1800,22 +1843,33 @@ __global__ __launch_bounds__(XGT) void xg_norm_fused(XgCall a) {
     if (pre + cnt < n) atomicOr(a.err, GP_DERR_STREAM);
     if (X > 0) a.xinfo[0] = (uint32_t)min(X, max((int64_t)0, pre + (int64_t)cnt - n));
   }
-  if (pre >= n + X || !prod) return;
-  uint32_t before = __builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u));
+  if (pre >= n + X) return;
+  uint32_t before = 0;  // produced positions of the block's earlier bitmap words
 #pragma unroll
-  for (int j = 0; j < XGW; ++j) before += j < wv ? (uint32_t)__builtin_popcountll(pmw[j]) : 0u;
-  const int64_t r = pre + before;
-  if (r >= n) {
-    if (r < n + X) {  // the extension: the next call's normals, at its scale, with their end positions
-      a.xdst[r - n] = 0.0 + a.xscale * (slow ? val : zf);
-      a.xend[r - n] = (uint32_t)q + (slow ? (uint32_t)span : 1u);
+  for (int m = 0; m < XG_PPT; ++m) {
+    const int wi = (XGT / 64) * m + wv;  // this position's bitmap word
+    const uint64_t pm = pmw[wi];
+    uint32_t b = before + __builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u));
+    for (int j = 0; j < wi; ++j) b += j >= (XGT / 64) * m ? (uint32_t)__builtin_popcountll(pmw[j]) : 0u;
+    if (prod[m]) {
+      const int q = q0 + XGT * m + t;
+      const int64_t r = pre + b;
+      if (r >= n) {
+        if (r < n + X) {  // the extension: the next call's normals, at its scale, with their end positions
+          a.xdst[r - n] = 0.0 + a.xscale * (slow[m] ? val[m] : zf[m]);
+          a.xend[r - n] = (uint32_t)q + (slow[m] ? (uint32_t)span[m] : 1u);
+        }
+      } else {
+        a.dst[r] = 0.0 + a.scale * (slow[m] ? val[m] : zf[m]);  // numpy: loc + scale * standard_normal
+        if (r == n - 1) {
+          const uint32_t endpos = (uint32_t)q + (slow[m] ? (uint32_t)span[m] : 1u);
+          xg_put_state(a.st, a.wr, s0, pcg_jump_ilp(a.jt, mk128(s0.s_hi, s0.s_lo), endpos), s0.has_u32, s0.uinteger);
+        }
+      }
     }
-    return;
-  }
-  a.dst[r] = 0.0 + a.scale * (slow ? val : zf);  // numpy: loc + scale * standard_normal
-  if (r == n - 1) {
-    const uint32_t endpos = (uint32_t)q + (slow ? (uint32_t)span : 1u);
-    xg_put_state(a.st, a.wr, s0, pcg_jump_ilp(a.jt, mk128(s0.s_hi, s0.s_lo), endpos), s0.has_u32, s0.uinteger);
+    // the words of sub-block m, all waves: the next sub-block's positions come after them
+#pragma unroll
+    for (int j = 0; j < XGT / 64; ++j) before += (uint32_t)__builtin_popcountll(pmw[(XGT / 64) * m + j]);
   }
   XSTAMP(xty, 7);
 }
@@ -2342,11 +2396,14 @@ struct CRoomsBackend : EnvBackend {
       a.xmax = (uint32_t)(2 * B);
       a.xscale = 0.5;
     }
-    unsigned nbp = (unsigned)(xg_P / XGT);
-    if (ext == 1 && a.xinfo) {  // the extension's launch covers up to B / 2 normals past n (a 25% wall-hit rate)
+    // positions the launch covers (the extension's launch up to B / 2 normals past n: a 25% wall-hit rate)
+    int64_t npos = xg_P;
+    if (ext == 1 && a.xinfo) {
       const int64_t nx = n_host + B / 2;
-      nbp = (unsigned)std::min<int64_t>(nbp, (nx + nx / 16 + 4096 + XGT - 1) / XGT);
+      npos = std::min<int64_t>(npos, nx + nx / 16 + 4096);
     }
+    const int ppt = xg_fused() && (npos + XGT - 1) / XGT > XG_PPT_MIN_BLOCKS ? 4 : 1;  // positions per thread
+    const unsigned nbp = (unsigned)((npos + XGT * ppt - 1) / (XGT * ppt));
     if (ext == 2 && a.xinfo) {
       hipLaunchKernelGGL(xg_wall_one, dim3(1), dim3(XT), 0, s, a, xd);
     } else if (!xg_fused()) {
@@ -2358,7 +2415,8 @@ struct CRoomsBackend : EnvBackend {
       a.tacc = xg_tacc.as<unsigned long long>();
       if (++xg_tag == 0) xg_tag = 1;  // (a wrapped tag could only meet slots 2^32 launches old)
       a.tag = xg_tag;
-      hipLaunchKernelGGL(xg_norm_fused, dim3(nbp), dim3(XGT), 0, s, a);
+      if (ppt == 4) hipLaunchKernelGGL(xg_norm_fused<4>, dim3(nbp), dim3(XGT), 0, s, a);
+      else hipLaunchKernelGGL(xg_norm_fused<1>, dim3(nbp), dim3(XGT), 0, s, a);
     }
     xg_slot ^= 1;
     GP_HIP_CHECK(hipGetLastError());
