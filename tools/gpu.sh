@@ -134,7 +134,7 @@ case "$task" in
       python3 tools/pmc_to_json.py $O/$n $k $c $O/$n.json $w $K
       cp $O/$n.json profiles/${R}_pmc_${c}_K${K}.json
     }
-    pm fr128 wgrid_rollout fourrooms_hansen4_B1048576_numpy fourrooms 128 --steps 1280 --warmup 256 --chunk 128
+    pm fr128 grid_rollout_numpy fourrooms_hansen4_B1048576_numpy fourrooms 128 --steps 1280 --warmup 256 --chunk 128
     pm taxi taxi_rollout taxi_B4194304_philox taxi 4 --workload taxi
     pm anttag anttag_rollout anttag_B2097152_philox anttag 64 --workload anttag
     pm crooms crooms_rollout crooms_B2097152_philox crooms 128 --workload crooms
