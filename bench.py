@@ -399,8 +399,9 @@ def main():
     t0 = time.perf_counter()
     run(args.steps)
     torch.cuda.synchronize(dev)
-    barrier()
-    torch.cuda.synchronize(dev)
+    if world > 1:  # (one rank: the barrier is a no-op and a second synchronize would only time an idle device)
+        barrier()
+        torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     tmax = shard.max_over_ranks(elapsed, dev)
 
