@@ -356,6 +356,9 @@ def main():
     shard.seed_shard(env, 0, rank, world)  # shard g: SeedSequence(0, spawn_key=(g,))
     env.reset()
     C = max(1, min(args.chunk, args.steps))
+    # numpy-mode FourRooms: the faster of the two bit-identical kernels for C-step launches on this board, timed
+    # on scratch state by the library before anything is timed here (gp_autotune; -1 elsewhere: a no-op)
+    tuned = env.autotune(C) if hasattr(env, "autotune") else -1
     g = torch.Generator(device=dev)
     g.manual_seed(1 + rank)
     if W["n_actions"] is None:  # continuous (y, x) actions, float32 U[-1, 1]^2
@@ -494,7 +497,8 @@ def main():
             "counter-based Philox draws from the reference's exact laws"),
         "config": {"workload": W["desc"].format(B=B),
                    "envs_per_gpu": B, "global_envs": args.envs if args.strong else B * world, "rng_mode": args.mode,
-                   "parallelism": f"independent env shards x{world}", "steps_per_launch_call": C},
+                   "parallelism": f"independent env shards x{world}", "steps_per_launch_call": C,
+                   "kernel_autotune": {1: "windowed", 0: "fused", -1: None}[tuned]},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "byte_model": (f"SURVEY 8(d): {W['bytes']} B per env-step + {W['state']} B per env per launch "

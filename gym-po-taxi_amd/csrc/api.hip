@@ -451,6 +451,11 @@ int gp_check(gp_env* env) {
   return env->be->check();
 }
 
+int gp_autotune(gp_env* env, int K, int reps, int* chosen) {
+  GP_REQUIRE_ENV();
+  return env->be->autotune(K, reps, chosen);
+}
+
 int gp_query(const gp_env* env, const char* key, int64_t* value) {
   if (!env || !env->be || !key || !value) {
     gp_set_error("gp_query: null argument");

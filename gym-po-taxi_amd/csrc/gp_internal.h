@@ -94,6 +94,11 @@ struct EnvBackend {
     return GP_OK;
   }
   virtual int debug_stamps(unsigned long long* out, int cap) { return 0; }
+  // gp_autotune: pick the faster of interchangeable kernels for K-step launches on this device (no-op here)
+  virtual int autotune(int K, int reps, int* chosen) {
+    if (chosen) *chosen = -1;
+    return GP_OK;
+  }
   virtual int reset_distribution(double* out, int cap) const {
     gp_set_error("no reset distribution for this env kind");
     return GP_E_UNSUPPORTED;

@@ -2786,6 +2786,7 @@ struct GridBackend : EnvBackend {
     return (int)v.size();
   }
   int metrics(double out[4]) override;
+  int autotune(int K, int reps, int* chosen) override;
 #ifdef GP_STAMPS
   int debug_stamps(unsigned long long* out, int cap) override {
     GP_HIP_CHECK(hipDeviceSynchronize());
@@ -3209,6 +3210,86 @@ int GridBackend::step(const void* act, void* obs, float* rew, uint8_t* term, uin
   if (e) return e;
   GP_HIP_CHECK(hipGetLastError());
   return GP_OK;
+}
+
+// Uniform random actions for gp_autotune's scratch launches (a hash of the index; any action mix will do).
+__global__ void autotune_actions(int32_t* a, size_t n, int nact) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    uint64_t x = (uint64_t)i * 0x9E3779B97F4A7C15ull;
+    x ^= x >> 31;
+    x *= 0xBF58476D1CE4E5B9ull;
+    x ^= x >> 29;
+    a[i] = (int32_t)((x >> 32) % (uint64_t)nact);
+  }
+}
+
+// Times `reps` K-step launches of the windowed and of the fused kernel on scratch actions / outputs, each from
+// the handle's current state, which is restored exactly afterwards (agent cells + elapsed, the stream and the
+// kernels' control block, the metric slots; both kernels' granule slots cleared, as allocated: tags are never 0).
+// Launches of K steps then go to the faster one (wg_kmax). Their results are identical; which one is faster at
+// short launches differs between MI355X boards (profiles/r05_ab_kernel_by_K.txt).
+int GridBackend::autotune(int K, int reps, int* chosen) {
+  if (chosen) *chosen = -1;
+  if (rng_mode != GP_RNG_NUMPY || !wg_G || !fused_G || B % 4 != 0 || K < 1) return GP_OK;
+  if (!has_reset) {
+    gp_set_error("autotune() before reset()");
+    return GP_E_STATE;
+  }
+  reps = std::max(1, std::min(reps, 64));
+  GP_HIP_CHECK(hipDeviceSynchronize());
+  const size_t nb = (size_t)B, kb = (size_t)K * nb;
+  DevBuf s_ae, s_ms, a, o, r, t, u;
+  GridCtl ctl_h;
+  int e;
+  if ((e = s_ae.alloc(4 * nb)) || (e = s_ms.alloc(b_mslot.n)) || (e = a.alloc(4 * kb)) || (e = o.alloc(4 * kb)) ||
+      (e = r.alloc(4 * kb)) || (e = t.alloc(kb)) || (e = u.alloc(kb)))
+    return e;
+  GP_HIP_CHECK(hipMemcpy(s_ae.p, d.ae, 4 * nb, hipMemcpyDeviceToDevice));
+  GP_HIP_CHECK(hipMemcpy(s_ms.p, d.mslot, b_mslot.n, hipMemcpyDeviceToDevice));
+  GP_HIP_CHECK(hipMemcpy(&ctl_h, d.ctl, sizeof(GridCtl), hipMemcpyDeviceToHost));
+  hipLaunchKernelGGL(autotune_actions, dim3(1024), dim3(256), 0, 0, a.as<int32_t>(), kb, d.nact);
+  GP_HIP_CHECK(hipGetLastError());
+  auto restore = [&]() -> int {
+    GP_HIP_CHECK(hipDeviceSynchronize());
+    GP_HIP_CHECK(hipMemcpy(d.ae, s_ae.p, 4 * nb, hipMemcpyDeviceToDevice));
+    GP_HIP_CHECK(hipMemcpy(d.mslot, s_ms.p, b_mslot.n, hipMemcpyDeviceToDevice));
+    GP_HIP_CHECK(hipMemcpy(d.ctl, &ctl_h, sizeof(GridCtl), hipMemcpyHostToDevice));
+    GP_HIP_CHECK(hipMemset(b_wslots.p, 0, b_wslots.n));
+    GP_HIP_CHECK(hipMemset(b_fslot.p, 0, b_fslot.n));
+    GP_HIP_CHECK(hipDeviceSynchronize());
+    return GP_OK;
+  };
+  const bool timer_on = timer.on;
+  timer.on = false;
+  hipEvent_t e0, e1;
+  GP_HIP_CHECK(hipEventCreate(&e0));
+  GP_HIP_CHECK(hipEventCreate(&e1));
+  float ms[2] = {0.f, 0.f};
+  for (int c = 0; c < 2 && !e; ++c) {
+    auto one = [&]() -> int {
+      if (c == 0) return launch_wgrid(K, a.p, o.p, r.as<float>(), t.as<uint8_t>(), u.as<uint8_t>(), 0);
+      return dispatch_obs(d.obs_kind, [&](auto okc) -> int {
+        constexpr int OK = decltype(okc)::value;
+        return launch_fused<OK>(K, a.p, o.p, r.as<float>(), t.as<uint8_t>(), u.as<uint8_t>(), 0);
+      });
+    };
+    if ((e = one())) break;  // warm
+    if (hipEventRecord(e0, 0) != hipSuccess) e = GP_E_HIP;
+    for (int i = 0; i < reps && !e; ++i) e = one();
+    if (!e && (hipEventRecord(e1, 0) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
+               hipEventElapsedTime(&ms[c], e0, e1) != hipSuccess))
+      e = GP_E_HIP;
+    if (int e2 = restore()) e = e ? e : e2;
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  timer.on = timer_on;
+  if (e) return e;
+  const bool wgrid_faster = ms[0] <= ms[1];
+  if (wgrid_faster) wg_kmax = std::max(wg_kmax, K);
+  else wg_kmax = std::min(wg_kmax, K - 1);
+  if (chosen) *chosen = wgrid_faster ? 1 : 0;
+  return check();
 }
 
 int GridBackend::rollout(int K, const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc,

@@ -87,6 +87,7 @@ SIGNATURES = {
     "gp_valid_cells": (ctypes.c_int, [_vp, ctypes.c_int, _i32p, ctypes.c_int]),
     "gp_metrics": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double)]),
     "gp_check": (ctypes.c_int, [_vp]),
+    "gp_autotune": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     "gp_query": (ctypes.c_int, [_vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)]),
     "gp_taxi_reset_distribution": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
     "gp_taxi_render": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _vp, ctypes.POINTER(ctypes.c_int32), _vp]),

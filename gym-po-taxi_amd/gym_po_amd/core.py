@@ -273,6 +273,15 @@ class NativeVecEnv:
             return keep.bufs
         return run, (out[0], out[1], out[2].view(torch.bool), out[3].view(torch.bool))
 
+    def autotune(self, K=20, reps=5):
+        """Pick, on this device, the faster of the handle's interchangeable kernels for launches of K steps
+        (numpy-mode FourRooms/ROOMS: the windowed and the fused kernel, bit-identical results) by timing `reps`
+        launches of each on scratch state; the env's own state, stream position and metrics are left exactly as
+        they were. Returns 1 (windowed), 0 (fused) or -1 (nothing to choose). After reset(); syncs."""
+        chosen = ctypes.c_int(-1)
+        check(lib().gp_autotune(self._handle, int(K), int(reps), ctypes.byref(chosen)), "gp_autotune")
+        return chosen.value
+
     def check(self):
         """Sync and raise GymPoError if a device-side failure hit any launch since the last seed (the
         asynchronous step/rollout calls cannot report it themselves; metrics() and rng_state check too)."""

@@ -218,6 +218,13 @@ int gp_metrics(gp_env* env, double out[4]);
  * asynchronous step/rollout calls cannot report such failures themselves; gp_metrics and
  * gp_get_rng_state run the same check. (No reference counterpart: numpy steps are synchronous.) */
 int gp_check(gp_env* env);
+/* Chooses, on this handle's device, the faster of interchangeable kernels for launches of K steps. Numpy-mode GRID
+ * with both the windowed (wgrid_rollout) and the fused (grid_rollout_numpy) kernel eligible: their results are
+ * identical, and which is faster at short launches differs between MI355X boards. Times `reps` K-step launches of
+ * each on scratch actions / outputs from the current state, restores that state exactly (env state, stream
+ * state, metrics), and sends K-step launches to the faster. *chosen (host, may be NULL) = 1 windowed, 0 fused,
+ * -1 not applicable (other kinds / modes: a no-op). After gp_reset; syncs. (No reference counterpart.) */
+int gp_autotune(gp_env* env, int K, int reps, int* chosen);
 /* Introspection of a handle (host-only, no sync): key = "num_envs", "rng_mode", and for GRID
  * "fused_blocks" (persistent grid size of the fused numpy rollout, 0 = not eligible),
  * "fused_tiles_per_block", "fused_staged" (1 = LDS-staged outputs + store waves),

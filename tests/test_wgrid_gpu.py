@@ -238,3 +238,27 @@ def test_wgrid_schedule_variants_bit_exact(tmode, gpu_device):
     ora = gridworld.FourRoomsOracle(B, 1, obs_type="hansen")
     np.testing.assert_array_equal(_reset_obs(env, 23).astype(np.int64), np.asarray(ora.reset_seed(23)).astype(np.int64))
     _check_chunks(env, ora, (7, 12), action_seed=2, n_act=4)
+
+
+def test_autotune_leaves_the_state_exactly(gpu_device):
+    """gp_autotune times both kernels on scratch state and restores the handle's: a tuned env and an untuned one
+    from the same seed give identical outputs, state, metrics and PCG64 state afterwards, over launches of the
+    tuned length and others."""
+    import torch
+    B = 1 << 18
+    e1, e2 = _fourrooms(B, gpu_device), _fourrooms(B, gpu_device)
+    o1, o2 = _reset_obs(e1, 12), _reset_obs(e2, 12)
+    acts = torch.randint(0, 4, (45, B), device=gpu_device, dtype=torch.int32)
+    e1.rollout(acts[:5])
+    e2.rollout(acts[:5])
+    chosen = e1.autotune(20, reps=3)
+    assert chosen in (0, 1)
+    assert (e1.query("wgrid_kmax") >= 20) == (chosen == 1)
+    for a, b in ((5, 25), (25, 26), (26, 45)):
+        r1, r2 = e1.rollout(acts[a:b]), e2.rollout(acts[a:b])
+        for x, y in zip(r1, r2):
+            assert torch.equal(x, y)
+    assert e1.rng_state == e2.rng_state
+    assert e1.metrics() == e2.metrics()
+    for x, y in zip(e1.get_state(), e2.get_state()):
+        assert torch.equal(x, y)
