@@ -1705,6 +1705,8 @@ __device__ __forceinline__ uint32_t xg_tprefix(const XgCall& a, int bid, int nbl
 // of ~4.7M positions was ~21,800 blocks of 256 whose lifetimes, ~4.5 resident per CU, serialised into ~470 us.
 // (XG_PPT = 1 below XG_PPT_MIN_BLOCKS blocks of XGT positions: small calls keep their parallelism.)
 constexpr int XG_PPT_MIN_BLOCKS = 1024;
+// The env kernels (xg_dry, xg_step) likewise take 4 env blocks per workgroup above this many env blocks.
+constexpr int XG_SPB_MIN_BLOCKS = 1024;
 
 template <int XG_PPT>
 __global__ __launch_bounds__(XGT) void xg_norm_fused(XgCall a) {
@@ -2100,116 +2102,138 @@ __global__ __launch_bounds__(XGT) void xg_uniforms(XgCall a, uint64_t* __restric
 }
 
 // Dry step on copies: which envs hit a wall (the wall-noise draw count, crooms.py:321-325) -> fd.
-template <int OK>
 // Round 4: the previous step's resets (fr: its resetting envs, gi / ai their draws, obs_prev its observation row)
 // are applied here first, as xg_apply_resets would (one launch per step fewer); fr.bits == nullptr: none pending.
+// SPB env blocks (of XGT envs: the unit of the flag bitmaps and counts) per workgroup, in turn: large batches
+// pay the per-workgroup latency (table staging, the prefix loads) once per SPB blocks; nsub = env blocks in all.
+template <int OK, int SPB>
 __global__ __launch_bounds__(XGT) void xg_dry(CrDev p, XgFlags fd, const void* __restrict__ act, size_t off,
                                               XgFlags fr, const int32_t* __restrict__ gi,
-                                              const int32_t* __restrict__ ai, void* __restrict__ obs_prev) {
+                                              const int32_t* __restrict__ ai, void* __restrict__ obs_prev, int nsub) {
   XSTAMP(1, 0);
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const int bid = blockIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  // the block's reset bitmap words, lane-indexed (vector loads: the previous step's kernel wrote them)
-  uint64_t rw = 0;
-  if (fr.bits && lane < XGW) rw = fr.bits[(size_t)bid * XGW + lane];
-  uint64_t any = 0, mine = 0;
-  uint32_t before = 0;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int sb0 = blockIdx.x * SPB;
+  // the env blocks' reset bitmap words, lane-indexed (vector loads: the previous step's kernel wrote them)
+  uint64_t rw[SPB];
+  uint64_t anyb = 0;
 #pragma unroll
-  for (int j = 0; j < XGW; ++j) {
-    const uint64_t x = __shfl(rw, j, 64);
-    any |= x;
-    if (j < wv) before += (uint32_t)__builtin_popcountll(x);
-    if (j == wv) mine = x;
+  for (int b = 0; b < SPB; ++b) {
+    rw[b] = 0;
+    if (fr.bits && lane < XGW && sb0 + b < nsub) rw[b] = fr.bits[(size_t)(sb0 + b) * XGW + lane];
+    anyb |= rw[b];
   }
   for (int i = threadIdx.x; i < p.tab_bytes / 16; i += XGT) ((uint4*)lds)[i] = ((const uint4*)p.tabs)[i];
   uint32_t pre = 0;
-  if (any) pre = xg_prefix(fr.c, bid);  // block-uniform (its block sum syncs the table copy too)
+  const bool any = __syncthreads_or(anyb != 0ull);
+  if (any) pre = xg_prefix(fr.c, sb0);  // block-uniform (its block sum syncs the table copy too)
   __syncthreads();
-  before += (uint32_t)__builtin_popcountll(mine & ((1ull << lane) - 1ull));
-  const bool rf = (mine >> lane) & 1ull;
-  const int env = bid * XGT + threadIdx.x;
-  bool f = false;
-  if (env < p.B) {
-    double a0, a1;
-    int ad;
-    x_load_action(p, act, off, env, a0, a1, ad);
-    double ay, ax, vy, vx;
-    uint32_t g;
-    if (rf) {  // crooms.py:217-244 with the previous step's draws (as xg_apply_resets)
-      const int r = (int)(pre + before);
-      Draws d;
-      d.k53 = 0;
-      d.gi = p.goal_fixed ? 0u : (uint32_t)gi[r];
-      d.ai = p.agent_fixed ? 0u : (uint32_t)ai[r];
-      g = x_goal(p, env);
-      reset_env(p, lds, d, ay, ax, vy, vx, g);
-      vy = vx = 0.0;
-      p.ay[env] = ay;
-      p.ax[env] = ax;
-      if (p.use_velocity) { p.vy[env] = 0.0; p.vx[env] = 0.0; }
-      if (!p.goal_fixed) p.goal[env] = g;
-      write_obs<OK>(p, lds, env, ay, ax, g, obs_prev);
-    } else {
-      ay = p.ay[env];
-      ax = p.ax[env];
-      vy = p.use_velocity ? p.vy[env] : 0.0;
-      vx = p.use_velocity ? p.vx[env] : 0.0;
-      g = x_goal(p, env);
+#pragma unroll
+  for (int b = 0; b < SPB; ++b) {
+    const int bid = sb0 + b;
+    if (bid >= nsub) break;  // block-uniform
+    uint64_t mine = 0;
+    uint32_t before = 0;
+#pragma unroll
+    for (int j = 0; j < XGW; ++j) {
+      const uint64_t x = __shfl(rw[b], j, 64);
+      if (j < wv) before += (uint32_t)__builtin_popcountll(x);
+      if (j == wv) mine = x;
     }
-    int32_t el = p.el[env];
-    float rs = 0.f;
-    uint32_t ep = 0, ln = 0;
-    const StepOut o = crooms_env_step<true>(p, lds, env, true, 0, a0, a1, ad, ay, ax, vy, vx, g, el, rs, ep, ln);
-    f = o.oob != 0;
+    before += (uint32_t)__builtin_popcountll(mine & ((1ull << lane) - 1ull));
+    const bool rf = (mine >> lane) & 1ull;
+    const int env = bid * XGT + threadIdx.x;
+    bool f = false;
+    if (env < p.B) {
+      double a0, a1;
+      int ad;
+      x_load_action(p, act, off, env, a0, a1, ad);
+      double ay, ax, vy, vx;
+      uint32_t g;
+      if (rf) {  // crooms.py:217-244 with the previous step's draws (as xg_apply_resets)
+        const int r = (int)(pre + before);
+        Draws d;
+        d.k53 = 0;
+        d.gi = p.goal_fixed ? 0u : (uint32_t)gi[r];
+        d.ai = p.agent_fixed ? 0u : (uint32_t)ai[r];
+        g = x_goal(p, env);
+        reset_env(p, lds, d, ay, ax, vy, vx, g);
+        vy = vx = 0.0;
+        p.ay[env] = ay;
+        p.ax[env] = ax;
+        if (p.use_velocity) { p.vy[env] = 0.0; p.vx[env] = 0.0; }
+        if (!p.goal_fixed) p.goal[env] = g;
+        write_obs<OK>(p, lds, env, ay, ax, g, obs_prev);
+      } else {
+        ay = p.ay[env];
+        ax = p.ax[env];
+        vy = p.use_velocity ? p.vy[env] : 0.0;
+        vx = p.use_velocity ? p.vx[env] : 0.0;
+        g = x_goal(p, env);
+      }
+      int32_t el = p.el[env];
+      float rs = 0.f;
+      uint32_t ep = 0, ln = 0;
+      const StepOut o = crooms_env_step<true>(p, lds, env, true, 0, a0, a1, ad, ay, ax, vy, vx, g, el, rs, ep, ln);
+      f = o.oob != 0;
+    }
+    xg_flag_block(fd, bid, nsub, f);
+    // the next env block's resets follow this one's (its count, published by the previous step's kernel)
+    if (any && b + 1 < SPB && bid + 1 < nsub) pre += fr.c.bc[bid];
   }
-  xg_flag_block(fd, blockIdx.x, gridDim.x, f);
   XSTAMP(1, 7);
 }
 
 // The step with the wall noise in place (crooms.py:276-298; an env that hits a wall reads pair r of the wall
-// noise, r = its rank among fd's envs), resets deferred -> fs.
-template <int OK>
+// noise, r = its rank among fd's envs), resets deferred -> fs. SPB env blocks per workgroup, as xg_dry.
+template <int OK, int SPB>
 __global__ __launch_bounds__(XGT) void xg_step(CrDev p, XgFlags fd, XgFlags fs, const void* __restrict__ act,
                                                size_t off, void* __restrict__ obs, float* __restrict__ rew,
-                                               uint8_t* __restrict__ term, uint8_t* __restrict__ trunc) {
+                                               uint8_t* __restrict__ term, uint8_t* __restrict__ trunc, int nsub) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   XSTAMP(3, 0);
   for (int i = threadIdx.x; i < p.tab_bytes / 16; i += XGT) ((uint4*)lds)[i] = ((const uint4*)p.tabs)[i];
-  const int bid = blockIdx.x;
-  const uint32_t wpre = xg_prefix(fd.c, bid);  // (its block sum syncs the table copy too)
+  const int sb0 = blockIdx.x * SPB;
+  uint32_t wpre = xg_prefix(fd.c, sb0);  // (its block sum syncs the table copy too)
   XSTAMP(3, 1);
-  uint32_t wbefore;
-  xg_block_bit(fd.bits + (size_t)bid * XGW, wbefore);
-  const int env = bid * XGT + threadIdx.x;
-  bool f = false;
   float rsum = 0.f;
   uint32_t eps = 0, lens = 0, nst = 0;
-  if (env < p.B) {
-    double a0, a1;
-    int ad;
-    x_load_action(p, act, off, env, a0, a1, ad);
-    double ay = p.ay[env], ax = p.ax[env];
-    double vy = p.use_velocity ? p.vy[env] : 0.0, vx = p.use_velocity ? p.vx[env] : 0.0;
-    uint32_t g = x_goal(p, env);
-    int32_t el = p.el[env];
-    const StepOut o = crooms_env_step<true, true>(p, lds, env, true, 0, a0, a1, ad, ay, ax, vy, vx, g, el, rsum, eps,
-                                                  lens, (int)(wpre + wbefore));
-    nst = 1;
-    rew[off + env] = o.rew;
-    term[off + env] = o.term;
-    trunc[off + env] = o.trunc;
-    f = (o.term | o.trunc) != 0;
-    if (!f) {
-      write_obs<OK>(p, lds, env, ay, ax, g, obs);
-      p.ay[env] = ay;
-      p.ax[env] = ax;
-      if (p.use_velocity) { p.vy[env] = vy; p.vx[env] = vx; }
+#pragma unroll
+  for (int b = 0; b < SPB; ++b) {
+    const int bid = sb0 + b;
+    if (bid >= nsub) break;  // block-uniform
+    uint32_t wbefore;
+    xg_block_bit(fd.bits + (size_t)bid * XGW, wbefore);
+    const int env = bid * XGT + threadIdx.x;
+    bool f = false;
+    if (env < p.B) {
+      double a0, a1;
+      int ad;
+      x_load_action(p, act, off, env, a0, a1, ad);
+      double ay = p.ay[env], ax = p.ax[env];
+      double vy = p.use_velocity ? p.vy[env] : 0.0, vx = p.use_velocity ? p.vx[env] : 0.0;
+      uint32_t g = x_goal(p, env);
+      int32_t el = p.el[env];
+      const StepOut o = crooms_env_step<true, true>(p, lds, env, true, 0, a0, a1, ad, ay, ax, vy, vx, g, el, rsum,
+                                                    eps, lens, (int)(wpre + wbefore));
+      nst += 1;
+      rew[off + env] = o.rew;
+      term[off + env] = o.term;
+      trunc[off + env] = o.trunc;
+      f = (o.term | o.trunc) != 0;
+      if (!f) {
+        write_obs<OK>(p, lds, env, ay, ax, g, obs);
+        p.ay[env] = ay;
+        p.ax[env] = ax;
+        if (p.use_velocity) { p.vy[env] = vy; p.vx[env] = vx; }
+      }
+      p.el[env] = el;
     }
-    p.el[env] = el;
+    xg_flag_block(fs, bid, nsub, f);
+    if (b + 1 < SPB && bid + 1 < nsub) wpre += fd.c.bc[bid];  // the next env block's wall hits follow this one's
   }
-  xg_flag_block(fs, bid, gridDim.x, f);
   XSTAMP(3, 2);
-  // episode statistics: block reduction, one set of atomics per block into slot 0
+  // episode statistics: block reduction, one set of atomics per workgroup
   __shared__ float m_r[XGW];
   __shared__ uint32_t m_e[XGW], m_l[XGW], m_n[XGW];
 #pragma unroll
@@ -2226,7 +2250,7 @@ __global__ __launch_bounds__(XGT) void xg_step(CrDev p, XgFlags fd, XgFlags fs, 
     float r = 0.f;
     uint32_t ee = 0, l = 0, nn = 0;
     for (int i = 0; i < XGW; ++i) { r += m_r[i]; ee += m_e[i]; l += m_l[i]; nn += m_n[i]; }
-    CrSlot& m = p.mslot[bid % p.nslot];  // (one slot for every block serialised up to 6 us of atomics)
+    CrSlot& m = p.mslot[blockIdx.x % p.nslot];  // (one slot for every block serialised up to 6 us of atomics)
     atomicAdd(&m.return_sum, (double)r);
     atomicAdd(&m.episodes, (unsigned long long)ee);
     atomicAdd(&m.length_sum, (unsigned long long)l);
@@ -3011,16 +3035,26 @@ int CRoomsBackend::xg_rollout(int K, const void* act, void* obs, float* rew, uin
     // the dry step: which envs hit a wall; their noise normal(0.5, (n_oob, 2)) (crooms.py:321-325)
     e = dispatch_obs(d.obs_kind, [&](auto okc) -> int {
       constexpr int OK = decltype(okc)::value;
-      hipLaunchKernelGGL(xg_dry<OK>, dim3(nbe), dim3(XGT), d.tab_bytes, s, dd, fd, act, off, k ? fs : XgFlags{},
-                         (const int32_t*)xd.gi, (const int32_t*)xd.ai, k ? (void*)(ob - B * osz) : nullptr);
+      const XgFlags fr = k ? fs : XgFlags{};
+      void* op = k ? (void*)(ob - B * osz) : nullptr;
+      if (nbe > XG_SPB_MIN_BLOCKS)
+        hipLaunchKernelGGL((xg_dry<OK, 4>), dim3((nbe + 3) / 4), dim3(XGT), d.tab_bytes, s, dd, fd, act, off, fr,
+                           (const int32_t*)xd.gi, (const int32_t*)xd.ai, op, (int)nbe);
+      else
+        hipLaunchKernelGGL((xg_dry<OK, 1>), dim3(nbe), dim3(XGT), d.tab_bytes, s, dd, fd, act, off, fr,
+                           (const int32_t*)xd.gi, (const int32_t*)xd.ai, op, (int)nbe);
       return GP_OK;
     });
     if (e || (e = xg_normals(0, 1, 2, 0.5, xd.wall, s, noise ? 2 : 0))) return e;
     // the step itself with the wall noise in place, resets deferred; then the resetting envs' goals / agents
     e = dispatch_obs(d.obs_kind, [&](auto okc) -> int {
       constexpr int OK = decltype(okc)::value;
-      hipLaunchKernelGGL(xg_step<OK>, dim3(nbe), dim3(XGT), d.tab_bytes, s, dd, fd, fs, act, off, (void*)ob, rew,
-                         term, trunc);
+      if (nbe > XG_SPB_MIN_BLOCKS)
+        hipLaunchKernelGGL((xg_step<OK, 4>), dim3((nbe + 3) / 4), dim3(XGT), d.tab_bytes, s, dd, fd, fs, act, off,
+                           (void*)ob, rew, term, trunc, (int)nbe);
+      else
+        hipLaunchKernelGGL((xg_step<OK, 1>), dim3(nbe), dim3(XGT), d.tab_bytes, s, dd, fd, fs, act, off, (void*)ob,
+                           rew, term, trunc, (int)nbe);
       return GP_OK;
     });
     if (e) return e;

@@ -84,6 +84,8 @@ ORACLE_CASES = [
     ({"obs_type": "vector_goal_mdp", "goal_xy": None, "use_velocity": True, "time_limit": 25}, 30001, 30, 3),
     ({"obs_type": "hansen8", "action_type": "ordinal", "layout": "16", "goal_xy": None, "time_limit": 20}, 20000, 25, 5),
     ({"obs_type": "grid", "action_type": "cardinal", "action_std": 0.0, "time_limit": 9}, 8193, 20, 20),
+    # 1,026 env blocks: the env kernels' 4-block workgroups with a partial last one; time-limit resets
+    ({"obs_type": "vector_mdp", "action_std": 0.5, "time_limit": 4}, 262444, 10, 5),
     # BASELINE configs[4]'s size: 2^21 envs (4M normals per step, ~1e3 tail normals, wall resamples)
     ({"obs_type": "vector_mdp"}, 1 << 21, 4, 2),
 ]
