@@ -152,9 +152,9 @@ case "$task" in
     done
     run 200 $O/lat.log python -u tools/latency_probe.py ${@:-1048576 1 20 128}
     grep "B=" $O/lat.log ;;
-  multi)
+  multi)  # 2 ranks share ONE GPU here: the persistent kernels of both must be co-resident (131072 envs each)
     GP_BENCH_BACKEND=gloo run 300 $O/multi2.log python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
-      --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 256 --warmup 128 --envs 262144 --no-cpu-baseline
+      --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 256 --warmup 128 --envs 131072 --no-cpu-baseline
     grep '"metric"' $O/multi2.log | cut -c1-900 ;;
   *)
     echo "unknown task '$task'"; exit 2 ;;
