@@ -114,3 +114,11 @@ print(f"  gather done - last publish                   median {np.median(x[:, :,
 rep("store: copy issue (13->14)", x[:, :, 14] - x[:, :, 13])
 print("block 0, step 10 (ns from env start):", (a[0, 10] - a[0, 10, 0]).tolist())
 print("median over blocks and steps of stamp i - env start (ns):", np.median(x - x[:, :, :1], axis=(0, 1)).astype(int).tolist())
+# per-XCD phase (blocks beta with beta % 8 = x: round-robin dispatch puts them on XCD x), median over steps of the
+# block's stamp minus the step's earliest env start over all blocks
+st0 = x[:, :, 0].min(0)[None]
+print("per XCD (beta % 8), median ns after the step's earliest env start: env start / transitions done / publish / gather done / cells")
+for xcd in range(8):
+    sel = np.arange(G) % 8 == xcd
+    vals = [np.median(x[sel, :, i] - st0) for i in (0, 1, 8, 9, 10)]
+    print(f"  XCD {xcd}: " + " / ".join(f"{v:6.0f}" for v in vals) + f"   transitions {np.median(x[sel, :, 1] - x[sel, :, 0]):5.0f}")
