@@ -262,3 +262,13 @@ def test_autotune_leaves_the_state_exactly(gpu_device):
     assert e1.metrics() == e2.metrics()
     for x, y in zip(e1.get_state(), e2.get_state()):
         assert torch.equal(x, y)
+
+
+def test_autotune_is_a_no_op_where_there_is_nothing_to_choose(gpu_device):
+    """Other kinds and modes have one kernel per launch length: gp_autotune returns -1 and changes nothing."""
+    from gym_po_amd import CRoomsEnv, TaxiVecEnv
+    envs = [_fourrooms(1 << 16, gpu_device, rng_mode="philox"), TaxiVecEnv(4096, device=gpu_device),
+            CRoomsEnv(4096, rng_mode="numpy", device=gpu_device)]
+    for env in envs:
+        env.reset(seed=3)
+        assert env.autotune(20) == -1
