@@ -3273,13 +3273,13 @@ int GridBackend::autotune(int K, int reps, int* chosen) {
         return launch_fused<OK>(K, a.p, o.p, r.as<float>(), t.as<uint8_t>(), u.as<uint8_t>(), 0);
       });
     };
-    if ((e = one())) break;  // warm
-    if (hipEventRecord(e0, 0) != hipSuccess) e = GP_E_HIP;
+    e = one();  // warm
+    if (!e && hipEventRecord(e0, 0) != hipSuccess) e = GP_E_HIP;
     for (int i = 0; i < reps && !e; ++i) e = one();
     if (!e && (hipEventRecord(e1, 0) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
                hipEventElapsedTime(&ms[c], e0, e1) != hipSuccess))
       e = GP_E_HIP;
-    if (int e2 = restore()) e = e ? e : e2;
+    if (int e2 = restore()) e = e ? e : e2;  // (also after a failed launch: the state is put back first)
   }
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
