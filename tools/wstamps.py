@@ -37,6 +37,8 @@ assert env.query("wgrid") == 1, "the windowed kernel is not eligible for this si
 G = int(env.query("wgrid_blocks"))
 env.reset(seed=0)
 acts = torch.randint(0, 4, (K, B), device="cuda", dtype=torch.int32)
+for _ in range(int(os.environ.get("SKIP", "0")) // K):  # SKIP=n: n steps first (a later episode phase)
+    env.rollout(acts)
 for _ in range(4):
     env.rollout(acts)
 torch.cuda.synchronize()
