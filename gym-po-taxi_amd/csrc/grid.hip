@@ -3259,11 +3259,15 @@ int GridBackend::autotune(int K, int reps, int* chosen) {
     GP_HIP_CHECK(hipDeviceSynchronize());
     return GP_OK;
   };
-  const bool timer_on = timer.on;
-  timer.on = false;
   hipEvent_t e0, e1;
   GP_HIP_CHECK(hipEventCreate(&e0));
-  GP_HIP_CHECK(hipEventCreate(&e1));
+  if (hipEventCreate(&e1) != hipSuccess) {
+    (void)hipEventDestroy(e0);
+    gp_set_error("autotune: hipEventCreate failed");
+    return GP_E_HIP;
+  }
+  const bool timer_on = timer.on;  // (the scratch launches are not the caller's to profile)
+  timer.on = false;
   float ms[2] = {0.f, 0.f};
   for (int c = 0; c < 2 && !e; ++c) {
     auto one = [&]() -> int {
