@@ -280,7 +280,7 @@ def _time_oracle(ora, acts, name, B, target_s):
                       f"2^{B.bit_length() - 1} envs x {n} steps, 1 process ({dt:.1f} s)"}
 
 
-def load_pmc(cfg_key, workload, steps_per_launch):
+def load_pmc(cfg_key, workload, steps_per_launch, kernel=None):
     """HBM traffic per launch of `steps_per_launch` steps from profiles/*pmc_*.json (rocprofv3 FETCH_SIZE /
     WRITE_SIZE passes, tools/pmc_to_json.py), only from records of the same kernel sources and config.
     A record at exactly this launch shape is used as is; otherwise, from records at two or more launch
@@ -293,6 +293,8 @@ def load_pmc(cfg_key, workload, steps_per_launch):
             d = json.load(open(fn))
         except Exception:  # noqa: BLE001
             continue
+        if kernel and d.get("kernel") and d["kernel"] not in kernel:
+            continue  # another kernel's record (numpy FourRooms has two for the same launch shape)
         if d.get("src_hash") == src_hash(workload) and d.get("config") == cfg_key and d.get("steps_per_launch"):
             recs[float(d["steps_per_launch"])] = (d["hbm_bytes_per_launch"], os.path.basename(fn))
     if not recs:
@@ -322,6 +324,8 @@ def main():
     ap.add_argument("--mode", default=None, choices=["numpy", "philox"])
     ap.add_argument("--chunk", type=int, default=None, help="steps per gp_rollout call")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--kernel", default="auto", choices=["auto", "windowed", "fused"],
+                    help="numpy FourRooms: gp_autotune's choice (default) or one kernel for every launch")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -352,13 +356,18 @@ def main():
     args.chunk = args.chunk or W.get("chunk", 64)
     from gym_po_amd import shard
     B = shard.shard_size(args.envs, world, rank, args.strong)
-    env = W["make"](B, dev, args.mode)
+    C = max(1, min(args.chunk, args.steps))
+    if args.kernel == "auto":
+        env = W["make"](B, dev, args.mode)
+    else:  # numpy-mode FourRooms kernel forced for every launch length (PMC records per kernel; A/Bs)
+        from gym_po_amd._lib import debug_knobs
+        with debug_knobs(wg_kmax=1 << 20 if args.kernel == "windowed" else 0):
+            env = W["make"](B, dev, args.mode)
     shard.seed_shard(env, 0, rank, world)  # shard g: SeedSequence(0, spawn_key=(g,))
     env.reset()
-    C = max(1, min(args.chunk, args.steps))
     # numpy-mode FourRooms: the faster of the two bit-identical kernels for C-step launches on this board, timed
     # on scratch state by the library before anything is timed here (gp_autotune; -1 elsewhere: a no-op)
-    tuned = env.autotune(C) if hasattr(env, "autotune") else -1
+    tuned = env.autotune(C) if args.kernel == "auto" and hasattr(env, "autotune") else -1
     g = torch.Generator(device=dev)
     g.manual_seed(1 + rank)
     if W["n_actions"] is None:  # continuous (y, x) actions, float32 U[-1, 1]^2
@@ -479,7 +488,10 @@ def main():
     total_steps = (args.envs if args.strong else B * world) * args.steps
     cfg_key = (f"fourrooms_hansen4_B{B}_{args.mode}" if args.workload == "fourrooms" else
                f"{args.workload}_B{B}_{args.mode}")
-    traffic, traffic_src = load_pmc(cfg_key, args.workload, steps_per_launch)
+    kname = W.get("kernel") or (kernel_name if kernel_name else ("grid_rollout_numpy<GP_OBS_HANSEN,2,4,true>"
+                                                             if steps_per_launch > 1.5 else "grid_step_numpy<GP_OBS_HANSEN>")
+                                if args.mode == "numpy" else "grid_rollout_counter<GP_OBS_HANSEN,false>")
+    traffic, traffic_src = load_pmc(cfg_key, args.workload, steps_per_launch, kname)
     line = {
         "metric": W["metric"],
         "value": total_steps / tmax,
@@ -498,7 +510,8 @@ def main():
         "config": {"workload": W["desc"].format(B=B),
                    "envs_per_gpu": B, "global_envs": args.envs if args.strong else B * world, "rng_mode": args.mode,
                    "parallelism": f"independent env shards x{world}", "steps_per_launch_call": C,
-                   "kernel_autotune": {1: "windowed", 0: "fused", -1: None}[tuned]},
+                   "kernel_autotune": {1: "windowed", 0: "fused", -1: None}[tuned] if args.kernel == "auto" else
+                   f"forced: {args.kernel}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "byte_model": (f"SURVEY 8(d): {W['bytes']} B per env-step + {W['state']} B per env per launch "
@@ -507,9 +520,7 @@ def main():
                      "bytes_per_launch_packed_state": bytes_packed,
                      "traffic_over_algorithmic": traffic / bytes_per_launch if traffic else None,
                      "traffic_source": traffic_src,
-                     "kernel": W.get("kernel") or (kernel_name if kernel_name else ("grid_rollout_numpy<GP_OBS_HANSEN,2,4,true>" if steps_per_launch > 1.5
-                                                   else "grid_step_numpy<GP_OBS_HANSEN>") if args.mode == "numpy"
-                                                  else "grid_rollout_counter<GP_OBS_HANSEN,false>"),
+                     "kernel": kname,
                      "steps_per_launch": steps_per_launch,
                      "kernel_avg_us": kavg_ms * 1e3,
                      "bytes_per_launch": bytes_per_launch,

@@ -112,10 +112,13 @@ case "$task" in
     i=0
     for C in FETCH_SIZE WRITE_SIZE; do
       i=$((i+1))
-      run 300 $O/p$i.log rocprofv3 --pmc $C --output-format csv -d $O/pmc/p$i -o p -- python3 bench.py --no-cpu-baseline --steps 20 --warmup 5
+      run 300 $O/p$i.log rocprofv3 --pmc $C --output-format csv -d $O/pmc/p$i -o p -- python3 bench.py --no-cpu-baseline --steps 20 --warmup 5 --kernel windowed
+      run 300 $O/q$i.log rocprofv3 --pmc $C --output-format csv -d $O/pmcf/p$i -o p -- python3 bench.py --no-cpu-baseline --steps 20 --warmup 5 --kernel fused
     done
-    python3 tools/pmc_to_json.py $O/pmc ${PMC_KERNEL:-wgrid_rollout} fourrooms_hansen4_B1048576_numpy $O/pmc.json fourrooms 20
-    cp $O/pmc.json profiles/${R}_pmc_fourrooms_hansen4_B1048576_numpy_K20.json
+    python3 tools/pmc_to_json.py $O/pmc wgrid_rollout fourrooms_hansen4_B1048576_numpy $O/pmc.json fourrooms 20
+    cp $O/pmc.json profiles/${R}_pmc_fourrooms_hansen4_B1048576_numpy_K20_wgrid_rollout.json
+    python3 tools/pmc_to_json.py $O/pmcf grid_rollout_numpy fourrooms_hansen4_B1048576_numpy $O/pmcf.json fourrooms 20
+    cp $O/pmcf.json profiles/${R}_pmc_fourrooms_hansen4_B1048576_numpy_K20_grid_rollout_numpy.json
     run 600 $O/bench_default.log python3 bench.py
     last_json $O/bench_default.log 3000
     run 300 $O/bench_driver.log python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline
@@ -132,9 +135,10 @@ case "$task" in
         run 300 $O/$n.p$i.log rocprofv3 --pmc $C --output-format csv -d $O/$n/p$i -o p -- python3 bench.py --no-cpu-baseline "$@"
       done
       python3 tools/pmc_to_json.py $O/$n $k $c $O/$n.json $w $K
-      cp $O/$n.json profiles/${R}_pmc_${c}_K${K}.json
+      cp $O/$n.json profiles/${R}_pmc_${c}_K${K}_${k}.json
     }
-    pm fr128 grid_rollout_numpy fourrooms_hansen4_B1048576_numpy fourrooms 128 --steps 1280 --warmup 256 --chunk 128
+    pm fr128 grid_rollout_numpy fourrooms_hansen4_B1048576_numpy fourrooms 128 --steps 1280 --warmup 256 --chunk 128 --kernel fused
+    pm fr128w wgrid_rollout fourrooms_hansen4_B1048576_numpy fourrooms 128 --steps 1280 --warmup 256 --chunk 128 --kernel windowed
     pm taxi taxi_rollout taxi_B4194304_philox taxi 4 --workload taxi
     pm anttag anttag_rollout anttag_B2097152_philox anttag 64 --workload anttag
     pm crooms crooms_rollout crooms_B2097152_philox crooms 128 --workload crooms

@@ -36,8 +36,10 @@ med = statistics.median(vals["WRITE_SIZE"])
 keep = [i for i, v in enumerate(vals["WRITE_SIZE"]) if abs(v - med) <= 0.05 * med]
 if len(vals["FETCH_SIZE"]) == len(vals["WRITE_SIZE"]):
     vals = {k: [v[i] for i in keep] for k, v in vals.items()}
-else:
-    vals["WRITE_SIZE"] = [vals["WRITE_SIZE"][i] for i in keep]
+else:  # the passes launched different sequences (e.g. an autotuned kernel choice): filter each on its own median
+    for k in vals:
+        m = statistics.median(vals[k])
+        vals[k] = [v for v in vals[k] if abs(v - m) <= 0.05 * m]
 fetch_kib = sum(vals["FETCH_SIZE"]) / len(vals["FETCH_SIZE"])
 write_kib = sum(vals["WRITE_SIZE"]) / len(vals["WRITE_SIZE"])
 here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
