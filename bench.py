@@ -367,7 +367,8 @@ def main():
     env.reset()
     # numpy-mode FourRooms: the faster of the two bit-identical kernels for C-step launches on this board, timed
     # on scratch state by the library before anything is timed here (gp_autotune; -1 elsewhere: a no-op)
-    tuned = env.autotune(C) if args.kernel == "auto" and hasattr(env, "autotune") else -1
+    # (20 launches per kernel: with 5 the choice flipped in 1 of 5 driver-command runs on one box, to the slower one)
+    tuned = env.autotune(C, reps=20) if args.kernel == "auto" and hasattr(env, "autotune") else -1
     g = torch.Generator(device=dev)
     g.manual_seed(1 + rank)
     if W["n_actions"] is None:  # continuous (y, x) actions, float32 U[-1, 1]^2
