@@ -367,8 +367,17 @@ def main():
     env.reset()
     # numpy-mode FourRooms: the faster of the two bit-identical kernels for C-step launches on this board, timed
     # on scratch state by the library before anything is timed here (gp_autotune; -1 elsewhere: a no-op)
-    # (20 launches per kernel: with 5 the choice flipped in 1 of 5 driver-command runs on one box, to the slower one)
+    # (20 launches per kernel: with 5 the choice flipped in 1 of 5 driver-command runs on one box, to the slower one;
+    # the library keeps the launch length's default kernel unless the other is >= 2% faster)
     tuned = env.autotune(C, reps=20) if args.kernel == "auto" and hasattr(env, "autotune") else -1
+    pretimed = None
+    if tuned >= 0:  # GPU work before the warmup, on scratch state (the env's state is restored exactly)
+        na, ka = env.query("autotune_launches"), env.query("autotune_steps")
+        pretimed = {"autotune_launches": na, "autotune_steps_per_launch": ka, "autotune_env_steps": na * ka * B,
+                    "autotune_us_per_launch": {"windowed": env.query("autotune_wgrid_ns") / 1e3,
+                                               "fused": env.query("autotune_fused_ns") / 1e3},
+                    "note": "both kernels timed on scratch actions/outputs before the warmup; the default kernel for "
+                            "the launch length is kept unless the other is >= 2% faster"}
     g = torch.Generator(device=dev)
     g.manual_seed(1 + rank)
     if W["n_actions"] is None:  # continuous (y, x) actions, float32 U[-1, 1]^2
@@ -512,7 +521,8 @@ def main():
                    "envs_per_gpu": B, "global_envs": args.envs if args.strong else B * world, "rng_mode": args.mode,
                    "parallelism": f"independent env shards x{world}", "steps_per_launch_call": C,
                    "kernel_autotune": {1: "windowed", 0: "fused", -1: None}[tuned] if args.kernel == "auto" else
-                   f"forced: {args.kernel}"},
+                   f"forced: {args.kernel}",
+                   "pretimed": pretimed},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "byte_model": (f"SURVEY 8(d): {W['bytes']} B per env-step + {W['state']} B per env per launch "
@@ -526,8 +536,8 @@ def main():
                      "kernel_avg_us": kavg_ms * 1e3,
                      "bytes_per_launch": bytes_per_launch,
                      "kernel_launches_timed": nk,
-                     "resolver_kernel": ("grid_resolve_numpy<GP_OBS_HANSEN>"
-                                         if args.mode == "numpy" and args.workload == "fourrooms" else None),
+                     # the two-kernel path's reset resolver (only launched when neither fused kernel runs)
+                     "resolver_kernel": "grid_resolve_numpy<GP_OBS_HANSEN>" if nr else None,
                      "resolver_avg_us": ravg_ms * 1e3 if nr else None},
         "episodes": {"count": m["episodes"], "mean_return": m["return_sum"] / max(m["episodes"], 1),
                      "mean_length": m["length_sum"] / max(m["episodes"], 1)},

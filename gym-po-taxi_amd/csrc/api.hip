@@ -37,9 +37,6 @@ const char* gp_derr_text(uint32_t flags) {
   if (flags & GP_DERR_BTPE)
     strncat(buf, "a Taxi numpy-mode reset needed numpy's BTPE binomial (not restated on the device); ",
             sizeof(buf) - strlen(buf) - 1);
-  if (flags & GP_DERR_LOGIC)
-    strncat(buf, "the windowed kernel's early reset count disagreed with its step masks (internal error); ",
-            sizeof(buf) - strlen(buf) - 1);
   if (flags & GP_DERR_STREAM)
     strncat(buf, "a numpy normal needed more words than one stream window holds; ", sizeof(buf) - strlen(buf) - 1);
   return buf;
@@ -225,6 +222,7 @@ int gp_debug_set(const char* key, int64_t value) {
   else if (!strcmp(key, "wg_kmax")) g_dbg.wg_kmax = (int)value;
   else if (!strcmp(key, "taxi_npg_min")) g_dbg.taxi_npg_min = (int)value;
   else if (!strcmp(key, "xg_min_envs")) g_dbg.xg_min_envs = (int)value;
+  else if (!strcmp(key, "fused_step")) g_dbg.fused_step = value;
   else {
     gp_set_error("gp_debug_set: unknown key '%s'", key);
     return GP_E_INVALID;
@@ -238,9 +236,16 @@ int gp_abi_version(void) { return GP_ABI_VERSION; }
 // return (a caller whose current device is another GPU, e.g. torch's, must not find it switched afterwards).
 struct DeviceGuard {
   int prev = -1;
+  bool ok = true;  // false: the env's device could not be made current (the call must not run on another one)
   explicit DeviceGuard(int dev) {
     int cur = -1;
-    if (hipGetDevice(&cur) == hipSuccess && cur != dev && hipSetDevice(dev) == hipSuccess) prev = cur;
+    if (hipGetDevice(&cur) != hipSuccess) {
+      ok = hipSetDevice(dev) == hipSuccess;
+    } else if (cur != dev) {
+      ok = hipSetDevice(dev) == hipSuccess;
+      if (ok) prev = cur;
+    }
+    if (!ok) gp_set_error("hipSetDevice(%d) failed", dev);
   }
   ~DeviceGuard() {
     if (prev >= 0) (void)hipSetDevice(prev);
@@ -266,6 +271,7 @@ int gp_create(int kind, const void* config, int64_t num_envs, int device, int rn
     return GP_E_INVALID;
   }
   DeviceGuard guard(device);
+  if (!guard.ok) return GP_E_HIP;
   int err = GP_OK;
   std::unique_ptr<EnvBackend> be;
   switch (kind) {
@@ -294,7 +300,8 @@ void gp_destroy(gp_env* env) { delete env; }
     gp_set_error("null env handle");     \
     return GP_E_INVALID;                 \
   }                                      \
-  DeviceGuard gp_device_guard_(env->be->device)
+  DeviceGuard gp_device_guard_(env->be->device); \
+  if (!gp_device_guard_.ok) return GP_E_HIP
 
 int gp_obs_info(const gp_env* env, int* dtype, int* width) {
   if (!env || !env->be) {

@@ -133,7 +133,6 @@ GP_HD uint32_t st_count(uint64_t s) { return (uint32_t)s; }
                             // (msrooms.py:400 action_matrix[action], extended_taxi.py:248 ACTIONS_YX[actions])
 #define GP_DERR_STREAM 4u   // C-ROOMS exact mode: a numpy normal needed more words than one window holds
 #define GP_DERR_OVERFLOW 8u // windowed grid kernel slow path: more rejected choice() words than it can list
-#define GP_DERR_LOGIC 32u  // windowed grid kernel: the early reset count disagreed with the step's masks (internal)
 #define GP_DERR_BTPE 16u    // Taxi numpy mode: a multinomial reset needed numpy's BTPE binomial (p n > 30) or an
                             // inversion did not end, neither of which the device walker restates
 // numpy indexing of an n-row table accepts a in [-n, n) (negatives wrap); anything else raises.

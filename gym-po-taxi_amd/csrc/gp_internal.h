@@ -35,8 +35,9 @@ struct GpDebugKnobs {
   int wg_bias = 0;          // GRID windowed kernel: added to the predicted reset count (forces window misses)
   int wg_tmode = 0;         // GRID windowed kernel: timing-study variants (wgrid.hip TM_*); some give wrong results
   int wg_kmax = -1;         // GRID: longest launch (steps) on the windowed kernel; longer ones on the fused kernel (-1 default)
-  int xg_min_envs = -1;
-  int taxi_npg_min = -1;    // TAXI numpy mode: largest B on the one-workgroup kernel (-1 = taxi.hip NPG_MIN_ENVS)     // CROOMS exact mode: largest B on the one-workgroup kernel (-1 = crooms.hip XG_MIN_ENVS)
+  int xg_min_envs = -1;      // CROOMS exact mode: largest B on the one-workgroup kernel (-1 = crooms.hip XG_MIN_ENVS)
+  int taxi_npg_min = -1;    // TAXI numpy mode: largest B on the one-workgroup kernel (-1 = taxi.hip NPG_MIN_ENVS)
+  int64_t fused_step = -1;  // GRID: the fused kernel's tag counter (GridCtl::step) set at every seed (-1 = kept)
 };
 const GpDebugKnobs& gp_debug_knobs();
 

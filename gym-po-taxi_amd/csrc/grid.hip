@@ -1018,9 +1018,11 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 
 // Wave 0: poll the G block granules of one round (lane l holds blocks 4l..4l+3) until every one
-// carries `tag`. Granules of blocks >= G read as 0.
+// carries `tag`. Granules of blocks >= G read as 0. `full`: the coverage rounds' granules carry the whole 32-bit
+// tag in their (otherwise unused) count bits too, so that a round-1/2 slot last written 8192 steps earlier
+// (same 15-bit tag, same parity) is never taken for this step's.
 __device__ __forceinline__ void gather_blocks(const GridDev& p, const uint64_t* slots, int G, uint32_t tag,
-                                              uint64_t (&g)[4]) {
+                                              uint64_t (&g)[4], bool full = false) {
   const int lane = threadIdx.x & 63;
   const uint64_t want = (uint64_t)(tag & TAG_MASK);
   uint32_t pend = 0;
@@ -1037,7 +1039,7 @@ __device__ __forceinline__ void gather_blocks(const GridDev& p, const uint64_t* 
         g[j] = __hip_atomic_load(&slots[lane * 4 + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      if ((pend & (1u << j)) && (g[j] >> 49) == want) pend &= ~(1u << j);
+      if ((pend & (1u << j)) && (g[j] >> 49) == want && (!full || (uint32_t)g[j] == tag)) pend &= ~(1u << j);
     if (!__any((int)pend)) break;
     if (spin_give_up(p, spins)) {  // flagged: the results of this launch are invalid (GP_E_DEVICE)
 #pragma unroll
@@ -1081,10 +1083,10 @@ __device__ __noinline__ uint32_t coverage_round(const GridDev* __restrict__ gp, 
   }
   const uint32_t any = __syncthreads_or((int)r) ? 1u : 0u;
   if (threadIdx.x == 0 && (int)blockIdx.x != p.fault_block)
-    __hip_atomic_store(&slots[blockIdx.x], bgran(tag, any, 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&slots[blockIdx.x], bgran(tag, any, (uint64_t)tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (wid == FENVW) {  // the control wave
     uint64_t g[4];
-    gather_blocks(p, slots, G, tag, g);
+    gather_blocks(p, slots, G, tag, g, true);
     uint32_t rj = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) rj |= (uint32_t)(g[j] >> 48) & 1u;
@@ -2712,6 +2714,8 @@ struct GridBackend : EnvBackend {
   int wg_G = 0, wg_E = 0, wg_NS = 0, wg_H = 0;
   int wg_kmax = WG_KMAX;  // launches of more steps go to the fused kernel when it can take them (gp_debug_set wg_kmax)
   size_t wg_lds = 0;
+  int at_launches = 0, at_steps = 0;  // the last gp_autotune's scratch launches (both kernels) and their length
+  float at_ms[2] = {0.f, 0.f};        // its mean ms per launch: windowed, fused
   WgParams wg{};
   std::vector<char> wg_img;        // LDS image of its tables (the PCG jump parts rebuilt on every seed)
   DevBuf b_wgp, b_wlimg, b_wjlane, b_wjrej, b_wjblk, b_wslots;
@@ -2751,6 +2755,13 @@ struct GridBackend : EnvBackend {
     else if (!strcmp(key, "wgrid_block_envs")) *v = wg_E;
     else if (!strcmp(key, "wgrid_halo")) *v = wg_H;
     else if (!strcmp(key, "wgrid_kmax")) *v = wg_kmax;
+    else if (!strcmp(key, "wgrid_lds")) *v = (int64_t)wg_lds;  // dynamic LDS bytes of one launch
+    // the last autotune: launches it made (both kernels, incl. one warm launch each), their length, and the mean
+    // time per launch of each kernel in ns
+    else if (!strcmp(key, "autotune_launches")) *v = at_launches;
+    else if (!strcmp(key, "autotune_steps")) *v = at_steps;
+    else if (!strcmp(key, "autotune_wgrid_ns")) *v = (int64_t)(at_ms[0] * 1e6f);
+    else if (!strcmp(key, "autotune_fused_ns")) *v = (int64_t)(at_ms[1] * 1e6f);
     else return EnvBackend::query(key, v);
     return GP_OK;
   }
@@ -2881,6 +2892,8 @@ int GridBackend::upload_rng() {
   c.has_u32 = rng.has_u32;
   c.uinteger = rng.uinteger;
   c.err = 0;  // a new stream position: earlier device errors no longer apply
+  // test knob: start the fused kernel's tag counter here (tests cross its 8192-step tag wrap without 8192 steps)
+  if (gp_debug_knobs().fused_step >= 0) c.step = (uint32_t)gp_debug_knobs().fused_step;
   GP_HIP_CHECK(hipMemcpy(d.ctl, &c, sizeof(c), hipMemcpyHostToDevice));
   std::vector<PcgJump> jt = build_jump_tables(rng.inc);
   GP_HIP_CHECK(hipMemcpy(b_jt.p, jt.data(), jt.size() * sizeof(PcgJump), hipMemcpyHostToDevice));
@@ -3225,7 +3238,8 @@ __global__ void autotune_actions(int32_t* a, size_t n, int nact) {
 
 // Times `reps` K-step launches of the windowed and of the fused kernel on scratch actions / outputs, each from
 // the handle's current state, which is restored exactly afterwards (agent cells + elapsed, the stream and the
-// kernels' control block, the metric slots; both kernels' granule slots cleared, as allocated: tags are never 0).
+// kernels' control block, the metric slots; both kernels' granule slots reset as allocated, to a tag neither
+// kernel ever expects).
 // Launches of K steps then go to the faster one (wg_kmax). Their results are identical; which one is faster at
 // short launches differs between MI355X boards (profiles/r05_ab_kernel_by_K.txt).
 int GridBackend::autotune(int K, int reps, int* chosen) {
@@ -3237,7 +3251,22 @@ int GridBackend::autotune(int K, int reps, int* chosen) {
   }
   reps = std::max(1, std::min(reps, 64));
   GP_HIP_CHECK(hipDeviceSynchronize());
-  const size_t nb = (size_t)B, kb = (size_t)K * nb;
+  // The scratch launches are at most AT_KMAX steps long (the outputs of one launch are 14 B per env-step: 1.9 GB at
+  // K = 128 and 2^20 envs). Longer launches are decided from AT_KMAX-step ones: per step both kernels are then in
+  // their long-launch regime (profiles/r05_ab_kernel_by_K.txt).
+  constexpr int AT_KMAX = 64;
+  const int Kt = std::min(K, AT_KMAX);
+  const size_t nb = (size_t)B, kb = (size_t)Kt * nb;
+  {
+    size_t fr = 0, tot = 0;
+    GP_HIP_CHECK(hipMemGetInfo(&fr, &tot));
+    const size_t need = 4 * nb + b_mslot.n + 14 * kb;
+    if (need > fr / 10 * 9) {
+      gp_set_error("autotune: %zu bytes of scratch (%d-step launches of %lld envs) exceed the free device memory (%zu)",
+                   need, Kt, (long long)B, fr);
+      return GP_E_INVALID;
+    }
+  }
   DevBuf s_ae, s_ms, a, o, r, t, u;
   GridCtl ctl_h;
   int e;
@@ -3254,8 +3283,8 @@ int GridBackend::autotune(int K, int reps, int* chosen) {
     GP_HIP_CHECK(hipMemcpy(d.ae, s_ae.p, 4 * nb, hipMemcpyDeviceToDevice));
     GP_HIP_CHECK(hipMemcpy(d.mslot, s_ms.p, b_mslot.n, hipMemcpyDeviceToDevice));
     GP_HIP_CHECK(hipMemcpy(d.ctl, &ctl_h, sizeof(GridCtl), hipMemcpyHostToDevice));
-    GP_HIP_CHECK(hipMemset(b_wslots.p, 0, b_wslots.n));
-    GP_HIP_CHECK(hipMemset(b_fslot.p, 0, b_fslot.n));
+    GP_HIP_CHECK(hipMemset(b_wslots.p, 0, b_wslots.n));   // windowed tags are never 0
+    GP_HIP_CHECK(hipMemset(b_fslot.p, 0xFF, b_fslot.n));  // fused tags are never 0x7FFF (as allocated)
     GP_HIP_CHECK(hipDeviceSynchronize());
     return GP_OK;
   };
@@ -3271,10 +3300,10 @@ int GridBackend::autotune(int K, int reps, int* chosen) {
   float ms[2] = {0.f, 0.f};
   for (int c = 0; c < 2 && !e; ++c) {
     auto one = [&]() -> int {
-      if (c == 0) return launch_wgrid(K, a.p, o.p, r.as<float>(), t.as<uint8_t>(), u.as<uint8_t>(), 0);
+      if (c == 0) return launch_wgrid(Kt, a.p, o.p, r.as<float>(), t.as<uint8_t>(), u.as<uint8_t>(), 0);
       return dispatch_obs(d.obs_kind, [&](auto okc) -> int {
         constexpr int OK = decltype(okc)::value;
-        return launch_fused<OK>(K, a.p, o.p, r.as<float>(), t.as<uint8_t>(), u.as<uint8_t>(), 0);
+        return launch_fused<OK>(Kt, a.p, o.p, r.as<float>(), t.as<uint8_t>(), u.as<uint8_t>(), 0);
       });
     };
     e = one();  // warm
@@ -3289,9 +3318,17 @@ int GridBackend::autotune(int K, int reps, int* chosen) {
   (void)hipEventDestroy(e1);
   timer.on = timer_on;
   if (e) return e;
-  const bool wgrid_faster = ms[0] <= ms[1];
+  // A margin: the kernel the launch length picks by default (WG_KMAX) is kept unless the other one is at least
+  // AT_MARGIN faster (one of five driver-command runs picked the kernel that was slower there with no margin).
+  constexpr float AT_MARGIN = 0.02f;
+  const bool def_wgrid = K <= WG_KMAX;
+  const bool wgrid_faster = def_wgrid ? !(ms[1] < (1.f - AT_MARGIN) * ms[0]) : ms[0] < (1.f - AT_MARGIN) * ms[1];
   if (wgrid_faster) wg_kmax = std::max(wg_kmax, K);
   else wg_kmax = std::min(wg_kmax, K - 1);
+  at_ms[0] = ms[0] / (float)reps;
+  at_ms[1] = ms[1] / (float)reps;
+  at_launches = 2 * (reps + 1);
+  at_steps = Kt;
   if (chosen) *chosen = wgrid_faster ? 1 : 0;
   return check();
 }
@@ -3722,6 +3759,9 @@ int GridBackend::build(const gp_grid_config* cfg) {
   d.flt4 = b_flt4.as<PcgJump>();
   d.fjB = b_fjB.as<PcgJump>();
   d.fslot = b_fslot.as<uint64_t>();
+  // The fused kernel's slots start with tag 0x7FFF: tags are (step + 1) * 4 + round with round <= 2, so this value
+  // is never expected (a zeroed slot would match tag 0, i.e. round 0 of every 8192nd step).
+  GP_HIP_CHECK(hipMemset(b_fslot.p, 0xFF, b_fslot.n));
 #ifdef GP_STAMPS
   if ((e = b_dbg.alloc(sizeof(unsigned long long) * (256 * 64 * 16 + 256 * 8)))) return e;
   d.dbg = b_dbg.as<unsigned long long>();

@@ -11,7 +11,8 @@ struct alignas(64) GridCtl {
   uint32_t epoch;                       // K2 launches so far (tags the per-block flags)
   uint32_t err;                         // bit0: spin timeout
   uint32_t b_total;                     // resets resolved by the last K2 (diagnostic)
-  uint32_t step;                        // numpy-mode steps taken (fused-kernel granule tags)
+  uint32_t step;                        // fused kernel: its own steps taken (its granule tags; only fused launches
+                                        //   advance it, so its steps stay contiguous when windowed launches interleave)
   uint32_t fb_last;                     // fused kernels: resets b of the last step (next launch's window centre)
   uint32_t wstep;                       // windowed kernel: its own steps taken (its granule tags)
 };

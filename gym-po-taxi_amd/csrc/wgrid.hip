@@ -75,6 +75,8 @@ constexpr int TM_EAGERSTORE = 64; // store waves copy a step as soon as it is fi
 constexpr int TM_NOCAND = 128;  // no candidate cells during the all-gather (every resetter's cell drawn after it)
 constexpr int TM_STORELOW = 256; // store waves at priority 0 (default 1)
 constexpr int TM_ENVHIGH = 512; // env waves at priority 2 throughout (default: 2 for the transitions, 0 otherwise)
+constexpr int TM_NOTABLES = 1024;  // no table staging at launch (stale LDS tables: measurement only)
+constexpr int TM_NOFIRST = 2048;   // no first-window fill at launch (stale words: measurement only)
 
 constexpr int EW = 8;                 // env waves
 constexpr int SW = 2;                 // store waves
@@ -582,8 +584,7 @@ __device__ __forceinline__ void wg_ctrl(const WgParams& P, WgShared& sh, const T
     C->has_u32 = h;
     C->uinteger = u;
     C->fb_last = bprev;
-    C->wstep = ts0 + (uint32_t)K - 1u;
-    C->step += (uint32_t)K;
+    C->wstep = ts0 + (uint32_t)K - 1u;  // (GridCtl::step is the fused kernel's own tag counter: not advanced here)
   }
 }
 
@@ -658,7 +659,7 @@ __device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Ta
   }
   // the first window, exact (word 0 = S(x_0 + 1 + E beta - heff)), filled from global data while the other waves
   // stage the tables (it lies behind them in LDS)
-  {
+  if (!(tmode & TM_NOFIRST)) {
     const GridCtl* C = P.ctl;
     fill_window(L.RW, jrw, j512, nw, apply_jump(P.jblk[2 * beta + 1], mk128(C->s_hi, C->s_lo)), lg);
   }
@@ -894,7 +895,7 @@ __global__ __launch_bounds__(TPB) void wgrid_rollout(const WgParams* __restrict_
   if (tid == 0) LSTAMP(P, 0);
   // stage the table image (each thread's 16-B loads in flight before its LDS stores)
   // (the control and store waves; the env waves fill their first window meanwhile)
-  if (wid >= EW) {
+  if (wid >= EW && !(P.tmode & TM_NOTABLES)) {
     constexpr int CT = (NWAVES - EW) * 64;
     const int t = tid - EW * 64;
     const int n = P.lds.total >> 4;

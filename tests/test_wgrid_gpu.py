@@ -77,6 +77,25 @@ def test_kernel_choice_by_launch_length_bit_exact(kmax, gpu_device):
     assert env.metrics()["env_steps"] == B * 169
 
 
+@pytest.mark.parametrize("fstep", [8185, 16380])
+def test_fused_tag_wrap_between_windowed_launches_bit_exact(fstep, gpu_device):
+    """The fused kernel's 15-bit granule tags ((step + 1) * 4 + round) wrap every 8192 of its steps; round 0 of the
+    wrapping step expects tag 0. Its tag counter (GridCtl::step, started near the wrap by the fused_step knob) is
+    advanced only by fused launches, its slots start at a tag it never expects, and windowed launches interleave:
+    the results must stay the oracle's through the wrap (zeroed slots matched tag 0)."""
+    from gym_po_amd._lib import debug_knobs
+    B = 1 << 18
+    with debug_knobs(fused_step=fstep):
+        env = _fourrooms(B, gpu_device)
+        ora = gridworld.FourRoomsOracle(B, 1, obs_type="hansen")
+        np.testing.assert_array_equal(_reset_obs(env, 77).astype(np.int64),
+                                      np.asarray(ora.reset_seed(77)).astype(np.int64))
+    assert env.query("wgrid") == 1 and env.query("wgrid_kmax") == 24
+    # windowed (3), fused across the wrap (40), windowed (2), fused (33)
+    _check_chunks(env, ora, (3, 40, 2, 33), action_seed=12, n_act=4)
+    assert env.metrics()["env_steps"] == B * 78
+
+
 @pytest.mark.parametrize("B,E", [(1 << 17, 512), (1 << 18, 1024), (1 << 19, 2048), (3 << 17, 2048), (8192, 512)])
 def test_wgrid_block_sizes_bit_exact(B, E, gpu_device):
     env = _fourrooms(B, gpu_device)

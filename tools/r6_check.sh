@@ -1,0 +1,50 @@
+# Round-6 GPU check: windowed-kernel parity tests, an in-call A/B of the round-5 library (libgympo_amd_r5.so,
+# tools/build_commit_variant.sh r5 <commit>) against the current one, the driver's bench command, and the
+# launch-footprint probe. Every GPU step under its own limit; the first failure ends the call.
+#   bash tools/r6_check.sh [tests|ab|bench|floor]...
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+O=gpurun_out/r6
+mkdir -p $O
+LD=$PWD/gym-po-taxi_amd/gym_po_amd
+run() {
+  local t=$1 log=$2
+  shift 2
+  timeout -k 10 "$t" "$@" > "$log" 2>&1 || { echo "FAIL ($?): $*"; tail -40 "$log"; exit 1; }
+}
+for task in "${@:-tests ab bench floor}"; do
+  case $task in
+    tests)
+      run 600 $O/tests.log python -u -m pytest -x -v --timeout 200 --timeout-method thread ${TESTS:-tests/test_wgrid_gpu.py tests/test_bench_path_gpu.py} -m gpu
+      tail -n 1 $O/tests.log ;;
+    ab)
+      for rep in 1 2; do
+        for V in r5 base; do
+          L=$LD/libgympo_amd_$V.so
+          [ "$V" = base ] && L=$LD/libgympo_amd.so
+          GYM_PO_AMD_LIB=$L GP_KNOBS=wg_kmax=1000 run 150 $O/lat_$V.log python -u tools/latency_probe.py 1048576 ${ABK:-20 128}
+          echo "== $rep $V"; grep "B=" $O/lat_$V.log
+        done
+      done ;;
+    bench)
+      for rep in 1 2; do
+        run 300 $O/bench_$rep.log python3 bench.py --no-cpu-baseline --steps 20 --warmup 5
+        tail -n 1 $O/bench_$rep.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); r=d["roofline"]; print("bench", d["value"], d["ms_per_step"], r["frac"], r["kernel_avg_us"], r["kernel"], d["config"]["kernel_autotune"])'
+      done ;;
+    stamps)  # phase stamps of the windowed kernel (the GP_STAMPS library, built beforehand on the CPU)
+      for K in ${STK:-64 20}; do
+        GYM_PO_AMD_LIB=$LD/libgympo_amd_stamps.so run 200 $O/wstamps_k$K.log python -u tools/wstamps.py 1048576 $K
+        cat $O/wstamps_k$K.log
+      done ;;
+    floorprof)  # the launch-footprint probe under rocprofv3 (dispatch-timestamp durations of the same launches)
+      run 300 $O/floorprof.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/floorprof -o p -- python3 -u tools/launch_floor.py 60
+      for f in $(find $O/floorprof -name "*kernel_stats.csv"); do cp $f $O/floor_kernel_stats.csv; cat $f; done ;;
+    counters)  # the PMC counters this GPU offers
+      run 120 $O/counters.log rocprofv3 -L
+      grep -i -E "icache|ifetch|SQC_" $O/counters.log | head -60 ;;
+    floor)
+      run 200 $O/floor.log python -u tools/launch_floor.py 200
+      cat $O/floor.log ;;
+  esac
+done
