@@ -27,6 +27,13 @@ for task in "${@:-tests ab bench floor}"; do
           echo "== $rep $V"; grep "B=" $O/lat_$V.log
         done
       done ;;
+    tmodes)  # in-call A/B of timing-study schedules of the current library (wg_tmode bits, csrc/wgrid.hip TM_*)
+      for rep in 1 2; do
+        for T in ${TMODES:-0 4096 64 4160 8 256}; do
+          GP_KNOBS=wg_kmax=1000,wg_tmode=$T run 150 $O/tm_$T.log python -u tools/latency_probe.py 1048576 ${ABK:-20 128}
+          echo "== $rep tmode $T"; grep "B=" $O/tm_$T.log
+        done
+      done ;;
     bench)
       for rep in 1 2; do
         run 300 $O/bench_$rep.log python3 bench.py --no-cpu-baseline --steps 20 --warmup 5
@@ -36,6 +43,11 @@ for task in "${@:-tests ab bench floor}"; do
       for K in ${STK:-64 20}; do
         GYM_PO_AMD_LIB=$LD/libgympo_amd_stamps.so run 200 $O/wstamps_k$K.log python -u tools/wstamps.py 1048576 $K
         cat $O/wstamps_k$K.log
+      done ;;
+    r5stamps)  # the round-5 schedule's stamps (libgympo_amd_r5stamps.so, the same LDS stamps) for comparison
+      for K in ${STK:-64 20}; do
+        GYM_PO_AMD_LIB=$LD/libgympo_amd_r5stamps.so run 200 $O/r5stamps_k$K.log python -u tools/wstamps_r5.py 1048576 $K
+        cat $O/r5stamps_k$K.log
       done ;;
     floorprof)  # the launch-footprint probe under rocprofv3 (dispatch-timestamp durations of the same launches)
       run 300 $O/floorprof.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/floorprof -o p -- python3 -u tools/launch_floor.py 60
