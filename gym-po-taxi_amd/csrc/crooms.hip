@@ -42,6 +42,12 @@ constexpr int EPB = TPB * EPT;
 constexpr int WAVES = TPB / 64;
 constexpr uint32_t TAG_NOISE = 0x63726f6fu;  // 'croo'
 constexpr uint32_t TAG_DRAW = 0x6d733121u;
+// Philox rounds of the philox-mode blocks (noise and reset draws; oracle/philox.py philox4x32(rounds=)): Random123's
+// default 10. Round 6 measured 7 (the fewest Salmon et al. 2011 report Crush-resistant) at configs[4]: 1905 vs 1945
+// us per 128-step launch (frac 0.393 vs 0.385, one call): too little for the lost margin, so 10 stays.
+#ifndef CR_PHILOX_ROUNDS
+#define CR_PHILOX_ROUNDS 10
+#endif
 #ifndef GP_CR_NORMAL_F64
 #define GP_CR_NORMAL_F64 0
 #endif
@@ -278,7 +284,8 @@ __device__ __forceinline__ void draw_normals(const CrDev& p, int env, uint64_t s
     x = v.y;
   } else {
     if (!have) {
-      blk = philox4x32_10((uint32_t)env, (uint32_t)step, (uint32_t)(step >> 32), TAG_NOISE, p.key0, p.key1);
+      blk = philox4x32<CR_PHILOX_ROUNDS>((uint32_t)env, (uint32_t)step, (uint32_t)(step >> 32), TAG_NOISE, p.key0,
+                                         p.key1);
       have = true;
     }
     double z0, z1;
@@ -298,7 +305,8 @@ __device__ __forceinline__ void draw_ints(const CrDev& p, int env, uint64_t step
     d.gi = p.rp_goal ? (uint32_t)min(max(p.rp_goal[env], 0), p.n_valid - 1) : 0u;
     d.ai = p.rp_agent ? (uint32_t)min(max(p.rp_agent[env], 0), p.n_valid - 1) : 0u;
   } else {
-    const Philox4 r = philox4x32_10((uint32_t)env, (uint32_t)step, (uint32_t)(step >> 32), TAG_DRAW, p.key0, p.key1);
+    const Philox4 r =
+        philox4x32<CR_PHILOX_ROUNDS>((uint32_t)env, (uint32_t)step, (uint32_t)(step >> 32), TAG_DRAW, p.key0, p.key1);
     d.k53 = ((((uint64_t)r.x[0]) << 32) | r.x[1]) >> 11;
     d.gi = lemire_value(r.x[2], (uint32_t)p.n_valid);
     d.ai = lemire_value(r.x[3], (uint32_t)p.n_valid);
@@ -320,6 +328,14 @@ __device__ __forceinline__ int cell_of(const CrDev& p, double y, double x) {
   // coord_to_grid (utils.py:15-20): floor(coord / cell_size)
   const int cy = (int)floor(per_cell(p, y)), cx = (int)floor(per_cell(p, x));
   if (cy < 0 || cx < 0 || cy >= p.H || cx >= p.W) return -1;
+  return cy * p.W + cx;
+}
+
+// The same for coordinates known to be >= 0 (the clipped position): floor == truncation there, so the integer
+// conversion (v_cvt_i32_f64 truncates) is the floor and the two float64 floors go.
+__device__ __forceinline__ int cell_of_nonneg(const CrDev& p, double y, double x) {
+  const int cy = (int)per_cell(p, y), cx = (int)per_cell(p, x);
+  if (cy >= p.H || cx >= p.W) return -1;
   return cy * p.W + cx;
 }
 
@@ -478,7 +494,7 @@ __device__ __forceinline__ StepOut crooms_env_step(const CrDev& p, const uint8_t
   }
   py = fmin(fmax(py, 0.0), p.hi_y);
   px = fmin(fmax(px, 0.0), p.hi_x);
-  const int pc = cell_of(p, py, px);
+  const int pc = cell_of_nonneg(p, py, px);
   const bool oob = pc < 0 || tab<uint8_t>(lds, p.off_wall)[pc] != 0;
   o.oob = oob ? 1 : 0;
   if (!oob) {
@@ -574,6 +590,7 @@ __global__ __launch_bounds__(TPB, GP_CR_WAVES) void crooms_rollout(CrDev p, int 
     }
     for (int k = 0; k < K; ++k) {
       const size_t off = (size_t)k * p.B;
+      const uint64_t stp = step0 + (uint64_t)k;
       double a0[EPT], a1[EPT];
       int ad[EPT];
       const bool full = env0 + EPT - 1 < p.B && (off & 1) == 0;  // pair-aligned rew / flag stores
@@ -620,7 +637,7 @@ __global__ __launch_bounds__(TPB, GP_CR_WAVES) void crooms_rollout(CrDev p, int 
       for (int i = 0; i < EPT; ++i) {
         const int env = env0 + i;
         const bool live = env < p.B;
-        StepOut o = crooms_env_step<REPLAY, false, SPEC>(p, lds, env, live, step0 + (uint64_t)k, a0[i], a1[i], ad[i], ay[i], ax[i],
+        StepOut o = crooms_env_step<REPLAY, false, SPEC>(p, lds, env, live, stp, a0[i], a1[i], ad[i], ay[i], ax[i],
                                             vy[i], vx[i], g[i], el[i], rsum, eps, lens);
         r[i] = o.rew;
         tm[i] = o.term;
@@ -3167,7 +3184,7 @@ __global__ __launch_bounds__(256) void zig_tail_kernel(uint32_t k0, uint32_t k1,
   double s1 = 0.0, s2 = 0.0;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < npairs; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t e = (uint32_t)i, s0 = (uint32_t)(i >> 32);
-    const Philox4 r = philox4x32_10(e, s0, 0u, TAG_NOISE, k0, k1);
+    const Philox4 r = philox4x32<CR_PHILOX_ROUNDS>(e, s0, 0u, TAG_NOISE, k0, k1);
     double z0, z1;
     box_muller_pair(((uint64_t)r.x[1] << 32) | r.x[0], ((uint64_t)r.x[3] << 32) | r.x[2], z0, z1);
     s1 += z0 + z1;

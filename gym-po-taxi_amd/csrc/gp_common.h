@@ -97,10 +97,14 @@ GP_HD uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return a ^ b ^ c;
 #endif
 }
-GP_HD Philox4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
+// Philox4x32-R (Salmon et al. 2011, "Parallel random numbers: as easy as 1, 2, 3"); R = 10 is Random123's default
+// (every philox-mode kernel), R = 7 the fewest rounds the paper reports Crush-resistant (a C-ROOMS build option,
+// csrc/crooms.hip CR_PHILOX_ROUNDS).
+template <int R>
+GP_HD Philox4 philox4x32(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
   const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
 #pragma unroll
-  for (int r = 0; r < 10; ++r) {
+  for (int r = 0; r < R; ++r) {
     uint64_t p0 = (uint64_t)M0 * c0, p1 = (uint64_t)M1 * c2;
     uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0, hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
     uint32_t n0 = xor3(hi1, c1, k0), n2 = xor3(hi0, c3, k1);
@@ -109,6 +113,9 @@ GP_HD Philox4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, 
   }
   Philox4 r; r.x[0] = c0; r.x[1] = c1; r.x[2] = c2; r.x[3] = c3;
   return r;
+}
+GP_HD Philox4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
+  return philox4x32<10>(c0, c1, c2, c3, k0, k1);
 }
 
 // ---------------------------------------------------------------- lookback status words ----

@@ -1,5 +1,5 @@
 // libm.hip — host copies of the device restatements of C library functions (gp_libm.h), for the CPU tests that pin
-// them against this machine's libm.
+// them against this machine's libm; and the host copy of the Philox block (gp_common.h) for the oracle's check.
 #include <cmath>
 
 #include "gp_internal.h"
@@ -35,4 +35,20 @@ extern "C" int gp_exp_host_variant(void) {
   }
   variant = diffs == 0 ? -1 : (is_fma ? 1 : (is_plain ? 0 : -1));
   return variant;
+}
+
+// Philox4x32-R blocks (gp_common.h philox4x32<R>, R = 7 or 10) of n counters ctr[6 i ..] = {c0, c1, c2, c3, k0, k1}
+// into out[4 i ..]: the header the kernels inline, compiled for the host.
+extern "C" int gp_philox_blocks(const uint32_t* ctr, int rounds, uint32_t* out, int64_t n) {
+  if (!ctr || !out || n < 0 || (rounds != 7 && rounds != 10)) {
+    gp_set_error("gp_philox_blocks: bad arguments");
+    return GP_E_INVALID;
+  }
+  for (int64_t i = 0; i < n; ++i) {
+    const uint32_t* c = ctr + 6 * i;
+    const Philox4 r = rounds == 7 ? philox4x32<7>(c[0], c[1], c[2], c[3], c[4], c[5])
+                                  : philox4x32<10>(c[0], c[1], c[2], c[3], c[4], c[5]);
+    for (int j = 0; j < 4; ++j) out[4 * i + j] = r.x[j];
+  }
+  return GP_OK;
 }

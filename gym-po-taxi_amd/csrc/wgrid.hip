@@ -80,7 +80,6 @@ constexpr int TM_STORELOW = 256; // store waves at priority 0 (default 1)
 constexpr int TM_ENVHIGH = 512; // env waves at priority 2 throughout (default: 2 for the transitions, 0 otherwise)
 constexpr int TM_NOTABLES = 1024;  // no table staging at launch (stale LDS tables: measurement only)
 constexpr int TM_NOFIRST = 2048;   // no first-window fill at launch (stale words: measurement only)
-constexpr int TM_CTRLLOW = 4096;   // the control wave at priority 1 while it steps the resetters (default: 3 throughout)
 
 constexpr int EW = 8;                 // env waves
 constexpr int SW = 2;                 // store waves
@@ -94,27 +93,27 @@ constexpr int NCAND = 512;            // candidate resetter cells drawn during t
 constexpr uint32_t CAND_W = 192;      // half-words of them before the predicted block prefix
 
 struct WgShared {
-  uint64_t mask[8][EW];      // env waves: this step's done ballots of the envs they stepped, by (slot k, env wave w)
-  uint64_t rmask[2][8][EW];  // control wave, by step parity: done bits of the envs IT stepped (the last step's resetters)
+  uint64_t mask[8][EW];      // this step's resetter ballots by (slot k, env wave w)
   // monotone LDS counters: the waves never meet at a workgroup barrier inside the step loop
   uint32_t trans_done;       // env waves done with a step's transitions (EW per step)
   uint32_t cs_done;          // env waves done with a step's coarse states
+  uint32_t r2s_done;         // env waves done listing a step's resetters in r2s
   uint32_t fill_done;        // env-wave window fills (and exact regenerations) completed
+  uint32_t res_done;         // env waves done taking a step's resetter cells (the staging is final)
   uint32_t st_done;          // store-wave step copies completed (SW per step)
-  uint32_t sx_ready;         // control wave: step k's S(x) and step k+1's predicted window base published (k + 1)
-  uint32_t off_ready;        // control wave: step k's window offset (and regeneration flag) published (k + 1)
-  uint32_t rtr_done;         // control wave: step k's transitions of the last step's resetters staged (k + 1)
-  uint32_t cells_done;       // control wave: step k's resetters' cells staged, i.e. step k's staging final (k + 1)
+  uint32_t sx_ready;         // control wave: step k's S(x) published (k + 1)
+  uint32_t sy_ready;         // control wave: step k's S(y) and step k+1's window base published (k + 1)
+  uint32_t cells_done;       // control wave: step k's exchange finished, its resetters' cells staged (k + 1)
+  uint32_t pro;              // prologue: the first window's base is published
   uint64_t sx[2][2];         // by step parity: S(x_t) (hi, lo), the state at the step's start
-  uint64_t rw[2][2];         // by parity of the step a window serves: its predicted base state (hi, lo)
-  uint64_t rwx[2][2];        // the same: its exact base when the prediction missed (regeneration)
+  uint64_t sy[2][2];         // by step parity: S(y_t) (hi, lo), the state after the step's random(B)
+  uint64_t rw[2][2];         // by parity of the step a window serves: its base state (hi, lo)
   int32_t rw_off[2];         // by step parity: env i of that step reads window word i + rw_off
-  uint32_t wfix[2];          // by step parity: bit 1 = that step's window is regenerated from rwx first
-  uint32_t nrp;              // slow path: # rejected positions listed
+  uint32_t fix[2];           // by step parity: bit 0 slow path, bit 1 window regeneration
+  uint32_t R, h, u, nrp;     // slow path: block prefix, has_uint32 / uinteger at the step start, # positions
   uint32_t rp[MAXRP];        // slow path: rejected half-word positions, ascending
-  uint16_t r2s[4096];        // resetter rank in the block -> env slot (control wave)
+  uint16_t r2s[4096];        // resetter rank in the block -> env slot
   uint16_t cand[NCAND];      // the cells of choice() half-words cbase .. cbase + NCAND - 1 (predicted block prefix)
-  uint8_t act[4096];         // env waves: the next step's action index by env slot (the control wave steps resetters)
 };
 
 // ------------------------------------------------------------------ small helpers ----
@@ -409,92 +408,16 @@ __device__ __forceinline__ uint32_t ctrl_slow(const WgParams& P, WgShared& sh, c
   return wtot;
 }
 
-// ------------------------------------------------------------------ one env-step ----
-// One env's transition (msrooms.py:398-412; action failure action_utils.py:84-90 as integer threshold compares):
-// window word x, threshold row t of its action, agent cell c at `el` steps into the episode (after this step).
-// Returns the staged word cell | term << 16 | trunc << 17 | wall bump << 18.
-template <int NA>
-__device__ __forceinline__ uint32_t step_one(uint64_t x, const char* t, const char* mv, uint32_t c, uint32_t el,
-                                             uint32_t goal, uint32_t tlim) {
-  uint32_t eb = 0;  // 2 x effective action
-#pragma unroll
-  for (int j = 0; j + 1 < NA; j += 2) {
-    const ulonglong2 tt = *reinterpret_cast<const ulonglong2*>(t + 8 * j);
-    eb = x > tt.x ? (uint32_t)(2 * (j + 1)) : eb;
-    if (j + 2 < NA) eb = x > tt.y ? (uint32_t)(2 * (j + 2)) : eb;
-  }
-  const uint32_t m = *reinterpret_cast<const uint16_t*>(mv + c * (2 * NA) + eb);
-  const uint32_t nc = m & 0x7FFFu, blocked = m >> 15;
-  const bool tm = nc == goal, tr = el > tlim;
-  return nc | ((uint32_t)tm << 16) | ((uint32_t)tr << 17) | (blocked << 18);
-}
-
 // ------------------------------------------------------------------ the control wave ----
-// The last step's resetters, after its exchange (control wave, beside the env waves' transitions of step k): each
-// one's cell from the last step's choice() words (rank q takes half-word R + q, or, on the slow path, the q-th
-// accepted position past the listed rejections) staged as its reset obs in stg(k - 1); then, when `step_them`, its
-// transition of step k from that cell (the env waves skip these envs this step) staged in stg(k), its done bit in
-// rmask(k).
+// Per step: S(x) published (sx_ready: the env waves' coarse states), the rejection check of its slice, the block's
+// reset count once the env waves' transitions are in, the granule published, S(y) and the next window's base
+// (sy_ready), the all-gather, the resetters' cells (cells_done), then the next step's S(x) = J_used(S(y)). Every
+// constant part of a jump (random(B), the block and lane offsets) is folded into per-lane / per-block tables, so
+// the chain from one exchange to the next publish is two table jumps and one per-lane jump.
 template <int NS, int NA>
-__device__ __forceinline__ void ctrl_resetters(const WgParams& P, WgShared& sh, const Tabs& tb, const Lds& L,
-                                               const char* thr, const char* mv, int k, bool step_them, uint32_t R,
-                                               uint32_t cb, uint32_t slow, uint32_t cbase, uint32_t h, uint32_t u,
-                                               u128 Sy) {
-  constexpr int E = NS * 512;
-  const int lane = threadIdx.x & 63;
-  uint16_t* stp = reinterpret_cast<uint16_t*>(L.stg(k - 1, E));
-  uint32_t* stn = reinterpret_cast<uint32_t*>(L.stg(k, E));
-  const uint64_t* CS = L.CS(k - 1);
-  const int32_t off = sh.rw_off[k & 1];
-  const uint32_t nag = (uint32_t)P.n_agent, goal = (uint32_t)P.goal, tlim = (uint32_t)P.time_limit;
-  const bool nocand = (P.tmode & TM_NOCAND) != 0;
-  for (uint32_t q = (uint32_t)lane; q < cb; q += 64u) {
-    const uint32_t slot = sh.r2s[q];
-    uint32_t p = R + q;
-    bool fromcand = false;
-    if (slow) {
-      const uint32_t n = sh.nrp;
-      for (uint32_t i = 0; i < n; ++i) p += sh.rp[i] <= p ? 1u : 0u;
-    } else {
-      fromcand = p - cbase < (uint32_t)NCAND && !nocand;  // (p >= cbase >= h: never the buffered half)
-    }
-    uint32_t cell;
-    if (fromcand) {
-      cell = sh.cand[p - cbase];
-    } else {
-      uint32_t word;
-      if (h && p == 0) {
-        word = u;
-      } else {
-        const uint32_t hh = p - h, d = hh >> 1;
-        const u128 st = d < 16384u ? draw_state(tb, CS, d) : pcg_jump(tb.jt64, Sy, d + 1u);
-        const uint64_t x = pcg_output(st);
-        word = (hh & 1u) ? (uint32_t)(x >> 32) : (uint32_t)x;
-      }
-      cell = tb.avalid(lemire_value(word, nag));
-    }
-    stp[2 * slot] = (uint16_t)cell;  // the low half of the staged word: the reset obs of step k - 1
-    if (step_them) {
-      const uint32_t v = step_one<NA>(L.RW[slot + (uint32_t)off], thr + (uint32_t)sh.act[slot] * (NA * 8), mv,
-                                      cell, 1u, goal, tlim);
-      stn[slot] = v;
-      if (v & 0x30000u)
-        __hip_atomic_fetch_or(&sh.rmask[k & 1][slot >> 9][(slot >> 6) & 7], 1ull << (slot & 63), __ATOMIC_RELAXED,
-                              __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-  }
-}
-
-// Per step k: S(x_k) and the predicted base of window k + 1 published (sx_ready); the rejection check of this
-// block's slice; the last step's resetters (cells, and their transitions of step k: ctrl_resetters); this block's
-// reset count once the env waves' transitions are in, the granule published; the resetters ranked (r2s); the
-// candidate cells; the all-gather; the next step's window offset (off_ready: the env waves start step k + 1's
-// transitions now, the resetters' cells come after); S(x_{k+1}) = J_used(S(y_k)). Every constant part of a jump
-// (random(B), the block and lane offsets) is folded into per-lane / per-block tables.
-template <int NS, int NA>
-__device__ __forceinline__ void wg_ctrl(const WgParams& P, WgShared& sh, const Tabs& tb, const Lds& L, const char* dyn,
-                                        int K) {
+__device__ __forceinline__ void wg_ctrl(const WgParams& P, WgShared& sh, const Tabs& tb, const Lds& L, int K) {
   const int lane = threadIdx.x & 63, beta = (int)blockIdx.x, G = (int)gridDim.x;
+  constexpr int E = NS * 512;
   GridCtl* C = P.ctl;
   u128 Sx = mk128(C->s_hi, C->s_lo);
   uint32_t h = C->has_u32, u = C->uinteger;
@@ -502,59 +425,31 @@ __device__ __forceinline__ void wg_ctrl(const WgParams& P, WgShared& sh, const T
   uint32_t Rprev = (uint32_t)(((uint64_t)bprev * (uint64_t)blockIdx.x) / (uint64_t)gridDim.x);  // a first guess
   const uint32_t ts0 = C->wstep + 1u;  // tag step of k = 0 (tags are never 0: the slots start zeroed)
   const PcgJump jr = P.jrej[(size_t)beta * 64 + lane];
-  const PcgJump jb = P.jblk[2 * beta];
+  const PcgJump jb = P.jblk[2 * beta], jpro = P.jblk[2 * beta + 1];
   const PcgJump jB = P.jB;
   const uint32_t nag = (uint32_t)P.n_agent, thra = P.thr_agent;
   const int32_t H = P.halo;
   const uint32_t bias = (uint32_t)P.wg_bias;
-  const char* thr = dyn + P.lds.thr;
-  const char* mv = dyn + P.lds.move;
   uint32_t* derr = &C->err;
-  // the last step's choice() call, whose resetters' cells are drawn during this step
-  uint32_t pR = 0, pcb = 0, pslow = 0, pcbase = 0, ph = 0, pu = 0;
-  u128 pSy = (u128)0;
-  uint32_t wtarget = EW;  // fill_done once this step's window is final (fills and regenerations so far)
-  lds_barrier();          // P1: tables staged, counters zeroed
-  if (lane == 0) {        // step 0's window (the env waves' prologue fill) is exact: word 0 is S(x_0 + 1 + E beta - heff)
+  lds_barrier();  // P1: tables staged, counters zeroed
+  // the first window: step 0's own random(B) words, exact: word 0 is S(x_0 + 1 + E beta - heff)
+  if (lane == 0) {
+    const u128 s = apply_jump(jpro, Sx);
+    sh.rw[0][0] = hi64(s);
+    sh.rw[0][1] = lo64(s);
     sh.rw_off[0] = beta == 0 ? 1 : H;
-    sh.wfix[0] = 0;
     lds_release();
-    __hip_atomic_store(&sh.off_ready, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_store(&sh.pro, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   LSTAMP(P, 1);
   for (int k = 0; k < K; ++k) {
     const uint32_t ts = ts0 + (uint32_t)k;
-    if (lane == 0) {  // S(x_k): the env waves' coarse states of this step's choice() stream
+    if (lane == 0) {
       sh.sx[k & 1][0] = hi64(Sx);
       sh.sx[k & 1][1] = lo64(Sx);
       lds_release();
       __hip_atomic_store(&sh.sx_ready, (uint32_t)k + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    // the last step's resetters: their cells, and their transitions of this step (beside the env waves' own)
-    if (P.tmode & TM_CTRLLOW) __builtin_amdgcn_s_setprio(1);
-    if (k > 0) {
-      reinterpret_cast<uint64_t*>(sh.rmask[k & 1])[lane] = 0ull;  // (NS * EW <= 64 words)
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-      lds_wait(&sh.fill_done, wtarget, derr);                                                // this step's window
-      if (k >= NSTG) lds_wait(&sh.st_done, (uint32_t)SW * (uint32_t)(k - NSTG + 1), derr);  // stg(k) copied out
-      ctrl_resetters<NS, NA>(P, sh, tb, L, thr, mv, k, true, pR, pcb, pslow, pcbase, ph, pu, pSy);
-    }
-    // the next step's window, around the used predicted from the last b (the env waves fill it once nobody reads
-    // this step's window: after every transition of this step, theirs and the resetters')
-    uint32_t used_p, hp;
-    words_to_draws(bprev + bias, h, used_p, hp);
-    int32_t heff_p;
-    const u128 Srw = rw_base(tb, jb, Sx, used_p, beta, heff_p);
-    if (lane == 0) {
-      sh.rw[(k + 1) & 1][0] = hi64(Srw);
-      sh.rw[(k + 1) & 1][1] = lo64(Srw);
-      lds_release();
-      __hip_atomic_store(&sh.cells_done, (uint32_t)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      __hip_atomic_store(&sh.rtr_done, (uint32_t)k + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    WSTAMP(P, k, 2);
     // Lemire check of this block's slice of the choice() stream (u64 draws 62 beta + 1 .. + 62 after random(B))
     uint32_t rj = 0;
     if (lane < SLICE) {
@@ -564,31 +459,31 @@ __device__ __forceinline__ void wg_ctrl(const WgParams& P, WgShared& sh, const T
       rj = lemire_rejected(u, nag, thra) ? 1u : 0u;  // the buffered half is hw 0
     }
     const uint32_t rejc = wave_sum(rj);
-    if (P.tmode & TM_CTRLLOW) __builtin_amdgcn_s_setprio(3);
     WSTAMP(P, k, 6);
     // this block's reset count, published
     lds_wait(&sh.trans_done, (uint32_t)EW * (uint32_t)(k + 1), derr);
     WSTAMP(P, k, 7);
-    const uint64_t mw = lane < NS * EW ? (sh.mask[lane >> 3][lane & 7] | sh.rmask[k & 1][lane >> 3][lane & 7]) : 0ull;
-    const uint32_t mc = (uint32_t)__builtin_popcountll(mw);
-    const uint32_t mincl = wave_incl_scan(mc);
-    const uint32_t cb = (uint32_t)__builtin_amdgcn_readlane((int)mincl, 63);
+    const uint32_t cb = wave_sum(lane < NS * EW ? (uint32_t)__builtin_popcountll(sh.mask[lane >> 3][lane & 7]) : 0u);
     uint64_t* slots = P.slots + (size_t)(ts & 1u) * 2 * G;
     publish(P, slots, ts << 6, rejc, cb);
     WSTAMP(P, k, 8);
-    const u128 Sy = apply_jump(jB, Sx);  // S(y_k), after this step's random(B)
-    // while the granules travel: the resetters' ranks in env order -> env slots (word lane = (slot k, wave w))
-    {
-      uint32_t r = mincl - mc;
-      uint64_t m = mw;
-      while (m) {
-        const uint32_t bit = (uint32_t)__builtin_ctzll(m);
-        m &= m - 1;
-        sh.r2s[r++] = (uint16_t)((uint32_t)(lane >> 3) * 512u + (uint32_t)(lane & 7) * 64u + bit);
-      }
+    // while the granules travel: S(y) and the next step's window, around the used predicted from the last b
+    const u128 Sy = apply_jump(jB, Sx);
+    uint32_t used_p, hp;
+    words_to_draws(bprev + bias, h, used_p, hp);
+    int32_t heff_p;
+    const u128 Srw = rw_base(tb, jb, Sx, used_p, beta, heff_p);
+    if (lane == 0) {
+      sh.sy[k & 1][0] = hi64(Sy);
+      sh.sy[k & 1][1] = lo64(Sy);
+      sh.rw[(k + 1) & 1][0] = hi64(Srw);
+      sh.rw[(k + 1) & 1][1] = lo64(Srw);
+      lds_release();
+      __hip_atomic_store(&sh.sy_ready, (uint32_t)k + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    // and the cells of the choice() half-words around the block prefix predicted by the last step's, so that the
-    // resetters' cells are one LDS read each. Candidate i is half-word cbase + i; cbase = 2 d0 + h.
+    // While the granules travel (the longest wait of a step): the cells of the choice() half-words around the block
+    // prefix predicted by the last step's, so that the resetters' cells after the exchange are one LDS read each.
+    // Candidate i is half-word cbase + i; cbase = 2 d0 + h, draws d0 .. d0 + NCAND / 2 - 1 (both halves each).
     const uint64_t* CS = L.CS(k);
     lds_wait(&sh.cs_done, (uint32_t)EW * (uint32_t)(k + 1), derr);
     const uint32_t d0 = min(Rprev > CAND_W + h ? (Rprev - CAND_W - h) >> 1 : 0u, 16384u - NCAND / 2);  // CS reach
@@ -622,43 +517,61 @@ __device__ __forceinline__ void wg_ctrl(const WgParams& P, WgShared& sh, const T
     const uint32_t rtot = wave_sum(grej(g[0]) + grej(g[1]) + grej(g[2]) + grej(g[3]));
     const bool slow = rtot != 0 || b > 124u * (uint32_t)G;
     uint32_t used, h2;
+    // (also before cells_done when nothing is drawn: every env wave has read this step's masks)
+    lds_wait(&sh.r2s_done, (uint32_t)EW * (uint32_t)(k + 1), derr);
     if (!slow) {
       words_to_draws(b, h, used, h2);
-    } else {
-      const uint32_t wtot = ctrl_slow(P, sh, tb, CS, Sy, h, u, b, ts, g);  // (lists the rejected positions: sh.rp)
-      words_to_draws(wtot, h, used, h2);
-    }
-    // the next step's window offset; a window more than H off is regenerated exactly by the env waves first
-    if (k + 1 < K) {
-      int32_t off = heff_p + (int32_t)used - (int32_t)used_p;
-      uint32_t fix = 0;
-      wtarget += EW;
-      if (off < 0 || off > 2 * H) {
-        int32_t heff;
-        const u128 s = rw_base(tb, jb, Sx, used, beta, heff);
-        off = heff;
-        fix = 2u;
-        wtarget += EW;
-        if (lane == 0) {
-          sh.rwx[(k + 1) & 1][0] = hi64(s);
-          sh.rwx[(k + 1) & 1][1] = lo64(s);
+      if (cb) {  // this block's resetters' cells: rank q takes half-word R + q
+        uint16_t* st = reinterpret_cast<uint16_t*>(L.stg(k, E));
+        for (uint32_t q = (uint32_t)lane; q < cb; q += 64u) {
+          const uint32_t hw = R + q;
+          const uint32_t slot = sh.r2s[q];
+          uint32_t cell;
+          if (hw - cbase < (uint32_t)NCAND && !(P.tmode & TM_NOCAND)) {  // (hw >= cbase >= h: never the buffered half)
+            cell = sh.cand[hw - cbase];
+          } else {
+            uint32_t word;
+            if (h && hw == 0) {
+              word = u;
+            } else {
+              const uint32_t hh = hw - h;
+              const uint64_t x = pcg_output(draw_state(tb, CS, hh >> 1));
+              word = (hh & 1u) ? (uint32_t)(x >> 32) : (uint32_t)x;
+            }
+            cell = tb.avalid(lemire_value(word, nag));
+          }
+          st[2 * slot] = (uint16_t)cell;  // the low half of the staged word
         }
       }
+    } else {
+      const uint32_t wtot = ctrl_slow(P, sh, tb, CS, Sy, h, u, b, ts, g);
+      words_to_draws(wtot, h, used, h2);
       if (lane == 0) {
-        sh.rw_off[(k + 1) & 1] = off;
-        sh.wfix[(k + 1) & 1] = fix;
-        lds_release();
-        __hip_atomic_store(&sh.off_ready, (uint32_t)k + 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        sh.R = R;
+        sh.h = h;
+        sh.u = u;
       }
     }
+    // the next step's window offset; a window more than H off is regenerated exactly by the env waves
+    int32_t off = heff_p + (int32_t)used - (int32_t)used_p;
+    uint32_t fix = slow ? 1u : 0u;
+    if (k + 1 < K && (off < 0 || off > 2 * H)) {
+      int32_t heff;
+      const u128 s = rw_base(tb, jb, Sx, used, beta, heff);
+      off = heff;
+      fix |= 2u;
+      if (lane == 0) {
+        sh.rw[(k + 1) & 1][0] = hi64(s);
+        sh.rw[(k + 1) & 1][1] = lo64(s);
+      }
+    }
+    if (lane == 0) {
+      sh.rw_off[(k + 1) & 1] = off;
+      sh.fix[k & 1] = fix;
+      lds_release();
+      __hip_atomic_store(&sh.cells_done, (uint32_t)k + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
     WSTAMP(P, k, 10);
-    pR = R;
-    pcb = cb;
-    pslow = slow ? 1u : 0u;
-    pcbase = cbase;
-    ph = h;
-    pu = u;
-    pSy = Sy;
     // the next step's state S(x_{t+1}) = S(y_t + used)
     Sx = jump_any(tb, Sy, used);
     if (used) u = (uint32_t)(pcg_output(Sx) >> 32);  // numpy keeps the last drawn high half in uinteger
@@ -666,13 +579,6 @@ __device__ __forceinline__ void wg_ctrl(const WgParams& P, WgShared& sh, const T
     bprev = b;
     Rprev = R;
     WSTAMP(P, k, 12);
-  }
-  // the last step's resetters' cells (the env waves write them into the env state: the next launch's first step
-  // takes them as ordinary envs)
-  ctrl_resetters<NS, NA>(P, sh, tb, L, thr, mv, K, false, pR, pcb, pslow, pcbase, ph, pu, pSy);
-  if (lane == 0) {
-    lds_release();
-    __hip_atomic_store(&sh.cells_done, (uint32_t)K, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   LSTAMP(P, 3);
   if (beta == 0 && lane == 0) {
@@ -690,6 +596,34 @@ struct Acc {
   uint32_t eps = 0, ngoal = 0, nwall = 0, lens = 0;
 };
 
+// Slow path: place this lane's resetters exactly (ranks -> positions past the listed rejections -> words).
+template <int NS>
+__device__ __forceinline__ void wg_env_slow(const WgParams& P, WgShared& sh, const Tabs& tb, const uint64_t* CS,
+                                            int k, char* stg, uint32_t dn, const uint32_t (&pre)[NS],
+                                            const uint64_t (&bm)[NS], uint32_t (&ae)[NS]) {
+  const int lg = threadIdx.x;
+  const u128 Sy = mk128(sh.sy[k & 1][0], sh.sy[k & 1][1]);
+  const uint32_t R = sh.R, h = sh.h, u = sh.u, n = sh.nrp;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    if (!((dn >> s) & 1u)) continue;
+    uint32_t p = R + pre[s] + mbcnt(bm[s]);
+    for (uint32_t q = 0; q < n; ++q) p += sh.rp[q] <= p ? 1u : 0u;
+    uint32_t word;
+    if (h && p == 0) {
+      word = u;
+    } else {
+      const uint32_t hh = p - h, d = hh >> 1;
+      const u128 st = d < 16384u ? draw_state(tb, CS, d) : pcg_jump(tb.jt64, Sy, d + 1u);
+      const uint64_t x = pcg_output(st);
+      word = (hh & 1u) ? (uint32_t)(x >> 32) : (uint32_t)x;
+    }
+    const uint32_t cell = tb.avalid(lemire_value(word, (uint32_t)P.n_agent));
+    reinterpret_cast<uint16_t*>(stg)[2 * (s * 512 + lg)] = (uint16_t)cell;
+    ae[s] = cell;
+  }
+}
+
 // Fill the window: word j = m * 512 + lg is the base state advanced by j (this lane: jump by lg, then by 512).
 __device__ __forceinline__ void fill_window(uint64_t* RW, const PcgJump& jl, const PcgJump& j512, int nw, u128 base, int lg) {
   u128 s = apply_jump(jl, base);
@@ -699,10 +633,6 @@ __device__ __forceinline__ void fill_window(uint64_t* RW, const PcgJump& jl, con
   }
 }
 
-// Per step k: the window offset (off_ready; a regeneration first if flagged), the transitions of every env except
-// the last step's resetters (the control wave steps those from their new cells: `rs`), the coarse states of step
-// k's choice() stream, the next step's window (once nobody reads this one), then the resetters' outcomes taken
-// from the staging (their new cell, or another reset).
 template <int NS, int NA>
 __device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Tabs& tb, const Lds& L, const char* dyn,
                                        const int32_t* __restrict__ act, int K, Acc& acc, int32_t* __restrict__ obs,
@@ -743,34 +673,27 @@ __device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Ta
     arow[k] = action_row<NA>(anext[k], derr);
     acc.lens += ae[k] >> 16;  // episode lengths: + elapsed at the start - elapsed at the end + steps
   }
+  lds_wait(&sh.pro, 1u, derr);  // the first window's offset
+  if (w == 0) LSTAMP(P, 7);
   if (lane == 0) lds_add(&sh.fill_done, 1u);
   uint32_t fill_target = EW;
-  uint32_t rs = 0;  // this lane's slots whose env the control wave steps this step (the last step's resetters)
+  uint64_t bm[NS];
+  uint32_t pre[NS];
   for (int k = 0; k < K; ++k) {
     char* stg = L.stg(k, E);
     if (k + 1 < K && !(tmode & TM_LATEACT)) {
 #pragma unroll
       for (int s = 0; s < NS; ++s) anext[s] = act[(size_t)(k + 1) * B + e0 + (size_t)s * 512 + lg];
     }
-    // (the waits that are normally over already come first: after the offset only its two words are read)
     lds_wait(&sh.fill_done, fill_target, derr);                  // every env wave's part of this step's window
     if (k >= NSTG) lds_wait(&sh.st_done, (uint32_t)SW * (uint32_t)(k - NSTG + 1), derr);  // this staging buffer copied out
-    lds_wait(&sh.off_ready, (uint32_t)k + 1u, derr);  // this step's window offset (after the last exchange)
     if (!(tmode & TM_NOPRIO)) __builtin_amdgcn_s_setprio(2);  // the transitions are on the critical path
-    if (w == 0 && k == 0) LSTAMP(P, 7);
-    const int32_t off = sh.rw_off[k & 1];
-    if (sh.wfix[k & 1] & 2u) {  // the prediction missed the window: regenerate it exactly
-      fill_window(L.RW, jrw, j512, nw, mk128(sh.rwx[k & 1][0], sh.rwx[k & 1][1]), lg);
-      lds_release();
-      if (lane == 0) lds_add(&sh.fill_done, 1u);
-      fill_target += EW;
-      lds_wait(&sh.fill_done, fill_target, derr);
-    }
     if (w == 0) WSTAMP(P, k, 0);
     // ---- transitions (the critical path) ----
     // Phased over the env slots so that their LDS round trips overlap: every slot's window word and threshold
     // row first, then the effective actions, the move-table entries, and the staged outputs last (a store to
     // the staging area between two slots' loads would order them: all of it is one LDS array to the compiler).
+    const int32_t off = sh.rw_off[k & 1];
     uint32_t dn = 0;
     uint32_t mvo[NS];
 #pragma unroll
@@ -790,28 +713,26 @@ __device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Ta
 #pragma unroll
     for (int s = 0; s < NS; ++s) mm[s] = *reinterpret_cast<const uint16_t*>(mv + mvo[s]);
     uint32_t sv[NS];
-    uint64_t bm[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-      const bool mine = !((rs >> s) & 1u);
       const uint32_t m = mm[s];
       const uint32_t nc = m & 0x7FFFu, blocked = m >> 15;
       const uint32_t el = (ae[s] >> 16) + 1u;
-      const bool tm = nc == goal, tr = el > tlim, done = tm || tr;
-      sv[s] = nc | ((uint32_t)tm << 16) | ((uint32_t)tr << 17) | (blocked << 18);
-      if (mine) ae[s] = done ? nc : (nc | (el << 16));
-      bm[s] = ballot(done && mine);
-      dn |= (uint32_t)(done && mine) << s;
-      acc.ngoal += (tm && mine) ? 1u : 0u;
-      acc.nwall += (blocked && !tm && mine) ? 1u : 0u;
+      const bool term = nc == goal, trunc = el > tlim, done = term || trunc;
+      sv[s] = nc | ((uint32_t)term << 16) | ((uint32_t)trunc << 17) | (blocked << 18);
+      ae[s] = done ? nc : (nc | (el << 16));
+      bm[s] = ballot(done);
+      dn |= (uint32_t)done << s;
+      acc.ngoal += term ? 1u : 0u;
+      acc.nwall += (blocked && !term) ? 1u : 0u;
     }
     if (lane == 0) {
 #pragma unroll
       for (int s = 0; s < NS; ++s) sh.mask[s][w] = bm[s];
     }
 #pragma unroll
-    for (int s = 0; s < NS; ++s)
-      if (!((rs >> s) & 1u)) reinterpret_cast<uint32_t*>(stg)[s * 512 + lg] = sv[s];
+    for (int s = 0; s < NS; ++s) reinterpret_cast<uint32_t*>(stg)[s * 512 + lg] = sv[s];
+    acc.eps += (uint32_t)__builtin_popcount(dn);
     lds_release();
     if (lane == 0) lds_add(&sh.trans_done, 1u);
     if (!(tmode & TM_NOPRIO) && !(tmode & TM_ENVHIGH)) __builtin_amdgcn_s_setprio(0);
@@ -821,8 +742,9 @@ __device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Ta
 #pragma unroll
       for (int s = 0; s < NS; ++s) anext[s] = act[(size_t)(k + 1) * B + e0 + (size_t)s * 512 + lg];
     }
-    // ---- while the exchange runs: coarse states, the next step's window ----
+    // ---- while the exchange runs: coarse states, resetter listing, the next step's window ----
     lds_wait(&sh.sx_ready, (uint32_t)k + 1u, derr);
+    if (w == 0) WSTAMP(P, k, 2);
     {
       const u128 cs = apply_jump(jcs, mk128(sh.sx[k & 1][0], sh.sx[k & 1][1]));  // S(x + B + 32 lg + 1)
       reinterpret_cast<ulonglong2*>(L.CS(k))[lg] = ulonglong2{lo64(cs), hi64(cs)};
@@ -830,57 +752,62 @@ __device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Ta
     lds_release();
     if (lane == 0) lds_add(&sh.cs_done, 1u);
     if (w == 0) WSTAMP(P, k, 3);
-    if (k + 1 < K) {
-      lds_wait(&sh.trans_done, (uint32_t)EW * (uint32_t)(k + 1), derr);  // nobody reads this step's window now
-      lds_wait(&sh.rtr_done, (uint32_t)k + 1u, derr);
-      if (w == 0) WSTAMP(P, k, 4);
-      const u128 Srw = mk128(sh.rw[(k + 1) & 1][0], sh.rw[(k + 1) & 1][1]);
-      if (!(tmode & TM_NOFILL)) fill_window(L.RW, jrw, j512, nw, Srw, lg);
+    lds_wait(&sh.trans_done, (uint32_t)EW * (uint32_t)(k + 1), derr);  // every wave's masks; nobody reads the window now
+    {
+      const uint32_t c = lane < NS * EW ? (uint32_t)__builtin_popcountll(sh.mask[lane >> 3][lane & 7]) : 0u;
+      const uint32_t ex = wave_incl_scan(c) - c;
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
-        arow[s] = action_row<NA>(anext[s], derr);
-        sh.act[s * 512 + lg] = (uint8_t)(arow[s] / (NA * 8));  // for the control wave (resetters of step k + 1)
+        pre[s] = (uint32_t)__builtin_amdgcn_readlane((int)ex, s * EW + w);
+        if ((dn >> s) & 1u) sh.r2s[pre[s] + mbcnt(bm[s])] = (uint16_t)(s * 512 + lg);
       }
+    }
+    lds_release();
+    if (lane == 0) lds_add(&sh.r2s_done, 1u);
+    if (w == 0) WSTAMP(P, k, 4);
+    if (k + 1 < K) {
+      lds_wait(&sh.sy_ready, (uint32_t)k + 1u, derr);
+      const u128 Srw = mk128(sh.rw[(k + 1) & 1][0], sh.rw[(k + 1) & 1][1]);
+      if (!(tmode & TM_NOFILL)) fill_window(L.RW, jrw, j512, nw, Srw, lg);
       lds_release();
       if (lane == 0) lds_add(&sh.fill_done, 1u);
       fill_target += EW;
-      if (w == 0) WSTAMP(P, k, 5);
-      if (w == EW - 1) WSTAMP(P, k, 15);
-    }
-    // ---- the last step's resetters, stepped by the control wave: their outcome from the staging ----
-    lds_wait(&sh.rtr_done, (uint32_t)k + 1u, derr);
-    if (rs) {
 #pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        if ((rs >> s) & 1u) {
-          const uint32_t v = reinterpret_cast<const uint32_t*>(stg)[s * 512 + lg];
-          const bool d = (v & 0x30000u) != 0, tm = (v >> 16) & 1u;
-          if (!d) ae[s] = (v & 0x7FFFu) | (1u << 16);
-          dn |= (uint32_t)d << s;
-          acc.ngoal += tm ? 1u : 0u;
-          acc.nwall += (((v >> 18) & 1u) && !tm) ? 1u : 0u;
-        }
-      }
+      for (int s = 0; s < NS; ++s) arow[s] = action_row<NA>(anext[s], derr);
     }
-    acc.eps += (uint32_t)__builtin_popcount(dn);
-    rs = dn;
+    if (w == 0) WSTAMP(P, k, 5);
+    if (w == EW - 1) WSTAMP(P, k, 15);
+    // ---- the exchange's outcome: the resetters' cells ----
+    lds_wait(&sh.cells_done, (uint32_t)k + 1u, derr);
     if (w == 0) WSTAMP(P, k, 11);
-    if (k == K - 1) {  // the launch's last step: its outputs (and the reset cells) straight from the env waves
-      lds_wait(&sh.cells_done, (uint32_t)K, derr);
+    const uint32_t fix = sh.fix[k & 1];
+    if (fix & 1u) {
+      wg_env_slow<NS>(P, sh, tb, L.CS(k), k, stg, dn, pre, bm, ae);
+    } else {
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+        if ((dn >> s) & 1u) ae[s] = reinterpret_cast<const uint16_t*>(stg)[2 * (s * 512 + lg)];
+    }
+    lds_release();
+    if (lane == 0) lds_add(&sh.res_done, 1u);
+    if (k == K - 1 && !(tmode & TM_NOSTORE)) {  // the launch's last step: its outputs straight from the env waves
       const uint32_t* st = reinterpret_cast<const uint32_t*>(stg);
       const size_t base = (size_t)k * B + e0 + (size_t)lg;
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
         const uint32_t v = st[s * 512 + lg];
-        if ((dn >> s) & 1u) ae[s] = v & 0xFFFFu;  // reset: the new cell, elapsed 0
-        if (!(tmode & TM_NOSTORE)) {
-          const size_t e = base + (size_t)s * 512;
-          obs[e] = tb.ocell(v & 0xFFFFu);
-          rew[e] = (v & 0x10000u) ? P.r_goal : ((v & 0x40000u) ? P.r_wall : P.r_step);
-          term[e] = (uint8_t)((v >> 16) & 1u);
-          trunc[e] = (uint8_t)((v >> 17) & 1u);
-        }
+        const size_t e = base + (size_t)s * 512;
+        obs[e] = tb.ocell(v & 0xFFFFu);
+        rew[e] = (v & 0x10000u) ? P.r_goal : ((v & 0x40000u) ? P.r_wall : P.r_step);
+        term[e] = (uint8_t)((v >> 16) & 1u);
+        trunc[e] = (uint8_t)((v >> 17) & 1u);
       }
+    }
+    if ((fix & 2u) && k + 1 < K) {  // the prediction missed the window: regenerate it exactly
+      fill_window(L.RW, jrw, j512, nw, mk128(sh.rw[(k + 1) & 1][0], sh.rw[(k + 1) & 1][1]), lg);
+      lds_release();
+      if (lane == 0) lds_add(&sh.fill_done, 1u);
+      fill_target += EW;
     }
   }
 #pragma unroll
@@ -910,7 +837,7 @@ __device__ __forceinline__ void wg_store(const WgParams& P, WgShared& sh, const 
   uint32_t* derr = &P.ctl->err;
   lds_barrier();  // P1
   for (int k = 0; k + 1 < K; ++k) {  // (the env waves write the last step themselves)
-    lds_wait(&sh.cells_done, (uint32_t)k + 1u, derr);  // step k's staging is final
+    lds_wait(&sh.res_done, (uint32_t)EW * (uint32_t)(k + 1), derr);
     // and out of the way of the next step's transitions (the critical path): start once they are done, except for
     // a launch's last steps, whose copies are the launch's tail
     if (k + WG_EAGER_TAIL < K && !(tmode & TM_EAGERSTORE))
@@ -993,17 +920,16 @@ __global__ __launch_bounds__(TPB) void wgrid_rollout(const WgParams* __restrict_
     if (wid == EW + 1) LSTAMP(P, 6);
   }
   if (tid == EW * 64) {
-    sh.trans_done = sh.cs_done = sh.fill_done = sh.st_done = 0;
-    sh.sx_ready = sh.off_ready = sh.rtr_done = sh.cells_done = 0;
-    sh.wfix[0] = sh.wfix[1] = 0;
+    sh.trans_done = sh.cs_done = sh.r2s_done = sh.fill_done = sh.res_done = sh.st_done = 0;
+    sh.sx_ready = sh.sy_ready = sh.cells_done = sh.pro = 0;
+    sh.fix[0] = sh.fix[1] = 0;
   }
-  if (wid == CWAVE) reinterpret_cast<uint64_t*>(sh.rmask)[lane] = 0ull;  // (step 0's: nothing stepped by the control wave)
   const Tabs tb(dyn, P);
   const Lds L(dyn, P, E);
   Acc acc;
   if (wid == CWAVE) {
     __builtin_amdgcn_s_setprio(3);  // the exchange is on every step's critical path
-    wg_ctrl<NS, NA>(P, sh, tb, L, dyn, K);
+    wg_ctrl<NS, NA>(P, sh, tb, L, K);
   } else if (wid > CWAVE) {
     if (P.tmode & TM_STORELOW) __builtin_amdgcn_s_setprio(0);
     else __builtin_amdgcn_s_setprio(1);

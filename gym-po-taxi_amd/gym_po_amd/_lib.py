@@ -107,6 +107,8 @@ SIGNATURES = {
     "gp_exp_libm": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                    ctypes.c_int64, ctypes.c_int]),
     "gp_exp_host_variant": (ctypes.c_int, []),
+    "gp_philox_blocks": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32), ctypes.c_int, ctypes.POINTER(ctypes.c_uint32),
+                                        ctypes.c_int64]),
     "gp_zig_log1p_neg": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                         ctypes.c_int64]),
     "gp_debug_set": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int64]),

@@ -7,11 +7,11 @@ the task/episode resets and the observation builder run in the HIP kernels of li
 RNG: `"philox"` (default, the fast path) draws from the *exact* law of the reference's reset
 (`multinomial(ns, p, b).argmax(-1)`, :344-352; `reset_distribution`, computed in closed form) and from the
 exact passenger/destination law of :354-364, counter-based per (env, step). `"numpy"` follows the
-reference's own PCG64 stream draw for draw (one workgroup walks numpy's random_multinomial /
-random_binomial_inversion and the buffered Lemire `integers` calls, csrc/taxi.hip), so a seeded run
-reproduces the reference's trajectories and final `np_random` state; it is a parity mode (a reset
-costs ~300 sequential binomials per env). `"replay"` takes caller-decided draws. The step itself
-uses no randomness.
+reference's own PCG64 stream draw for draw (the transitions and the reset ranking grid-wide above 1,024
+envs; numpy's random_multinomial / random_binomial_inversion reset rows and the buffered Lemire `integers`
+calls walked in stream order, csrc/taxi.hip), so a seeded run reproduces the reference's trajectories and
+final `np_random` state; it is a parity mode (a reset row is ~300 dependent binomial draws).
+`"replay"` takes caller-decided draws. The step itself uses no randomness.
 
 Extra keyword arguments beyond the reference: `device`, `rng_mode`, `one_hot` (emit the observation
 index one-hot as uint8 [B, n_obs], a build-side encoding).

@@ -295,6 +295,10 @@ int gp_zig_log1p_neg(const double* u, double* out, int64_t n);
  * distributions.c). fma != 0: the -mfma build glibc selects on CPUs with FMA (x86-64 ifunc), else the plain one.
  * Host-only check entry for the CPU tests. */
 int gp_exp_libm(const double* x, double* out, int64_t n, int fma);
+/* Philox4x32-R blocks (R = rounds: 7 or 10) of n counters ctr[6 i .. 6 i + 5] = {c0, c1, c2, c3, k0, k1} into
+ * out[4 i .. 4 i + 3], computed by the header the philox-mode kernels inline (gp_common.h philox4x32<R>).
+ * Host-only check entry for the CPU tests (oracle/philox.py is checked against it). */
+int gp_philox_blocks(const uint32_t* ctr, int rounds, uint32_t* out, int64_t n);
 /* Which build of the C library's exp this host runs (the one numpy's distributions get): 1 = the -mfma build,
  * 0 = the plain build, -1 = neither restatement matches (exact-stream exp-dependent branches then follow the FMA
  * build: parity unpinned). Decided once per process by comparing libm with both restatements where they differ;

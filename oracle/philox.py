@@ -1,10 +1,13 @@
-"""ORACLE / TEST INFRASTRUCTURE — Philox4x32-10 and Lemire bounded draws in numpy (vectorised).
+"""ORACLE / TEST INFRASTRUCTURE — Philox4x32-R and Lemire bounded draws in numpy (vectorised).
 
 Restates the counter-based generator of the device's `rng_mode="philox"` (gym-po-taxi_amd/csrc/
-gp_common.h: philox4x32_10, lemire_value) so that build-defined envs (grid Ant-Tag) can be checked
-bit-exactly in philox mode. Philox4x32-10 is the published algorithm of Salmon et al. (SC'11,
-"Parallel random numbers: as easy as 1, 2, 3"): 10 rounds of two 32x32->64 multiplies with the
-multipliers 0xD2511F53 / 0xCD9E8D57 and the Weyl key increments 0x9E3779B9 / 0xBB67AE85.
+gp_common.h: philox4x32<R>, philox4x32_10, lemire_value) so that build-defined envs (grid Ant-Tag) can be checked
+bit-exactly in philox mode. Philox4x32-R is the published algorithm of Salmon et al. (SC'11,
+"Parallel random numbers: as easy as 1, 2, 3"): R rounds of two 32x32->64 multiplies with the
+multipliers 0xD2511F53 / 0xCD9E8D57 and the Weyl key increments 0x9E3779B9 / 0xBB67AE85. R = 10 (Random123's
+default; pinned by its known-answer vectors, tests/test_oracle_extra.py) in every philox-mode kernel; R = 7 (the
+paper's Crush-resistant minimum) is a build option of C-ROOMS (csrc/crooms.hip CR_PHILOX_ROUNDS): the same round
+function with fewer iterations, both checked against the device header's host copy (tests/test_philox_cpu.py).
 
 Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline may use this module.
 """
@@ -17,10 +20,15 @@ MASK32 = np.uint64(0xFFFFFFFF)
 
 def philox4x32_10(c0, c1, c2, c3, k0, k1):
     """Counters (uint32 arrays / scalars, broadcast) and key -> 4 uint32 arrays."""
+    return philox4x32(c0, c1, c2, c3, k0, k1, rounds=10)
+
+
+def philox4x32(c0, c1, c2, c3, k0, k1, rounds=10):
+    """Philox4x32-`rounds`: counters (uint32 arrays / scalars, broadcast) and key -> 4 uint32 arrays."""
     c0, c1, c2, c3 = (np.asarray(c, dtype=np.uint64) & MASK32 for c in (c0, c1, c2, c3))
     c0, c1, c2, c3 = np.broadcast_arrays(c0, c1, c2, c3)
     k0, k1 = int(k0) & 0xFFFFFFFF, int(k1) & 0xFFFFFFFF
-    for _ in range(10):
+    for _ in range(rounds):
         p0 = M0 * c0
         p1 = M1 * c2
         hi0, lo0 = p0 >> np.uint64(32), p0 & MASK32

@@ -44,11 +44,6 @@ for task in "${@:-tests ab bench floor}"; do
         GYM_PO_AMD_LIB=$LD/libgympo_amd_stamps.so run 200 $O/wstamps_k$K.log python -u tools/wstamps.py 1048576 $K
         cat $O/wstamps_k$K.log
       done ;;
-    r5stamps)  # the round-5 schedule's stamps (libgympo_amd_r5stamps.so, the same LDS stamps) for comparison
-      for K in ${STK:-64 20}; do
-        GYM_PO_AMD_LIB=$LD/libgympo_amd_r5stamps.so run 200 $O/r5stamps_k$K.log python -u tools/wstamps_r5.py 1048576 $K
-        cat $O/r5stamps_k$K.log
-      done ;;
     floorprof)  # the launch-footprint probe under rocprofv3 (dispatch-timestamp durations of the same launches)
       run 300 $O/floorprof.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/floorprof -o p -- python3 -u tools/launch_floor.py 60
       for f in $(find $O/floorprof -name "*kernel_stats.csv"); do cp $f $O/floor_kernel_stats.csv; cat $f; done ;;

@@ -2,14 +2,13 @@
 
     python gym-po-taxi_amd/build.py --stamps && python tools/wstamps.py [B] [K]
 
-Stamps are s_memrealtime (100 MHz, synchronous across XCDs), per block and step k (round-6 schedule: the control
-wave steps the last step's resetters itself, the env waves start a step once its window offset is published):
-  env wave 0: 0 step start, 1 transitions done, 3 coarse states done, 4 window free (next fill starts), 5 next
-              window filled, 11 resetters' outcomes taken; env wave 7: 15 next window filled
-  control:    2 last step's resetters done (cells + transitions) and the next window's base published, 6 rejection
-              check done, 7 transitions seen, 8 granule publish, 9 all-gather done, 10 next offset published,
-              12 next state done
-  store wave: 13 copy start, 14 copy issued
+Stamps are s_memrealtime (100 MHz, synchronous across XCDs), kept in LDS during the launch (round 6: a global store
+per stamp was waited for by later vmcnt(0) waits and stretched the phases), per block and step k:
+  env wave 0: 0 step start, 1 transitions done, 2 S(y) seen, 3 coarse states done, 4 resetters listed,
+              5 window filled (before B2); env wave 7: 15 window filled
+  control:    6 S(y) + rejection check + window base published, 7 transitions seen, 8 granule publish,
+              9 all-gather done, 10 cells drawn (before B2), 11 after B2, 12 next state done
+  store wave: 13 copy start (after B2), 14 copy issued
 Launch stamps per block: 0 entry, 1 P1 passed (control), 2 env wave 0's first window filled, 3 control step loop
 done, 4 kernel end, 5 / 6 table staging done (control wave / store wave 0), 7 env wave 0 has the first
 window's offset.
@@ -75,7 +74,7 @@ def at(k, i):  # stamp i of step k over blocks, ns from the first block's entry
 print("first steps (median/max over blocks, ns from launch):")
 for k in range(min(K, 3)):
     print(f"  k={k}: env start {at(k, 0)}  transitions done {at(k, 1)}  publish {at(k, 8)}  gather done {at(k, 9)}  "
-          f"offset {at(k, 10)}")
+          f"cells {at(k, 10)}")
 kl = min(K, 64) - 1
 print(f"last step k={kl}: env start {at(kl, 0)}  publish {at(kl, 8)}  gather done {at(kl, 9)}  next state {at(kl, 12)}")
 print(f"  tail: last next-state (max) -> kernel end (max) {ls[:, 4].max() - (a[:, kl, 12].max())} ns")
@@ -99,19 +98,19 @@ def rep(name, d):
 step = a[:, 3:kk, 0] - a[:, 2:kk - 1, 0]
 rep("step (env wave 0 start -> next start)", step)
 rep("env: transitions (0->1)", x[:, :, 1] - x[:, :, 0])
-rep("env: coarse states (1->3)", x[:, :, 3] - x[:, :, 1])
-rep("env: wait window free (3->4)", x[:, :, 4] - x[:, :, 3])
+rep("env: S(y) wait (1->2)", x[:, :, 2] - x[:, :, 1])
+rep("env: coarse states (2->3)", x[:, :, 3] - x[:, :, 2])
+rep("env: resetter listing (3->4)", x[:, :, 4] - x[:, :, 3])
 rep("env: window fill (4->5)", x[:, :, 5] - x[:, :, 4])
-rep("env: resetters taken (5->11)", x[:, :, 11] - x[:, :, 5])
-rep("env: next start after offset (ctrl 10 -> next 0)", a[:, 3:kk, 0] - a[:, 2:kk - 1, 10])
+rep("env: B2 wait (5 -> ctrl 11)", x[:, :, 11] - x[:, :, 5])
 rep("env wave 7 window done - wave 0 (15-5)", x[:, :, 15] - x[:, :, 5])
-rep("ctrl: resetters + window base (prev 12 -> 2)", a[:, 3:kk, 2] - a[:, 2:kk - 1, 12])
-rep("ctrl: rejection check (2->6)", x[:, :, 6] - x[:, :, 2])
+rep("ctrl: step-start work (prev 12 -> 6)", a[:, 3:kk, 6] - a[:, 2:kk - 1, 12])
+rep("ctrl: after B2 -> next state (11->12)", x[:, :, 12] - x[:, :, 11])
 rep("ctrl: trans wait (6->7)", x[:, :, 7] - x[:, :, 6])
 rep("ctrl: publish (7->8)", x[:, :, 8] - x[:, :, 7])
 rep("ctrl: gather (8->9)", x[:, :, 9] - x[:, :, 8])
-rep("ctrl: offset (9->10)", x[:, :, 10] - x[:, :, 9])
-rep("ctrl: next state (10->12)", x[:, :, 12] - x[:, :, 10])
+rep("ctrl: cells (9->10)", x[:, :, 10] - x[:, :, 9])
+rep("ctrl: B2 wait (10->11)", x[:, :, 11] - x[:, :, 10])
 pub = x[:, :, 8]
 print(f"  publish spread across blocks (max-min)       median {np.median(pub.max(0) - pub.min(0)):.0f} ns")
 print(f"  gather done - last publish                   median {np.median(x[:, :, 9] - pub.max(0)[None]):.0f} ns")
@@ -121,7 +120,7 @@ print("median over blocks and steps of stamp i - env start (ns):", np.median(x -
 # per-XCD phase (blocks beta with beta % 8 = x: round-robin dispatch puts them on XCD x), median over steps of the
 # block's stamp minus the step's earliest env start over all blocks
 st0 = x[:, :, 0].min(0)[None]
-print("per XCD (beta % 8), median ns after the step's earliest env start: env start / transitions done / publish / gather done / offset")
+print("per XCD (beta % 8), median ns after the step's earliest env start: env start / transitions done / publish / gather done / cells")
 for xcd in range(8):
     sel = np.arange(G) % 8 == xcd
     vals = [np.median(x[sel, :, i] - st0) for i in (0, 1, 8, 9, 10)]
