@@ -644,10 +644,126 @@ __device__ void np_reset_rows(const TaxiDev& p, const TaxiNpDev& q, const NpCats
   if (flags) atomicOr(p.derr, flags);
 }
 
+// _reset_passenger_and_destination's draws (extended_taxi.py:360-363) across the workgroup. numpy's integers(L, b)
+// is b buffered 32-bit Lemire draws (random_bounded_uint64_fill -> buffered_bounded_lemire_uint32), one next_uint32
+// each unless a word is rejected (leftover < (2^32 - L) % L: never for L a power of two, p ~ L / 2^32 otherwise).
+// So with no rejection half-word k of the stream (the buffered half first) is p of completion k for k < b1, d of
+// completion k - b1 for k < 2 b1, and every `while d == p` round gives its colliding completions, in env order, the
+// next half-words by rank. Each thread makes the half-words of a contiguous range of positions: one jump from the
+// step's state, then LCG steps. Returns false (nothing written to the stream state) when a word in these ranges is
+// rejected: the caller then walks the stream serially.
+__device__ bool np_pd_parallel(const TaxiDev& p, const TaxiNpDev& q, NpShared& sh, uint32_t b1) {
+  __shared__ uint32_t s_cnt[NP_WAVES];
+  __shared__ uint32_t s_flag;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const uint32_t L = (uint32_t)p.nlocs;
+  const uint32_t thr = (0xFFFFFFFFu - (L - 1u)) % L;
+  const u128 S = mk128(sh.S[0], sh.S[1]), inc = mk128(q.rng[2], q.rng[3]);
+  const uint32_t h0 = sh.has, u0 = sh.uval;
+  uint16_t* vh = reinterpret_cast<uint16_t*>(q.vtc);  // completion i: [2 i] = d, [2 i + 1] = p
+  if (t == 0) s_flag = 0;
+  __syncthreads();
+  // half-words [k0, k0 + n) of the stream -> f(k, value); rejections flagged
+  auto words = [&](uint32_t k0, uint32_t n, auto&& f) {
+    if (!n) return;
+    uint32_t k = k0, left = n;
+    if (h0 && k == 0) {  // the buffered half
+      f(k, u0);
+      ++k;
+      --left;
+    }
+    if (!left) return;
+    const uint32_t j = h0 ? k - 1u : k;  // position among the fresh halves
+    u128 st = pcg_jump(q.jt, S, j / 2u + 1u);
+    uint64_t x = pcg_output(st);
+    bool hi = (j & 1u) != 0;
+    for (; left; --left, ++k) {
+      f(k, hi ? (uint32_t)(x >> 32) : (uint32_t)x);
+      if (hi) {
+        st = pcg_step(st, inc);
+        x = pcg_output(st);
+      }
+      hi = !hi;
+    }
+  };
+  auto lemire = [&](uint32_t word, bool& rej) {
+    const uint64_t m = (uint64_t)word * L;
+    rej |= (uint32_t)m < thr;
+    return (uint32_t)(m >> 32);
+  };
+  bool rej = false;
+  {  // p of every completion, then d: half-words 0 .. 2 b1 - 1
+    const uint32_t n = 2u * b1, per = (n + NP_TPB - 1u) / NP_TPB;
+    const uint32_t k0 = min((uint32_t)t * per, n), k1 = min(k0 + per, n);
+    words(k0, k1 - k0, [&](uint32_t k, uint32_t v) {
+      const uint32_t x = lemire(v, rej);
+      if (k < b1) vh[2 * k + 1] = (uint16_t)x;
+      else vh[2 * (k - b1)] = (uint16_t)x;
+    });
+  }
+  uint32_t pos = 2u * b1;
+  const uint32_t per = (b1 + NP_TPB - 1u) / NP_TPB;  // completions per thread (env order)
+  const uint32_t i0 = min((uint32_t)t * per, b1), i1 = min(i0 + per, b1);
+  for (int round = 0; round < 4096; ++round) {
+    if (rej) s_flag = 1;  // (benign race: every writer stores 1)
+    __threadfence_block();
+    __syncthreads();
+    if (s_flag) return false;
+    // this round's colliding completions (p == d), ranked in env order
+    uint32_t c = 0;
+    for (uint32_t i = i0; i < i1; ++i) c += vh[2 * i] == vh[2 * i + 1] ? 1u : 0u;
+    uint32_t v = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(v, d, 64);
+      if (lane >= d) v += y;
+    }
+    if (lane == 63) s_cnt[w] = v;
+    __syncthreads();
+    uint32_t base = 0, m = 0;
+    for (int x = 0; x < NP_WAVES; ++x) {
+      base += x < w ? s_cnt[x] : 0u;
+      m += s_cnt[x];
+    }
+    base += v - c;
+    __syncthreads();  // (s_cnt reused next round)
+    if (m == 0) break;
+    if (c) {  // my colliders take half-words pos + base .. pos + base + c - 1, in order
+      uint32_t i = i0;
+      words(pos + base, c, [&](uint32_t, uint32_t val) {
+        while (vh[2 * i] != vh[2 * i + 1]) ++i;  // the next collider (its d is rewritten below)
+        vh[2 * i] = (uint16_t)lemire(val, rej);
+        ++i;
+      });
+    }
+    pos += m;
+  }
+  __threadfence_block();
+  __syncthreads();
+  if (t == 0) {  // the stream after `pos` half-words
+    uint32_t used, h;
+    if (h0) {
+      used = pos >> 1;
+      h = (pos - 1u) & 1u;
+    } else {
+      used = (pos + 1u) >> 1;
+      h = pos & 1u;
+    }
+    const u128 S2 = used ? pcg_jump(q.jt, S, used) : S;
+    sh.S[0] = hi64(S2);
+    sh.S[1] = lo64(S2);
+    sh.has = h;
+    if (used) sh.uval = (uint32_t)(pcg_output(S2) >> 32);  // numpy keeps the last drawn high half (buffered or not)
+  }
+  __syncthreads();
+  return true;
+}
+
 // The draws of one step (or of reset(): b1 = 0, every env a reset), between the two env passes.
-__device__ void np_draws(const TaxiDev& p, const TaxiNpDev& q, const NpCats& c, NpShared& sh) {
+__device__ void np_draws(const TaxiDev& p, const TaxiNpDev& q, const NpCats& c, NpShared& sh, bool rows = true) {
   const uint32_t b1 = sh.b1, b2 = sh.b2;
-  if (threadIdx.x == 0) {
+  const bool done_pd = b1 && np_pd_parallel(p, q, sh, b1);
+  if (threadIdx.x == 0 && !done_pd) {
     NpRng g{mk128(sh.S[0], sh.S[1]), mk128(q.rng[2], q.rng[3]), sh.has, sh.uval};
     if (b1) {  // extended_taxi.py:360-363
       const uint32_t L = (uint32_t)p.nlocs;
@@ -671,7 +787,7 @@ __device__ void np_draws(const TaxiDev& p, const TaxiNpDev& q, const NpCats& c, 
     sh.uval = g.uval;
   }
   __syncthreads();
-  if (b2) np_reset_rows(p, q, c, sh, b2);
+  if (b2 && rows) np_reset_rows(p, q, c, sh, b2);
 }
 
 // The numpy-mode rollout / reset: one workgroup, K steps (K = 0: reset(), every env draws a start state).
@@ -806,6 +922,12 @@ struct NpgDev {
   uint32_t* bcnt;   // [ntiles] tile counts: tc | rs << 16
   uint64_t* bpre;   // [ntiles] tile prefixes: tc | rs << 32
   int32_t grid;     // metric slots (p.mslot)
+  // the multinomial rows, grid-wide (taxi_npg_rows)
+  uint32_t* rres;   // [RW_R * RW_W] row results: arg << 16 | doubles used (0xFFFF: not evaluated)
+  uint32_t* rctl;   // [16] 0: barrier arrivals (monotone), 1: b2 (rows of this step), 2: rows done (r0), 3: the mean
+                    //      deficit per row x 256 (window centre), 5: the arrival count a launch starts from
+  uint64_t* rst;    // [2] the stream state at the round's first row (hi, lo)
+  int32_t rgrid;    // blocks of taxi_npg_rows (all resident: one per CU)
 };
 
 // Exclusive block scan of a u64 per thread (256 threads); the block total in tot.
@@ -939,7 +1061,154 @@ __global__ __launch_bounds__(TPB) void taxi_npg_pass1(TaxiDev p, TaxiNpDev q, Np
   if (!RESET) npg_metrics(p, g.grid, rsum, eps, lens, nst);
 }
 
-// The draws of one step (one workgroup of NP_TPB threads): tile prefixes, b1 / b2, then np_draws.
+// ---- the multinomial rows of a step (or of reset()) grid-wide: taxi_npg_rows ----
+// A row's start in the stream is the sum of the doubles the rows before it used: C0 each unless a row stops early
+// (the last categories empty) or an inversion restarts, so the deficit D_i = C0 i - (start of row i) drifts by a
+// few tenths per row. Each round evaluates rows r0 .. r0 + RW_R - 1 at RW_W candidate starts each, centred on
+// the drift predicted from earlier rounds (lane (i, j): start C0 i - (base_i + j), base_i = m i - RW_W / 2), one
+// row per thread over the whole grid; then block 0 chains them in order from the exact D_0 = 0 (row i's result
+// at its true D_i is looked up, D_{i+1} = D_i + C0 - used) until a true start falls outside its candidates or the
+// rows run out, and the next round starts at the first unchained row (row r0 is always chained: base_0 <= 0). A
+// grid barrier (one counter, bounded spins) separates the evaluation from the chain and the chain from the next
+// round's evaluation.
+constexpr int RW_W = 64;        // candidate starts per row
+constexpr int RW_R = 1024;      // rows per round (RW_R * RW_W threads: one row each)
+constexpr int RW_TPB = 256;
+constexpr int RW_CHUNK = 128;   // rows block 0 stages in LDS at a time while chaining
+constexpr uint32_t RW_SPIN = 1u << 24;
+
+__device__ __forceinline__ void npg_grid_barrier(const TaxiDev& p, uint32_t* ctr, uint32_t target) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();  // this block's results / publications before its arrival
+    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t n = 0;
+    while ((int32_t)(__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++n > RW_SPIN) {
+        atomicOr(p.derr, GP_DERR_TIMEOUT);
+        break;
+      }
+    }
+    __threadfence();  // acquire: the others' writes
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ int32_t rw_base(uint32_t mdef, uint32_t i) {
+  return (int32_t)(((uint64_t)mdef * i) >> 8) - RW_W / 2;
+}
+
+// Persistent: every block stages the category tables, then rounds of evaluation + chain until the step's b2 rows
+// are placed (q.vrs[r] = start state of reset rank r); block 0 leaves the stream state after the last row in q.rng.
+__global__ __launch_bounds__(RW_TPB) void taxi_npg_rows(TaxiDev p, TaxiNpDev q, NpgDev g) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  __shared__ uint64_t etab[256];
+  __shared__ uint32_t s_r0, s_n, s_mdef;
+  __shared__ int32_t s_D;
+  __shared__ uint64_t s_S[2];
+  const int t = threadIdx.x;
+  {
+    const uint4* s2 = (const uint4*)q.mtab;
+    uint4* d2 = (uint4*)lds;
+    for (int i = t; i < q.mtab_bytes / 16; i += RW_TPB) d2[i] = s2[i];
+    for (int i = t; i < 256; i += RW_TPB) etab[i] = gp_libm::kExpTab[i];
+  }
+  uint32_t* res_lds = reinterpret_cast<uint32_t*>(lds + ((q.mtab_bytes + 15) & ~15));  // block 0: RW_CHUNK x RW_W
+  const NpCats c{(const double*)(lds + q.off_pp), (const double*)(lds + q.off_q), (const double*)(lds + q.off_lq),
+                 (const uint16_t*)(lds + q.off_cat), lds + q.off_flip, etab};
+  const u128 inc = mk128(q.rng[2], q.rng[3]);
+  const uint32_t G = gridDim.x;
+  const uint32_t b2 = __hip_atomic_load(&g.rctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint32_t r0 = 0, mdef = __hip_atomic_load(&g.rctl[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  u128 S = mk128(__hip_atomic_load(&q.rng[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                 __hip_atomic_load(&q.rng[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  // the barrier counter only grows: this launch's arrivals count from where the last launch left it
+  const uint32_t bar0 = __hip_atomic_load(&g.rctl[5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint32_t flags = 0, bar = 0;
+  __syncthreads();
+  while (r0 < b2) {
+    // evaluation: thread (block, t) -> lane L -> row i = L / RW_W, candidate j = L % RW_W
+    for (uint32_t L = blockIdx.x * RW_TPB + t; L < (uint32_t)(RW_R * RW_W); L += G * RW_TPB) {
+      const uint32_t i = L / RW_W, j = L % RW_W;
+      uint32_t v = 0xFFFFu;
+      if (r0 + i < b2) {
+        const int64_t off = (int64_t)q.C0 * i - (int64_t)(rw_base(mdef, i) + (int32_t)j);
+        if (off >= 0) {
+          uint32_t used = 0;
+          const uint32_t a = np_row(q, c, off ? pcg_jump(q.jt, S, (uint32_t)off) : S, inc, used, flags);
+          v = (a << 16) | min(used, 0xFFFEu);
+        }
+      }
+      g.rres[L] = v;
+    }
+    npg_grid_barrier(p, &g.rctl[0], bar0 + G * ++bar);
+    if (blockIdx.x == 0) {  // the chain, RW_CHUNK rows at a time from LDS
+      int32_t D = 0;
+      uint32_t n = 0;
+      bool go = true;
+      while (go && n < (uint32_t)RW_R && r0 + n < b2) {
+        const uint32_t rows = min(min((uint32_t)RW_CHUNK, (uint32_t)RW_R - n), b2 - r0 - n);
+        for (uint32_t x = t; x < rows * RW_W; x += RW_TPB) res_lds[x] = g.rres[n * RW_W + x];
+        __syncthreads();
+        if (t == 0) {
+          uint32_t k = 0;
+          for (; k < rows; ++k) {
+            const int32_t jj = D - rw_base(mdef, n + k);
+            if (jj < 0 || jj >= RW_W) break;
+            const uint32_t v = res_lds[k * RW_W + (uint32_t)jj];
+            if ((v & 0xFFFFu) == 0xFFFFu) break;  // (not evaluated: cannot happen for a chained start)
+            q.vrs[r0 + n + k] = (uint16_t)(v >> 16);
+            D += q.C0 - (int32_t)(v & 0xFFFFu);
+          }
+          s_n = k;
+          s_D = D;
+        }
+        __syncthreads();
+        const uint32_t k = s_n;
+        D = s_D;
+        n += k;
+        go = k == rows;
+        __syncthreads();
+      }
+      if (t == 0) {
+        const u128 S2 = pcg_jump(q.jt, S, (uint32_t)((int64_t)q.C0 * n - D));
+        // the drift estimate for the next round: this round's mean deficit per row (x 256), kept when n is small
+        uint32_t m2 = mdef;
+        if (n >= 32) m2 = (uint32_t)max((int64_t)0, ((int64_t)D << 8) / (int64_t)n);
+        g.rst[0] = hi64(S2);
+        g.rst[1] = lo64(S2);
+        g.rctl[2] = r0 + n;
+        g.rctl[3] = m2;
+      }
+    }
+    npg_grid_barrier(p, &g.rctl[0], bar0 + G * ++bar);
+    if (t == 0) {
+      s_r0 = __hip_atomic_load(&g.rctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_mdef = __hip_atomic_load(&g.rctl[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_S[0] = __hip_atomic_load(&g.rst[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_S[1] = __hip_atomic_load(&g.rst[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (s_r0 <= r0) {  // no progress: a logic error (row r0 is always chained); flag and stop
+      if (t == 0 && blockIdx.x == 0) atomicOr(p.derr, GP_DERR_TIMEOUT);
+      break;
+    }
+    r0 = s_r0;
+    mdef = s_mdef;
+    S = mk128(s_S[0], s_S[1]);
+    __syncthreads();
+  }
+  if (flags) atomicOr(p.derr, flags);
+  if (blockIdx.x == 0 && t == 0) {  // the stream after the rows (the 32-bit buffer is untouched: doubles only)
+    q.rng[0] = hi64(S);
+    q.rng[1] = lo64(S);
+    g.rctl[5] = bar0 + G * bar;  // every block made the same `bar` arrivals: the next launch counts from here
+  }
+}
+
+// The draws of one step (one workgroup of NP_TPB threads): tile prefixes, b1 / b2, then the p / d draws; the step's
+// b2 for taxi_npg_rows.
 __global__ __launch_bounds__(NP_TPB) void taxi_npg_draws(TaxiDev p, TaxiNpDev q, NpgDev g, int ntiles) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   __shared__ NpShared sh;
@@ -997,13 +1266,14 @@ __global__ __launch_bounds__(NP_TPB) void taxi_npg_draws(TaxiDev p, TaxiNpDev q,
   __syncthreads();
   const NpCats c{(const double*)(lds + q.off_pp), (const double*)(lds + q.off_q), (const double*)(lds + q.off_lq),
                  (const uint16_t*)(lds + q.off_cat), lds + q.off_flip, etab};
-  np_draws(p, q, c, sh);
+  np_draws(p, q, c, sh, false);  // the p / d draws; the rows are taxi_npg_rows's (after this launch)
   __syncthreads();
   if (t == 0) {
     q.rng[0] = sh.S[0];
     q.rng[1] = sh.S[1];
     q.rng[4] = sh.has;
     q.rng[5] = sh.uval;
+    g.rctl[1] = sh.b2;
   }
 }
 
@@ -1118,7 +1388,8 @@ struct TaxiBackend : EnvBackend {
   }
   // grid-wide numpy mode (B > npg_min): per step pass 1, the draws, pass 2 (K = 0: reset())
   NpgDev npg{};
-  DevBuf b_bcnt, b_bpre;
+  DevBuf b_bcnt, b_bpre, b_rres, b_rctl, b_rst;
+  size_t rows_lds() const { return (size_t)((np.mtab_bytes + 15) & ~15) + (size_t)RW_CHUNK * RW_W * 4; }
   int npg_min = NPG_MIN_ENVS;
   template <int OH>
   void launch_npg_pass2(size_t off, void* obs, hipStream_t s) {
@@ -1136,6 +1407,7 @@ struct TaxiBackend : EnvBackend {
         hipLaunchKernelGGL((taxi_npg_pass1<false>), dim3((unsigned)d.ntiles), dim3(TPB), (size_t)d.tab_bytes, s, d, np,
                            npg, off, (const int32_t*)act, rew, term, trunc);
       hipLaunchKernelGGL(taxi_npg_draws, dim3(1), dim3(NP_TPB), (size_t)np.mtab_bytes, s, d, np, npg, d.ntiles);
+      hipLaunchKernelGGL(taxi_npg_rows, dim3((unsigned)npg.rgrid), dim3(RW_TPB), rows_lds(), s, d, np, npg);
       switch (cs) {
         case 0: launch_npg_pass2<0>(off, obs, s); break;
         case 16: launch_npg_pass2<16>(off, obs, s); break;
@@ -1550,6 +1822,27 @@ int TaxiBackend::np_build(const std::vector<uint16_t>& valid) {
   npg.bcnt = b_bcnt.as<uint32_t>();
   npg.bpre = b_bpre.as<uint64_t>();
   npg.grid = grid;
+  // the grid-wide rows: one block per CU, all resident (its barrier waits on every block)
+  if ((e = b_rres.alloc(sizeof(uint32_t) * RW_R * RW_W)) || (e = b_rctl.alloc(sizeof(uint32_t) * 16)) ||
+      (e = b_rst.alloc(sizeof(uint64_t) * 2)))
+    return e;
+  npg.rres = b_rres.as<uint32_t>();
+  npg.rctl = b_rctl.as<uint32_t>();
+  npg.rst = b_rst.as<uint64_t>();
+  {
+    const uint32_t m0 = 64;  // the drift's first estimate: 0.25 doubles per row (x 256); each round re-measures it
+    GP_HIP_CHECK(hipMemcpy(npg.rctl + 3, &m0, sizeof(m0), hipMemcpyHostToDevice));
+    int cus = 0, occ = 0;
+    GP_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+    GP_HIP_CHECK(hipFuncSetAttribute((const void*)taxi_npg_rows, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)rows_lds()));
+    GP_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, taxi_npg_rows, RW_TPB, rows_lds()));
+    if (occ < 1) {
+      gp_set_error("taxi: the grid-wide row kernel does not fit a CU (%zu B of LDS)", rows_lds());
+      return GP_E_UNSUPPORTED;
+    }
+    npg.rgrid = cus;
+  }
   return np_upload_rng();
 }
 

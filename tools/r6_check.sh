@@ -47,6 +47,10 @@ for task in "${@:-tests ab bench floor}"; do
     floorprof)  # the launch-footprint probe under rocprofv3 (dispatch-timestamp durations of the same launches)
       run 300 $O/floorprof.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/floorprof -o p -- python3 -u tools/launch_floor.py 60
       for f in $(find $O/floorprof -name "*kernel_stats.csv"); do cp $f $O/floor_kernel_stats.csv; cat $f; done ;;
+    taxiprof)  # per-kernel time of seed-identical Taxi at 65,536 and 4M envs (rocprofv3 kernel trace)
+      run 400 $O/taxiprof.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/taxiprof -o p -- python3 -u tools/taxi_numpy_rate.py ${TAXI_B:-65536 4194304}
+      grep numpy $O/taxiprof.log
+      for f in $(find $O/taxiprof -name "*kernel_stats.csv"); do cp $f $O/taxi_kernel_stats.csv; head -12 $f | cut -c1-220; done ;;
     counters)  # the PMC counters this GPU offers
       run 120 $O/counters.log rocprofv3 -L
       grep -i -E "icache|ifetch|SQC_" $O/counters.log | head -60 ;;

@@ -22,7 +22,11 @@ def rate(mode, B, K=None, reps=3):
     knobs = {"taxi_npg_min": int(os.environ["NPG_MIN"])} if os.environ.get("NPG_MIN") else {}
     with debug_knobs(**knobs):
         env = HansenTaxiVecEnv(B, rng_mode=mode, one_hot=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
     env.reset(seed=0)
+    torch.cuda.synchronize()
+    reset_s = time.perf_counter() - t0  # every env draws a start state: B multinomial rows (numpy mode)
     a = torch.randint(0, 5, (K, B), device=env.device, dtype=torch.int32)
     env.rollout(a)
     torch.cuda.synchronize()
@@ -33,7 +37,7 @@ def rate(mode, B, K=None, reps=3):
     dt = time.perf_counter() - t0
     m = env.metrics()
     return {"mode": mode, "num_envs": B, "steps": K * reps, "us_per_step": dt / (K * reps) * 1e6,
-            "env_steps_per_s": B * K * reps / dt, "episodes_so_far": m["episodes"],
+            "env_steps_per_s": B * K * reps / dt, "episodes_so_far": m["episodes"], "reset_s": reset_s,
             "path": ("grid-wide" if B > knobs.get("taxi_npg_min", 4096) else "one workgroup") if mode == "numpy" else "-"}
 
 
