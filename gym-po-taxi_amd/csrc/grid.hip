@@ -2713,6 +2713,7 @@ struct GridBackend : EnvBackend {
   // windowed numpy rollout (wgrid.hip): G blocks of E = 512 * NS envs; 0 = not eligible
   int wg_G = 0, wg_E = 0, wg_NS = 0, wg_H = 0;
   int wg_kmax = WG_KMAX;  // launches of more steps go to the fused kernel when it can take them (gp_debug_set wg_kmax)
+  int wg_kmax_default = WG_KMAX;  // the size-based choice before any autotune (the autotune's margin favours it)
   size_t wg_lds = 0;
   int at_launches = 0, at_steps = 0;  // the last gp_autotune's scratch launches (both kernels) and their length
   float at_ms[2] = {0.f, 0.f};        // its mean ms per launch: windowed, fused
@@ -3318,10 +3319,10 @@ int GridBackend::autotune(int K, int reps, int* chosen) {
   (void)hipEventDestroy(e1);
   timer.on = timer_on;
   if (e) return e;
-  // A margin: the kernel the launch length picks by default (WG_KMAX) is kept unless the other one is at least
+  // A margin: the kernel the launch length picks by default (wg_kmax_default) is kept unless the other one is at least
   // AT_MARGIN faster (one of five driver-command runs picked the kernel that was slower there with no margin).
   constexpr float AT_MARGIN = 0.02f;
-  const bool def_wgrid = K <= WG_KMAX;
+  const bool def_wgrid = K <= wg_kmax_default;
   const bool wgrid_faster = def_wgrid ? !(ms[1] < (1.f - AT_MARGIN) * ms[0]) : ms[0] < (1.f - AT_MARGIN) * ms[1];
   if (wgrid_faster) wg_kmax = std::max(wg_kmax, K);
   else wg_kmax = std::min(wg_kmax, K - 1);
@@ -3718,7 +3719,12 @@ int GridBackend::build(const gp_grid_config* cfg) {
     for (int c = 0; c < nc; ++c)
       ocell[c] = cfg->obs_kind == GP_OBS_HANSEN ? ofix[c] : t1[c] + (t2.empty() ? 0 : t2[d.fixed_goal]);
     if (int e2 = build_wgrid(move, thr, ocell)) return e2;
+    // Blocks of <= 1,024 envs (<= 2^18 envs, e.g. the strong-scaling shards): the windowed kernel at every launch
+    // length (round 6, tools/r6_check.sh strong: 3.02 vs 3.69 us/step at 2^17 envs and 3.32 vs 3.60 at 2^18 in
+    // 128-step launches, 67 vs 82 us per 20-step launch at 2^17).
+    if (dbg.wg_kmax < 0 && wg_G && wg_NS <= 2) wg_kmax = 1 << 30;
   }
+  wg_kmax_default = wg_kmax;
   nslots = std::max({d.nblk, grid_persist, fused_G, wg_G});
   if ((e = b_jt.alloc(sizeof(PcgJump) * JT_LEVELS * JT_RADIX)) || (e = b_lt4.alloc(sizeof(PcgJump) * TPB)) ||
       (e = b_lt2.alloc(sizeof(PcgJump) * TPB)) || (e = b_tja.alloc(sizeof(PcgJump) * (size_t)d.nblk)) ||

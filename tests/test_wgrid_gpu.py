@@ -84,7 +84,7 @@ def test_fused_tag_wrap_between_windowed_launches_bit_exact(fstep, gpu_device):
     advanced only by fused launches, its slots start at a tag it never expects, and windowed launches interleave:
     the results must stay the oracle's through the wrap (zeroed slots matched tag 0)."""
     from gym_po_amd._lib import debug_knobs
-    B = 1 << 18
+    B = 1 << 19  # (2048-env blocks: launches of > 24 steps default to the fused kernel)
     with debug_knobs(fused_step=fstep):
         env = _fourrooms(B, gpu_device)
         ora = gridworld.FourRoomsOracle(B, 1, obs_type="hansen")
@@ -94,6 +94,15 @@ def test_fused_tag_wrap_between_windowed_launches_bit_exact(fstep, gpu_device):
     # windowed (3), fused across the wrap (40), windowed (2), fused (33)
     _check_chunks(env, ora, (3, 40, 2, 33), action_seed=12, n_act=4)
     assert env.metrics()["env_steps"] == B * 78
+
+
+def test_small_blocks_default_to_windowed_at_every_length(gpu_device):
+    """Blocks of <= 1,024 envs (2^17 / 2^18 envs: the strong-scaling shards) run the windowed kernel for every launch
+    length by default; 2048-env blocks hand launches of more than 24 steps to the fused kernel."""
+    for B, kmax in ((1 << 17, 1 << 30), (1 << 18, 1 << 30), (1 << 19, 24), (1 << 20, 24)):
+        env = _fourrooms(B, gpu_device)
+        assert env.query("wgrid_kmax") == kmax, B
+        env.close()
 
 
 @pytest.mark.parametrize("B,E", [(1 << 17, 512), (1 << 18, 1024), (1 << 19, 2048), (3 << 17, 2048), (8192, 512)])

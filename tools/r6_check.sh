@@ -51,6 +51,13 @@ for task in "${@:-tests ab bench floor}"; do
       run 400 $O/taxiprof.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/taxiprof -o p -- python3 -u tools/taxi_numpy_rate.py ${TAXI_B:-65536 4194304}
       grep numpy $O/taxiprof.log
       for f in $(find $O/taxiprof -name "*kernel_stats.csv"); do cp $f $O/taxi_kernel_stats.csv; head -12 $f | cut -c1-220; done ;;
+    strong)  # strong-scaling shard sizes: the fused kernel (wg_kmax 0) vs the windowed kernel (wg_kmax 1000)
+      for B in ${STRONG_B:-131072 262144}; do
+        for kn in 0 1000; do
+          GP_KNOBS=wg_kmax=$kn run 150 $O/strong_${B}_$kn.log python -u tools/latency_probe.py $B 20 128
+          echo "== B $B wg_kmax $kn"; grep "B=" $O/strong_${B}_$kn.log
+        done
+      done ;;
     counters)  # the PMC counters this GPU offers
       run 120 $O/counters.log rocprofv3 -L
       grep -i -E "icache|ifetch|SQC_" $O/counters.log | head -60 ;;
