@@ -223,6 +223,7 @@ int gp_debug_set(const char* key, int64_t value) {
   else if (!strcmp(key, "taxi_npg_min")) g_dbg.taxi_npg_min = (int)value;
   else if (!strcmp(key, "xg_min_envs")) g_dbg.xg_min_envs = (int)value;
   else if (!strcmp(key, "fused_step")) g_dbg.fused_step = value;
+  else if (!strcmp(key, "wg_block_envs")) g_dbg.wg_block_envs = (int)value;
   else {
     gp_set_error("gp_debug_set: unknown key '%s'", key);
     return GP_E_INVALID;

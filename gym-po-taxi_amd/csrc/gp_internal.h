@@ -38,6 +38,7 @@ struct GpDebugKnobs {
   int xg_min_envs = -1;      // CROOMS exact mode: largest B on the one-workgroup kernel (-1 = crooms.hip XG_MIN_ENVS)
   int taxi_npg_min = -1;    // TAXI numpy mode: largest B on the one-workgroup kernel (-1 = taxi.hip NPG_MIN_ENVS)
   int64_t fused_step = -1;  // GRID: the fused kernel's tag counter (GridCtl::step) set at every seed (-1 = kept)
+  int wg_block_envs = 0;    // GRID windowed kernel: the smallest envs per block to use (0 = the smallest that fits)
 };
 const GpDebugKnobs& gp_debug_knobs();
 

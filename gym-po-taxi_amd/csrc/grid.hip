@@ -2978,7 +2978,7 @@ int GridBackend::build_wgrid(const std::vector<uint16_t>& move, const std::vecto
   const int cus = std::min(prop.multiProcessorCount, 256);
   int E = 0;
   for (int e = 512; e <= 4096; e *= 2)
-    if (B % e == 0 && B / e <= cus) {
+    if (B % e == 0 && B / e <= cus && (dbg.wg_block_envs <= 0 || e >= dbg.wg_block_envs)) {
       E = e;
       break;
     }

@@ -58,6 +58,11 @@ for task in "${@:-tests ab bench floor}"; do
           echo "== B $B wg_kmax $kn"; grep "B=" $O/strong_${B}_$kn.log
         done
       done ;;
+    blocks)  # windowed kernel block size at a shard size (wg_block_envs knob): envs per block E -> G = B / E blocks
+      for E in ${BLK_E:-512 1024 2048}; do
+        GP_KNOBS=wg_kmax=1000,wg_block_envs=$E run 150 $O/blk_$E.log python -u tools/latency_probe.py ${BLK_B:-131072} 20 128
+        echo "== E $E"; grep "B=" $O/blk_$E.log
+      done ;;
     counters)  # the PMC counters this GPU offers
       run 120 $O/counters.log rocprofv3 -L
       grep -i -E "icache|ifetch|SQC_" $O/counters.log | head -60 ;;
