@@ -357,12 +357,16 @@ def main():
     from gym_po_amd import shard
     B = shard.shard_size(args.envs, world, rank, args.strong)
     C = max(1, min(args.chunk, args.steps))
-    if args.kernel == "auto":
+    from gym_po_amd._lib import debug_knobs
+    # GP_KNOBS="key=value,...": diagnostic library knobs for in-call A/Bs (never set by the driver's command)
+    knobs = dict((kv.split("=")[0], int(kv.split("=")[1])) for kv in os.environ.get("GP_KNOBS", "").split(",") if kv)
+    if args.kernel != "auto":  # numpy-mode FourRooms kernel forced for every launch length (PMC records per kernel)
+        knobs["wg_kmax"] = 1 << 20 if args.kernel == "windowed" else 0
+    with debug_knobs(**knobs):
         env = W["make"](B, dev, args.mode)
-    else:  # numpy-mode FourRooms kernel forced for every launch length (PMC records per kernel; A/Bs)
-        from gym_po_amd._lib import debug_knobs
-        with debug_knobs(wg_kmax=1 << 20 if args.kernel == "windowed" else 0):
-            env = W["make"](B, dev, args.mode)
+    persist = None
+    if args.workload != "fourrooms":  # the streaming rollouts' persistent grid (persistent_grid, csrc/gp_internal.h)
+        persist = {"blocks": env.query("persist_blocks"), "resident_per_cu": env.query("persist_occupancy")}
     shard.seed_shard(env, 0, rank, world)  # shard g: SeedSequence(0, spawn_key=(g,))
     env.reset()
     # numpy-mode FourRooms: the faster of the two bit-identical kernels for C-step launches on this board, timed
@@ -522,7 +526,8 @@ def main():
                    "parallelism": f"independent env shards x{world}", "steps_per_launch_call": C,
                    "kernel_autotune": {1: "windowed", 0: "fused", -1: None}[tuned] if args.kernel == "auto" else
                    f"forced: {args.kernel}",
-                   "pretimed": pretimed},
+                   "pretimed": pretimed, **({"knobs": knobs} if knobs else {}),
+                   **({"persistent_grid": persist} if persist else {})},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "byte_model": (f"SURVEY 8(d): {W['bytes']} B per env-step + {W['state']} B per env per launch "

@@ -177,7 +177,10 @@ __device__ __forceinline__ bool quad_ok(const void* base, int env0, int B, int e
 }
 
 template <bool REPLAY>
-__global__ __launch_bounds__(TPB) void anttag_rollout(AtDev p, int K, uint64_t step0, const int32_t* __restrict__ act,
+#ifndef GP_AT_WAVES
+#define GP_AT_WAVES 1  // launch bound: minimum waves per SIMD (register budget of the rollout)
+#endif
+__global__ __launch_bounds__(TPB, GP_AT_WAVES) void anttag_rollout(AtDev p, int K, uint64_t step0, const int32_t* __restrict__ act,
                                                       int4* __restrict__ obs, float* __restrict__ rew,
                                                       uint8_t* __restrict__ term, uint8_t* __restrict__ trunc) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -476,8 +479,9 @@ int AntTagBackend::build(const gp_anttag_config* cfg) {
   GP_HIP_CHECK(hipGetDeviceProperties(&prop, device));
   int occ = 0;
   GP_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, anttag_rollout<false>, TPB, d.tab_bytes));
-  occ = std::max(1, std::min(occ, 8));
-  grid = std::max(1, std::min(d.ntiles, prop.multiProcessorCount * occ));
+  grid = persistent_grid(d.ntiles, prop.multiProcessorCount, occ);
+  persist_grid = grid;
+  persist_occ = occ;
   if ((e = b_slot.alloc(sizeof(AtSlot) * grid))) return e;
   d.mslot = b_slot.as<AtSlot>();
   if ((e = derr.alloc())) return e;

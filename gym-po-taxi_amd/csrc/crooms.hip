@@ -53,7 +53,7 @@ constexpr uint32_t TAG_DRAW = 0x6d733121u;
 #endif
 // Minimum waves per SIMD of the rollout kernel (caps its VGPRs at 512 / waves; tuning knob).
 #ifndef GP_CR_WAVES
-#define GP_CR_WAVES 2
+#define GP_CR_WAVES 6
 #endif
 constexpr double MAX_VELOCITY = 5.0;
 // Largest batch of the exact (numpy-stream) mode, which runs in one workgroup.
@@ -2443,7 +2443,8 @@ struct CRoomsBackend : EnvBackend {
       const int64_t nx = n_host + B / 2;
       npos = std::min<int64_t>(npos, nx + nx / 16 + 4096);
     }
-    const int ppt = xg_fused() && (npos + XGT - 1) / XGT > XG_PPT_MIN_BLOCKS ? 4 : 1;  // positions per thread
+    const int pmin = gp_debug_knobs().xg_ppt_min >= 0 ? gp_debug_knobs().xg_ppt_min : XG_PPT_MIN_BLOCKS;
+    const int ppt = xg_fused() && (npos + XGT - 1) / XGT > pmin ? 4 : 1;  // positions per thread
     const unsigned nbp = (unsigned)((npos + XGT * ppt - 1) / (XGT * ppt));
     if (ext == 2 && a.xinfo) {
       hipLaunchKernelGGL(xg_wall_one, dim3(1), dim3(XT), 0, s, a, xd);
@@ -2943,8 +2944,9 @@ int CRoomsBackend::build(const gp_crooms_config* cfg) {
   GP_HIP_CHECK(hipGetDeviceProperties(&prop, device));
   int occ = 0;
   GP_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, crooms_rollout<GP_OBS_F32, false>, TPB, d.tab_bytes));
-  occ = std::max(1, std::min(occ, 8));
-  grid = std::max(1, std::min(d.ntiles, prop.multiProcessorCount * occ));
+  grid = persistent_grid(d.ntiles, prop.multiProcessorCount, occ);
+  persist_grid = grid;
+  persist_occ = occ;
   if ((e = b_slot.alloc(sizeof(CrSlot) * grid))) return e;
   d.mslot = b_slot.as<CrSlot>();
   d.nslot = grid;
@@ -3037,6 +3039,7 @@ int CRoomsBackend::xg_rollout(int K, const void* act, void* obs, float* rew, uin
   const size_t osz = (size_t)d.obs_width * (d.obs_kind == GP_OBS_F32 ? (d.obs_f64 ? 8 : 4)
                                             : (d.obs_kind == GP_OBS_HANSEN || d.obs_kind == GP_OBS_TABLE ? 4 : 1));
   const XgFlags fd = xg_flags(1), fs = xg_flags(2);  // wall hits of the dry step, resets of the step
+  const int spb_min = gp_debug_knobs().xg_spb_min >= 0 ? gp_debug_knobs().xg_spb_min : XG_SPB_MIN_BLOCKS;
   int e;
   for (int k = 0; k < K; ++k) {
     const size_t off = (size_t)k * B;
@@ -3054,7 +3057,7 @@ int CRoomsBackend::xg_rollout(int K, const void* act, void* obs, float* rew, uin
       constexpr int OK = decltype(okc)::value;
       const XgFlags fr = k ? fs : XgFlags{};
       void* op = k ? (void*)(ob - B * osz) : nullptr;
-      if (nbe > XG_SPB_MIN_BLOCKS)
+      if ((int)nbe > spb_min)
         hipLaunchKernelGGL((xg_dry<OK, 4>), dim3((nbe + 3) / 4), dim3(XGT), d.tab_bytes, s, dd, fd, act, off, fr,
                            (const int32_t*)xd.gi, (const int32_t*)xd.ai, op, (int)nbe);
       else
@@ -3066,7 +3069,7 @@ int CRoomsBackend::xg_rollout(int K, const void* act, void* obs, float* rew, uin
     // the step itself with the wall noise in place, resets deferred; then the resetting envs' goals / agents
     e = dispatch_obs(d.obs_kind, [&](auto okc) -> int {
       constexpr int OK = decltype(okc)::value;
-      if (nbe > XG_SPB_MIN_BLOCKS)
+      if ((int)nbe > spb_min)
         hipLaunchKernelGGL((xg_step<OK, 4>), dim3((nbe + 3) / 4), dim3(XGT), d.tab_bytes, s, dd, fd, fs, act, off,
                            (void*)ob, rew, term, trunc, (int)nbe);
       else

@@ -36,11 +36,28 @@ struct GpDebugKnobs {
   int wg_tmode = 0;         // GRID windowed kernel: timing-study variants (wgrid.hip TM_*); some give wrong results
   int wg_kmax = -1;         // GRID: longest launch (steps) on the windowed kernel; longer ones on the fused kernel (-1 default)
   int xg_min_envs = -1;      // CROOMS exact mode: largest B on the one-workgroup kernel (-1 = crooms.hip XG_MIN_ENVS)
+  int xg_ppt_min = -1;       // CROOMS exact mode: normal calls above this many 256-position blocks take 4 per thread
+  int xg_spb_min = -1;       // CROOMS exact mode: env kernels above this many env blocks take 4 per workgroup
   int taxi_npg_min = -1;    // TAXI numpy mode: largest B on the one-workgroup kernel (-1 = taxi.hip NPG_MIN_ENVS)
   int64_t fused_step = -1;  // GRID: the fused kernel's tag counter (GridCtl::step) set at every seed (-1 = kept)
   int wg_block_envs = 0;    // GRID windowed kernel: the smallest envs per block to use (0 = the smallest that fits)
+  int wg_fill_shift = -1;   // GRID windowed kernel: window rows moved per env wave onto SIMD 3's waves (-1 = default)
+  int persist_bpc = 0;      // TAXI / CROOMS / ANT-TAG streaming rollouts: blocks per CU (0 = every resident block, persistent_grid)
 };
 const GpDebugKnobs& gp_debug_knobs();
+
+// Grid of a persistent grid-stride tile loop (the Taxi / C-ROOMS / Ant-Tag rollouts: K steps per tile with the
+// tile's state in registers): every resident block (occupancy x CUs), capped by the tiles. An equal number of
+// tiles per block measured slower (round 6, profiles/r06_persist_grid.txt: C-ROOMS at 2^21 envs 17.4 us/step with
+// 1,024 blocks of 4 tiles vs 15.7 with 1,280 blocks of 3-4; Ant-Tag 14.6 vs 13.9): per-wave latency, not the
+// SIMDs' issue rate, bounds these loops, so more resident waves win even with a ragged last round. The knob
+// persist_bpc forces the blocks per CU (A/Bs).
+inline int persistent_grid(int ntiles, int cus, int occ) {
+  const int forced = gp_debug_knobs().persist_bpc;
+  const int bpc = forced > 0 ? forced : (occ < 1 ? 1 : (occ > 8 ? 8 : occ));
+  const int g = cus * bpc;
+  return ntiles < g ? (ntiles > 0 ? ntiles : 1) : g;
+}
 
 // Per-kind backend interface; gp_env owns one.
 // hipEvent pairs around the step-kernel launches (gp_set_profiling / gp_profile_read).
@@ -62,6 +79,8 @@ struct EnvBackend {
   int64_t B = 0;
   int device = 0;
   int rng_mode = GP_RNG_NUMPY;
+  int persist_grid = 0;  // blocks of the persistent rollout grid (Taxi / C-ROOMS / Ant-Tag; gp_query "persist_blocks")
+  int persist_occ = 0;   // resident blocks per CU of that rollout kernel (the occupancy query)
   int obs_dtype = GP_DTYPE_I32;
   int obs_width = 1;
   bool has_reset = false;
@@ -89,6 +108,8 @@ struct EnvBackend {
   virtual int query(const char* key, int64_t* v) const {
     if (!strcmp(key, "num_envs")) *v = B;
     else if (!strcmp(key, "rng_mode")) *v = rng_mode;
+    else if (!strcmp(key, "persist_blocks")) *v = persist_grid;
+    else if (!strcmp(key, "persist_occupancy")) *v = persist_occ;
     else {
       gp_set_error("gp_query: unknown key '%s'", key);
       return GP_E_INVALID;

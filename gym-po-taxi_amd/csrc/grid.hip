@@ -40,6 +40,10 @@ constexpr int MAX_TPB2 = 1024;  // max tiles per K2 block (B <= 256 * 1024 * EPB
 #ifndef WG_KMAX
 #define WG_KMAX 24
 #endif
+// Windowed kernel: window rows each env wave on SIMDs 0-2 hands to the env waves of SIMD 3 (3 per row given up).
+#ifndef WG_FILL_SHIFT
+#define WG_FILL_SHIFT 0
+#endif
 
 struct GridLdsTab {
   int32_t off, bytes;
@@ -3032,7 +3036,18 @@ int GridBackend::build_wgrid(const std::vector<uint16_t>& move, const std::vecto
   w.r_goal = d.r_goal;
   w.spin_limit = d.spin_limit;
   w.fault_block = d.fault_block;
-  w.rw_words = (E + 2 * H) / 512;
+  w.rw_words = (E + 2 * H) / 64;
+  {  // rows per env wave: env waves 3 and 7 share their SIMD with no control or store wave, so they take 3 rows from
+     // the six others for every row those give up (knob wg_fill_shift; -1 = default)
+    const int base = w.rw_words / 8;
+    const int sh = std::min(dbg.wg_fill_shift >= 0 ? dbg.wg_fill_shift : WG_FILL_SHIFT, base - 1);
+    int r = 0;
+    for (int v = 0; v < 8; ++v) {
+      w.fill_row0[v] = r;
+      w.fill_rows[v] = (v & 3) == 3 ? base + 3 * sh : base - sh;
+      r += w.fill_rows[v];
+    }
+  }
   w.wg_bias = dbg.wg_bias;
   w.tmode = dbg.wg_tmode;
   w.lds = L;
@@ -3068,11 +3083,14 @@ int GridBackend::upload_wgrid() {
   std::vector<PcgJump> jl(1024), jr((size_t)64 * wg_G), jb(2 * (size_t)wg_G);
   const PcgJump one = pcg_jump_params((u128)1, inc), j32s = pcg_jump_params((u128)32, inc);
   const PcgJump jBp1 = pcg_jump_params((u128)B + 1, inc);  // B + 1
-  jl[0] = PcgJump{0, 1, 0, 0};
   jl[1] = jBp1;
-  for (int l = 1; l < 512; ++l) {
-    jl[2 * l] = compose(one, jl[2 * (l - 1)]);            // lg
-    jl[2 * l + 1] = compose(j32s, jl[2 * (l - 1) + 1]);   // B + 32 lg + 1
+  for (int l = 1; l < 512; ++l) jl[2 * l + 1] = compose(j32s, jl[2 * (l - 1) + 1]);  // B + 32 lg + 1
+  for (int v = 0; v < 8; ++v) {  // 64 fill_row0[v] + lane
+    PcgJump x = pcg_jump_params((u128)(64 * w.fill_row0[v]), inc);
+    for (int l = 0; l < 64; ++l) {
+      jl[2 * (64 * v + l)] = x;
+      x = compose(one, x);
+    }
   }
   const PcgJump j62 = pcg_jump_params((u128)62, inc);
   PcgJump row = jBp1;  // B + 62 beta + 1
@@ -3087,7 +3105,7 @@ int GridBackend::upload_wgrid() {
     jb[2 * b + 1] = b ? pcg_jump_params((u128)(wg_E * b - wg_H + 1), inc) : PcgJump{0, 1, 0, 0};
   }
   w.jB = pcg_jump_params((u128)B, inc);
-  w.j512 = pcg_jump_params((u128)512, inc);
+  w.jrow = pcg_jump_params((u128)64, inc);
   w.jt64 = d.jt;
   w.dbg = d.dbg;
   w.ctl = d.ctl;

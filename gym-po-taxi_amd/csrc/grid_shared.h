@@ -40,23 +40,25 @@ struct WgParams {
   float r_step, r_wall, r_goal;
   uint32_t spin_limit;          // polls before a cross-block wait gives up (flags GridCtl::err)
   int32_t fault_block;          // test knob: this block never publishes (-1 off)
-  int32_t rw_words;             // words per env lane per window fill: (E + 2H) / 512
+  int32_t rw_words;             // 64-word rows of a window: (E + 2H) / 64
+  int32_t fill_row0[8], fill_rows[8];  // env wave w fills rows fill_row0[w] .. + fill_rows[w] - 1 of each window
   int32_t wg_bias;              // test knob: added to the predicted reset count (forces window misses); 0
   int32_t tmode;                // timing-study knob (gp_debug_set wg_tmode; 0 in production): see wgrid.hip TM_*
   WgLds lds;
   const char* limg;             // [lds.total] LDS image of the tables
   // Per-lane / per-block constant jumps, all applied to S(x_t), the state at a step's start (B = num envs):
-  const PcgJump* jlane;         // [512][2]: by lg (window fill from its base) and by B + 32 lg + 1 (coarse state lg)
+  const PcgJump* jlane;         // [512][2]: by 64 fill_row0[w] + lane (lg = 64 w + lane: the lane's first window word from
+                                //   the window base) and by B + 32 lg + 1 (coarse state lg)
   const PcgJump* jrej;          // [G][64]: by B + 62 beta + l + 1 (rejection-check slice of block beta, lane l)
   const PcgJump* jblk;          // [G][2]: by B + E beta - H (beta > 0; B for beta 0): the next window's base after
                                 //   the choice() draws; by E beta - H + 1 (beta > 0; 0 for beta 0): a launch's first
   const PcgJump* jt64;          // radix-64 general jump tables (JT_LEVELS x 64) for the rare paths
-  PcgJump jB, j512;             // jump by B (random(B)), by 512 (a lane's next window word)
+  PcgJump jB, jrow;             // jump by B (random(B)), by 64 (a lane's next window word: the next row)
   GridCtl* ctl;
   MetricSlot* mslot;            // [G]
   uint32_t* ae;                 // [B] agent cell | elapsed << 16
   uint64_t* slots;              // [2 step parities][2 round parities][G] tagged granules
-  unsigned long long* dbg;      // GP_STAMPS builds: [G][64][16] step stamps, then [G][8] launch stamps
+  unsigned long long* dbg;      // GP_STAMPS builds: [G][1024] step stamps (wgrid.hip ST_*), then [G][8] launch stamps
 };
 
 struct WgArgs {  // one launch: K steps, caller-owned action [K][B] and output [K][B] buffers

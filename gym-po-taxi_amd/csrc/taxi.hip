@@ -1734,8 +1734,9 @@ int TaxiBackend::build(const gp_taxi_config* cfg) {
   GP_HIP_CHECK(hipGetDeviceProperties(&prop, device));
   int occ = 0;
   GP_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, taxi_rollout<16, false>, TPB, d.tab_bytes));
-  occ = std::max(1, std::min(occ, 8));
-  grid = std::max(1, std::min(d.ntiles, prop.multiProcessorCount * occ));
+  grid = persistent_grid(d.ntiles, prop.multiProcessorCount, occ);
+  persist_grid = grid;
+  persist_occ = occ;
   if (int e = b_slot.alloc(sizeof(TaxiSlot) * grid)) return e;
   d.mslot = b_slot.as<TaxiSlot>();
   if (int e = derr.alloc()) return e;

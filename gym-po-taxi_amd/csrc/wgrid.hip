@@ -40,13 +40,14 @@ namespace {
 // kept in LDS during the launch and copied out at its end (a global store per stamp would be waited for by every
 // later `s_waitcnt vmcnt(0)` of that wave, gfx950 counting stores in vmcnt, and stretch the phases it measures).
 #ifdef GP_STAMPS
-__shared__ unsigned long long g_stamp[64 * 16 + 8];
+constexpr int ST_STEPS = 24, ST_SLOTS = 42;  // stamps of the first 24 steps, 42 per step (tools/wstamps.py)
+__shared__ unsigned long long g_stamp[32 * 32 + 8];
 #define WSTAMP(P, k, i)                                                                                  \
   do {                                                                                                   \
-    if ((threadIdx.x & 63) == 0 && (k) < 64) {                                                           \
+    if ((threadIdx.x & 63) == 0 && (k) < ST_STEPS) {                                                     \
       unsigned long long t_;                                                                             \
       asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                     \
-      g_stamp[(k) * 16 + (i)] = t_;                                                                      \
+      g_stamp[(k) * ST_SLOTS + (i)] = t_;                                                                \
     }                                                                                                    \
   } while (0)
 #define LSTAMP(P, i)                                                                                     \
@@ -54,7 +55,7 @@ __shared__ unsigned long long g_stamp[64 * 16 + 8];
     if ((threadIdx.x & 63) == 0) {                                                                       \
       unsigned long long t_;                                                                             \
       asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                     \
-      g_stamp[64 * 16 + (i)] = t_;                                                                       \
+      g_stamp[32 * 32 + (i)] = t_;                                                                       \
     }                                                                                                    \
   } while (0)
 #else
@@ -624,12 +625,17 @@ __device__ __forceinline__ void wg_env_slow(const WgParams& P, WgShared& sh, con
   }
 }
 
-// Fill the window: word j = m * 512 + lg is the base state advanced by j (this lane: jump by lg, then by 512).
-__device__ __forceinline__ void fill_window(uint64_t* RW, const PcgJump& jl, const PcgJump& j512, int nw, u128 base, int lg) {
+// Fill the window: env wave w writes rows fr0 .. fr0 + nrow - 1 of 64 words (word j = 64 r + lane): the lane's state
+// is the base jumped by 64 fr0 + lane (its jlane entry), then by 64 per row. The rows per wave (WgParams::fill_rows)
+// lean on the SIMD that hosts neither the control wave nor a store wave (round 6: its env waves finished their
+// fills ~0.7 us before the others).
+__device__ __forceinline__ void fill_window(uint64_t* RW, const PcgJump& jl, const PcgJump& jrow, int fr0, int nrow,
+                                            u128 base, int lane) {
   u128 s = apply_jump(jl, base);
-  for (int m = 0; m < nw; ++m) {
-    RW[m * 512 + lg] = pcg_output(s);
-    s = apply_jump(j512, s);
+  uint64_t* d = RW + fr0 * 64 + lane;
+  for (int m = 0; m < nrow; ++m) {
+    d[m * 64] = pcg_output(s);
+    s = apply_jump(jrow, s);
   }
 }
 
@@ -648,10 +654,10 @@ __device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Ta
   const uint32_t goal = (uint32_t)P.goal, tlim = (uint32_t)P.time_limit;
   uint32_t* derr = &P.ctl->err;
   uint32_t* aeg = P.ae;
-  const int nw = P.rw_words;
+  const int fr0 = P.fill_row0[w], nrow = P.fill_rows[w];  // this wave's window rows
   const int tmode = P.tmode;
-  const PcgJump j512 = P.j512;
-  // per-lane constant jumps: by lg (window fill) and by 32 lg + 1 (coarse state)
+  const PcgJump jrow = P.jrow;
+  // per-lane constant jumps: to the lane's first window word (64 fill_row0[w] + lane) and by 32 lg + 1 (coarse state)
   const PcgJump jrw = P.jlane[2 * lg], jcs = P.jlane[2 * lg + 1];
   uint32_t ae[NS];
   int32_t arow[NS], anext[NS];
@@ -664,7 +670,7 @@ __device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Ta
   // stage the tables (it lies behind them in LDS)
   if (!(tmode & TM_NOFIRST)) {
     const GridCtl* C = P.ctl;
-    fill_window(L.RW, jrw, j512, nw, apply_jump(P.jblk[2 * beta + 1], mk128(C->s_hi, C->s_lo)), lg);
+    fill_window(L.RW, jrw, jrow, fr0, nrow, apply_jump(P.jblk[2 * beta + 1], mk128(C->s_hi, C->s_lo)), lane);
   }
   if (w == 0) LSTAMP(P, 2);
   lds_barrier();  // P1
@@ -685,10 +691,13 @@ __device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Ta
 #pragma unroll
       for (int s = 0; s < NS; ++s) anext[s] = act[(size_t)(k + 1) * B + e0 + (size_t)s * 512 + lg];
     }
+    if (w == 0) WSTAMP(P, k, 40);
     lds_wait(&sh.fill_done, fill_target, derr);                  // every env wave's part of this step's window
+    if (w == 0) WSTAMP(P, k, 41);
     if (k >= NSTG) lds_wait(&sh.st_done, (uint32_t)SW * (uint32_t)(k - NSTG + 1), derr);  // this staging buffer copied out
     if (!(tmode & TM_NOPRIO)) __builtin_amdgcn_s_setprio(2);  // the transitions are on the critical path
     if (w == 0) WSTAMP(P, k, 0);
+    WSTAMP(P, k, 32 + w);
     // ---- transitions (the critical path) ----
     // Phased over the env slots so that their LDS round trips overlap: every slot's window word and threshold
     // row first, then the effective actions, the move-table entries, and the staged outputs last (a store to
@@ -737,6 +746,7 @@ __device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Ta
     if (lane == 0) lds_add(&sh.trans_done, 1u);
     if (!(tmode & TM_NOPRIO) && !(tmode & TM_ENVHIGH)) __builtin_amdgcn_s_setprio(0);
     if (w == 0) WSTAMP(P, k, 1);
+    WSTAMP(P, k, 16 + w);
     // the next step's actions (one step ahead)
     if (k + 1 < K && (tmode & TM_LATEACT)) {
 #pragma unroll
@@ -768,7 +778,7 @@ __device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Ta
     if (k + 1 < K) {
       lds_wait(&sh.sy_ready, (uint32_t)k + 1u, derr);
       const u128 Srw = mk128(sh.rw[(k + 1) & 1][0], sh.rw[(k + 1) & 1][1]);
-      if (!(tmode & TM_NOFILL)) fill_window(L.RW, jrw, j512, nw, Srw, lg);
+      if (!(tmode & TM_NOFILL)) fill_window(L.RW, jrw, jrow, fr0, nrow, Srw, lane);
       lds_release();
       if (lane == 0) lds_add(&sh.fill_done, 1u);
       fill_target += EW;
@@ -777,6 +787,7 @@ __device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Ta
     }
     if (w == 0) WSTAMP(P, k, 5);
     if (w == EW - 1) WSTAMP(P, k, 15);
+    WSTAMP(P, k, 24 + w);
     // ---- the exchange's outcome: the resetters' cells ----
     lds_wait(&sh.cells_done, (uint32_t)k + 1u, derr);
     if (w == 0) WSTAMP(P, k, 11);
@@ -804,7 +815,7 @@ __device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Ta
       }
     }
     if ((fix & 2u) && k + 1 < K) {  // the prediction missed the window: regenerate it exactly
-      fill_window(L.RW, jrw, j512, nw, mk128(sh.rw[(k + 1) & 1][0], sh.rw[(k + 1) & 1][1]), lg);
+      fill_window(L.RW, jrw, jrow, fr0, nrow, mk128(sh.rw[(k + 1) & 1][0], sh.rw[(k + 1) & 1][1]), lane);
       lds_release();
       if (lane == 0) lds_add(&sh.fill_done, 1u);
       fill_target += EW;
@@ -979,12 +990,12 @@ __global__ __launch_bounds__(TPB) void wgrid_rollout(const WgParams* __restrict_
   }
 #ifdef GP_STAMPS
   __syncthreads();
-  for (int i = tid; i < 64 * 16; i += TPB) P.dbg[(size_t)blockIdx.x * 64 * 16 + i] = g_stamp[i];
-  if (tid < 8 && tid != 4) P.dbg[(size_t)256 * 64 * 16 + (size_t)blockIdx.x * 8 + tid] = g_stamp[64 * 16 + tid];
+  for (int i = tid; i < 32 * 32; i += TPB) P.dbg[(size_t)blockIdx.x * 32 * 32 + i] = g_stamp[i];
+  if (tid < 8 && tid != 4) P.dbg[(size_t)256 * 32 * 32 + (size_t)blockIdx.x * 8 + tid] = g_stamp[32 * 32 + tid];
   if (tid == 0) {  // kernel end (after the copy-out)
     unsigned long long t_;
     asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");
-    P.dbg[(size_t)256 * 64 * 16 + (size_t)blockIdx.x * 8 + 4] = t_;
+    P.dbg[(size_t)256 * 32 * 32 + (size_t)blockIdx.x * 8 + 4] = t_;
   }
 #endif
 }

@@ -1,8 +1,9 @@
-"""Throughput of C-ROOMS exact mode (rng_mode='numpy': one workgroup up to 4096 envs, the multi-workgroup draw
-calls above) beside philox mode, same config.
+"""Throughput of C-ROOMS exact mode (rng_mode='numpy': one workgroup up to 1,024 envs (XG_MIN_ENVS), the
+multi-workgroup draw calls above) beside philox mode, same config.
 
 Usage (GPU box): python tools/crooms_numpy_rate.py [B ...] -> one JSON line per (mode, B). XG_MIN=n: the
-one-workgroup kernel only up to n envs (gp_debug_set xg_min_envs; crossover measurements). MODES=numpy: one mode.
+one-workgroup kernel only up to n envs (gp_debug_set xg_min_envs; crossover measurements). GP_KNOBS="k=v,...":
+other library knobs (recorded in the line). MODES=numpy: one mode.
 """
 import json
 import os
@@ -20,6 +21,7 @@ def rate(mode, B, K=None, reps=3):
     K = K or (50 if B <= 65536 else 8)
     from gym_po_amd._lib import debug_knobs
     knobs = {"xg_min_envs": int(os.environ["XG_MIN"])} if os.environ.get("XG_MIN") else {}
+    knobs.update((kv.split("=")[0], int(kv.split("=")[1])) for kv in os.environ.get("GP_KNOBS", "").split(",") if kv)
     with debug_knobs(**knobs):
         env = CRoomsEnv(B, obs_type="vector_mdp", rng_mode=mode)
     env.reset(seed=0)
@@ -32,7 +34,7 @@ def rate(mode, B, K=None, reps=3):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     return {"mode": mode, "num_envs": B, "steps": K * reps, "us_per_step": dt / (K * reps) * 1e6,
-            "env_steps_per_s": B * K * reps / dt, "xg_min_envs": knobs.get("xg_min_envs", 4096)}
+            "env_steps_per_s": B * K * reps / dt, "knobs": knobs}
 
 
 if __name__ == "__main__":

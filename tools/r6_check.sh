@@ -51,6 +51,13 @@ for task in "${@:-tests ab bench floor}"; do
       run 400 $O/taxiprof.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/taxiprof -o p -- python3 -u tools/taxi_numpy_rate.py ${TAXI_B:-65536 4194304}
       grep numpy $O/taxiprof.log
       for f in $(find $O/taxiprof -name "*kernel_stats.csv"); do cp $f $O/taxi_kernel_stats.csv; head -12 $f | cut -c1-220; done ;;
+    fshift)  # windowed kernel: window rows moved onto SIMD 3's env waves (wg_fill_shift), latency_probe per value
+      for rep in 1 2; do
+        for F in ${FSHIFTS:-0 1 2}; do
+          GP_KNOBS=wg_kmax=1000,wg_fill_shift=$F run 150 $O/fs_$F.log python -u tools/latency_probe.py ${FS_B:-1048576} ${ABK:-20 128}
+          echo "== $rep fill_shift $F"; grep "B=" $O/fs_$F.log
+        done
+      done ;;
     strong)  # strong-scaling shard sizes: the fused kernel (wg_kmax 0) vs the windowed kernel (wg_kmax 1000)
       for B in ${STRONG_B:-131072 262144}; do
         for kn in 0 1000; do
@@ -63,6 +70,37 @@ for task in "${@:-tests ab bench floor}"; do
         GP_KNOBS=wg_kmax=1000,wg_block_envs=$E run 150 $O/blk_$E.log python -u tools/latency_probe.py ${BLK_B:-131072} 20 128
         echo "== E $E"; grep "B=" $O/blk_$E.log
       done ;;
+    persist)  # the streaming rollouts' persistent grid: balanced_grid's choice (bpc 0) vs forced blocks per CU
+      for W in ${PW:-crooms anttag taxi}; do
+        for rep in 1 2; do
+          for bpc in ${PBPC:-0 5 4}; do
+            GP_KNOBS=persist_bpc=$bpc run 300 $O/persist_${W}_$bpc.log python3 bench.py --no-cpu-baseline --workload $W ${PSTEPS:---steps 1024 --warmup 128}
+            tail -n 1 $O/persist_${W}_$bpc.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); r=d["roofline"]; print("'$W' bpc '$bpc'", "%.4g" % d["value"], "us/step %.3f" % (d["ms_per_step"]*1e3), "frac %.3f" % r["frac"], d["config"].get("persistent_grid"))'
+          done
+        done
+      done ;;
+    occ)  # streaming rollouts: library variant (occupancy build) x forced blocks per CU, "W:LIB:BPC" cases
+      for rep in 1 2; do
+        for c in ${OCC_CASES:-crooms:base:0 crooms:base:8 crooms:cw6:0 crooms:cw8:0 anttag:base:0 anttag:base:8 anttag:at8:0}; do
+          IFS=: read W V bpc <<< "$c"
+          L=$LD/libgympo_amd_$V.so
+          [ "$V" = base ] && L=$LD/libgympo_amd.so
+          GYM_PO_AMD_LIB=$L GP_KNOBS=persist_bpc=$bpc run 300 $O/occ_${W}_${V}_$bpc.log python3 bench.py --no-cpu-baseline --workload $W --steps 1024 --warmup 128
+          tail -n 1 $O/occ_${W}_${V}_$bpc.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); r=d["roofline"]; print("'$c'", "%.4g" % d["value"], "us/step %.3f" % (d["ms_per_step"]*1e3), "frac %.3f" % r["frac"], d["config"].get("persistent_grid"))'
+        done
+      done ;;
+    xg)  # C-ROOMS exact mode per knob set (XG_CASES: ';'-separated GP_KNOBS values, '-' = none) at XG_B envs
+      for rep in 1 2; do
+        IFS=';' read -ra CS <<< "${XG_CASES:--;xg_ppt_min=64;xg_ppt_min=64,xg_spb_min=64}"
+        for c in "${CS[@]}"; do
+          kn=$c; [ "$c" = "-" ] && kn=""
+          GP_KNOBS=$kn MODES=numpy run 300 $O/xg.log python3 -u tools/crooms_numpy_rate.py ${XG_B:-65536}
+          echo "== $rep [$c]"; cat $O/xg.log | grep numpy
+        done
+      done ;;
+    valu)  # VALU issue rates (tools/mb_valu.hip, built beforehand)
+      run 120 $O/valu.log tools/mb_valu.bin
+      cat $O/valu.log ;;
     counters)  # the PMC counters this GPU offers
       run 120 $O/counters.log rocprofv3 -L
       grep -i -E "icache|ifetch|SQC_" $O/counters.log | head -60 ;;
