@@ -53,7 +53,7 @@ constexpr uint32_t TAG_DRAW = 0x6d733121u;
 #endif
 // Minimum waves per SIMD of the rollout kernel (caps its VGPRs at 512 / waves; tuning knob).
 #ifndef GP_CR_WAVES
-#define GP_CR_WAVES 6
+#define GP_CR_WAVES 7
 #endif
 constexpr double MAX_VELOCITY = 5.0;
 // Largest batch of the exact (numpy-stream) mode, which runs in one workgroup.

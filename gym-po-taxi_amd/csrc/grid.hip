@@ -40,9 +40,9 @@ constexpr int MAX_TPB2 = 1024;  // max tiles per K2 block (B <= 256 * 1024 * EPB
 #ifndef WG_KMAX
 #define WG_KMAX 24
 #endif
-// Windowed kernel: window rows each env wave on SIMDs 0-2 hands to the env waves of SIMD 3 (3 per row given up).
-#ifndef WG_FILL_SHIFT
-#define WG_FILL_SHIFT 0
+// Windowed kernel: window rows per env wave, per-SIMD deltas (wg_fill_simd's encoding; 0 = even rows).
+#ifndef WG_FILL_SIMD
+#define WG_FILL_SIMD 0x3FFF  // SIMD 3 (no control or store wave) +3 rows per env wave, SIMDs 0-2 -1 (profiles/r06_prologue_fill_rows_ab.txt)
 #endif
 
 struct GridLdsTab {
@@ -2723,7 +2723,7 @@ struct GridBackend : EnvBackend {
   float at_ms[2] = {0.f, 0.f};        // its mean ms per launch: windowed, fused
   WgParams wg{};
   std::vector<char> wg_img;        // LDS image of its tables (the PCG jump parts rebuilt on every seed)
-  DevBuf b_wgp, b_wlimg, b_wjlane, b_wjrej, b_wjblk, b_wslots;
+  DevBuf b_wgp, b_wlimg, b_wjlane, b_wjrej, b_wjblk, b_wslots, b_wjfirst;
   bool fused_stg = false;          // outputs staged in LDS and written by the store waves
   // replay pointers for the next step
   const uint64_t* rp_u = nullptr;
@@ -3037,14 +3037,22 @@ int GridBackend::build_wgrid(const std::vector<uint16_t>& move, const std::vecto
   w.spin_limit = d.spin_limit;
   w.fault_block = d.fault_block;
   w.rw_words = (E + 2 * H) / 64;
-  {  // rows per env wave: env waves 3 and 7 share their SIMD with no control or store wave, so they take 3 rows from
-     // the six others for every row those give up (knob wg_fill_shift; -1 = default)
+  {  // rows per env wave (waves v and v + 4 share SIMD v): base +- a per-SIMD delta d[v & 3] (knob wg_fill_simd: four
+     // signed 4-bit deltas, SIMD 0 in the low nibble; they must sum to 0, else the rows stay even)
     const int base = w.rw_words / 8;
-    const int sh = std::min(dbg.wg_fill_shift >= 0 ? dbg.wg_fill_shift : WG_FILL_SHIFT, base - 1);
+    const int code = dbg.wg_fill_simd != 0 ? dbg.wg_fill_simd : WG_FILL_SIMD;
+    int dl[4], sum = 0;
+    bool ok = true;
+    for (int q = 0; q < 4; ++q) {
+      dl[q] = ((code >> (4 * q)) & 15) >= 8 ? ((code >> (4 * q)) & 15) - 16 : ((code >> (4 * q)) & 15);
+      sum += dl[q];
+      ok = ok && base + dl[q] >= 1;
+    }
+    if (sum != 0 || !ok) dl[0] = dl[1] = dl[2] = dl[3] = 0;
     int r = 0;
     for (int v = 0; v < 8; ++v) {
       w.fill_row0[v] = r;
-      w.fill_rows[v] = (v & 3) == 3 ? base + 3 * sh : base - sh;
+      w.fill_rows[v] = base + dl[v & 3];
       r += w.fill_rows[v];
     }
   }
@@ -3054,8 +3062,10 @@ int GridBackend::build_wgrid(const std::vector<uint16_t>& move, const std::vecto
   int e;
   if ((e = b_wgp.alloc(sizeof(WgParams))) || (e = b_wlimg.alloc((size_t)L.total)) ||
       (e = b_wjlane.alloc(sizeof(PcgJump) * 1024)) || (e = b_wjrej.alloc(sizeof(PcgJump) * 64 * (size_t)wg_G)) ||
-      (e = b_wjblk.alloc(sizeof(PcgJump) * 2 * (size_t)wg_G)) || (e = b_wslots.alloc(sizeof(uint64_t) * 4 * (size_t)wg_G)))
+      (e = b_wjblk.alloc(sizeof(PcgJump) * 2 * (size_t)wg_G)) || (e = b_wslots.alloc(sizeof(uint64_t) * 4 * (size_t)wg_G)) ||
+      (e = b_wjfirst.alloc(sizeof(PcgJump) * 1024)))
     return e;
+  w.jfirst = b_wjfirst.as<PcgJump>();
   w.limg = b_wlimg.as<char>();
   w.jlane = b_wjlane.as<PcgJump>();
   w.jrej = b_wjrej.as<PcgJump>();
@@ -3106,6 +3116,14 @@ int GridBackend::upload_wgrid() {
   }
   w.jB = pcg_jump_params((u128)B, inc);
   w.jrow = pcg_jump_params((u128)64, inc);
+  w.j512 = pcg_jump_params((u128)512, inc);
+  std::vector<PcgJump> jf(1024);
+  jf[0] = one;                                    // block 0: 1 + lg
+  jf[512] = pcg_jump_params((u128)wg_H, inc);     // blocks > 0: H + lg
+  for (int l = 1; l < 512; ++l) {
+    jf[l] = compose(one, jf[l - 1]);
+    jf[512 + l] = compose(one, jf[512 + l - 1]);
+  }
   w.jt64 = d.jt;
   w.dbg = d.dbg;
   w.ctl = d.ctl;
@@ -3115,6 +3133,7 @@ int GridBackend::upload_wgrid() {
   GP_HIP_CHECK(hipMemcpy(b_wjlane.p, jl.data(), jl.size() * sizeof(PcgJump), hipMemcpyHostToDevice));
   GP_HIP_CHECK(hipMemcpy(b_wjrej.p, jr.data(), jr.size() * sizeof(PcgJump), hipMemcpyHostToDevice));
   GP_HIP_CHECK(hipMemcpy(b_wjblk.p, jb.data(), jb.size() * sizeof(PcgJump), hipMemcpyHostToDevice));
+  GP_HIP_CHECK(hipMemcpy(b_wjfirst.p, jf.data(), jf.size() * sizeof(PcgJump), hipMemcpyHostToDevice));
   GP_HIP_CHECK(hipMemcpy(b_wgp.p, &w, sizeof(WgParams), hipMemcpyHostToDevice));
   return GP_OK;
 }

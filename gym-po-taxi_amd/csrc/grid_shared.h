@@ -52,8 +52,11 @@ struct WgParams {
   const PcgJump* jrej;          // [G][64]: by B + 62 beta + l + 1 (rejection-check slice of block beta, lane l)
   const PcgJump* jblk;          // [G][2]: by B + E beta - H (beta > 0; B for beta 0): the next window's base after
                                 //   the choice() draws; by E beta - H + 1 (beta > 0; 0 for beta 0): a launch's first
+  const PcgJump* jfirst;        // [2][512]: by 1 + lg (block 0) / by H + lg (blocks > 0) from the first window's base:
+                                //   a launch's step-0 word of env slot 0 of lane lg
   const PcgJump* jt64;          // radix-64 general jump tables (JT_LEVELS x 64) for the rare paths
-  PcgJump jB, jrow;             // jump by B (random(B)), by 64 (a lane's next window word: the next row)
+  PcgJump jB, jrow, j512;       // jump by B (random(B)), by 64 (a lane's next window word: the next row), by 512 (the
+                                //   next env slot's step-0 word)
   GridCtl* ctl;
   MetricSlot* mslot;            // [G]
   uint32_t* ae;                 // [B] agent cell | elapsed << 16

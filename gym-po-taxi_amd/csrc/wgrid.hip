@@ -81,9 +81,14 @@ constexpr int TM_STORELOW = 256; // store waves at priority 0 (default 1)
 constexpr int TM_ENVHIGH = 512; // env waves at priority 2 throughout (default: 2 for the transitions, 0 otherwise)
 constexpr int TM_NOTABLES = 1024;  // no table staging at launch (stale LDS tables: measurement only)
 constexpr int TM_NOFIRST = 2048;   // no first-window fill at launch (stale words: measurement only)
+constexpr int TM_ACTSTART = 4096;  // env waves issue the next step's action loads at the step's start (default: loop top)
+constexpr int TM_OLDPRO = 8192;    // round-5 prologue: the whole first window by rows, then the control wave's go-ahead
 
 constexpr int EW = 8;                 // env waves
-constexpr int SW = 2;                 // store waves
+#ifndef WG_SW
+#define WG_SW 2
+#endif
+constexpr int SW = WG_SW;             // store waves (3: one on each SIMD without the control wave, 12 waves per CU)
 constexpr int CWAVE = EW;             // the control wave
 constexpr int NWAVES = EW + 1 + SW;
 constexpr int TPB = NWAVES * 64;      // 704 threads
@@ -433,8 +438,8 @@ __device__ __forceinline__ void wg_ctrl(const WgParams& P, WgShared& sh, const T
   const uint32_t bias = (uint32_t)P.wg_bias;
   uint32_t* derr = &C->err;
   lds_barrier();  // P1: tables staged, counters zeroed
-  // the first window: step 0's own random(B) words, exact: word 0 is S(x_0 + 1 + E beta - heff)
-  if (lane == 0) {
+  // round 5's prologue (TM_OLDPRO): the first window's offset for the env waves, which filled the window by rows
+  if (lane == 0 && (P.tmode & TM_OLDPRO)) {
     const u128 s = apply_jump(jpro, Sx);
     sh.rw[0][0] = hi64(s);
     sh.rw[0][1] = lo64(s);
@@ -666,11 +671,28 @@ __device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Ta
     ae[k] = aeg[e0 + (size_t)k * 512 + lg];
     anext[k] = act[e0 + (size_t)k * 512 + lg];
   }
-  // the first window, exact (word 0 = S(x_0 + 1 + E beta - heff)), filled from global data while the other waves
-  // stage the tables (it lies behind them in LDS)
+  // Step 0's words are exact (no prediction): env i = s 512 + lg of block beta draws S(x_0 + 1 + E beta + i). Each lane
+  // computes its own NS words straight into the window slots its envs read (i + off0), from global data while the
+  // control and store waves stage the tables (the window lies behind them in LDS), so step 0 waits for no other
+  // wave's words and for no go-ahead: only for the tables (P1). (TM_OLDPRO: round 5's prologue, the whole window
+  // by rows, then the control wave's offset.)
+  const bool oldpro = (tmode & TM_OLDPRO) != 0;
   if (!(tmode & TM_NOFIRST)) {
     const GridCtl* C = P.ctl;
-    fill_window(L.RW, jrw, jrow, fr0, nrow, apply_jump(P.jblk[2 * beta + 1], mk128(C->s_hi, C->s_lo)), lane);
+    const u128 S0 = mk128(C->s_hi, C->s_lo);
+    if (oldpro) {
+      fill_window(L.RW, jrw, jrow, fr0, nrow, apply_jump(P.jblk[2 * beta + 1], S0), lane);
+    } else {
+      const int32_t off0 = beta == 0 ? 1 : P.halo;
+      u128 st = apply_jump(P.jfirst[(beta ? 512 : 0) + lg], apply_jump(P.jblk[2 * beta + 1], S0));
+      const PcgJump j512 = P.j512;
+#pragma unroll
+      for (int k = 0; k < NS; ++k) {
+        L.RW[k * 512 + lg + off0] = pcg_output(st);
+        if (k + 1 < NS) st = apply_jump(j512, st);
+      }
+      if (lg == 0) sh.rw_off[0] = off0;
+    }
   }
   if (w == 0) LSTAMP(P, 2);
   lds_barrier();  // P1
@@ -679,25 +701,31 @@ __device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Ta
     arow[k] = action_row<NA>(anext[k], derr);
     acc.lens += ae[k] >> 16;  // episode lengths: + elapsed at the start - elapsed at the end + steps
   }
-  lds_wait(&sh.pro, 1u, derr);  // the first window's offset
+  if (oldpro) {
+    lds_wait(&sh.pro, 1u, derr);  // the first window's offset
+    if (lane == 0) lds_add(&sh.fill_done, 1u);
+  }
   if (w == 0) LSTAMP(P, 7);
-  if (lane == 0) lds_add(&sh.fill_done, 1u);
   uint32_t fill_target = EW;
   uint64_t bm[NS];
   uint32_t pre[NS];
   for (int k = 0; k < K; ++k) {
     char* stg = L.stg(k, E);
-    if (k + 1 < K && !(tmode & TM_LATEACT)) {
+    if (w == 0) WSTAMP(P, k, 41);
+    if (k + 1 < K && !(tmode & (TM_LATEACT | TM_ACTSTART))) {
 #pragma unroll
       for (int s = 0; s < NS; ++s) anext[s] = act[(size_t)(k + 1) * B + e0 + (size_t)s * 512 + lg];
     }
     if (w == 0) WSTAMP(P, k, 40);
     lds_wait(&sh.fill_done, fill_target, derr);                  // every env wave's part of this step's window
-    if (w == 0) WSTAMP(P, k, 41);
     if (k >= NSTG) lds_wait(&sh.st_done, (uint32_t)SW * (uint32_t)(k - NSTG + 1), derr);  // this staging buffer copied out
     if (!(tmode & TM_NOPRIO)) __builtin_amdgcn_s_setprio(2);  // the transitions are on the critical path
     if (w == 0) WSTAMP(P, k, 0);
     WSTAMP(P, k, 32 + w);
+    if (k + 1 < K && (tmode & TM_ACTSTART)) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s) anext[s] = act[(size_t)(k + 1) * B + e0 + (size_t)s * 512 + lg];
+    }
     // ---- transitions (the critical path) ----
     // Phased over the env slots so that their LDS round trips overlap: every slot's window word and threshold
     // row first, then the effective actions, the move-table entries, and the staged outputs last (a store to
@@ -933,6 +961,7 @@ __global__ __launch_bounds__(TPB) void wgrid_rollout(const WgParams* __restrict_
   if (tid == EW * 64) {
     sh.trans_done = sh.cs_done = sh.r2s_done = sh.fill_done = sh.res_done = sh.st_done = 0;
     sh.sx_ready = sh.sy_ready = sh.cells_done = sh.pro = 0;
+    if (!(P.tmode & TM_OLDPRO)) sh.fill_done = EW;  // step 0's words: every env wave wrote its own before P1
     sh.fix[0] = sh.fix[1] = 0;
   }
   const Tabs tb(dyn, P);

@@ -117,13 +117,13 @@ def test_wgrid_block_sizes_bit_exact(B, E, gpu_device):
     assert m["env_steps"] == B * 54
 
 
-@pytest.mark.parametrize("knobs", [dict(wg_halo=512), dict(wg_bias=3000), dict(wg_bias=-600), dict(wg_fill_shift=0),
-                                   dict(wg_fill_shift=2), dict(wg_fill_shift=2, wg_bias=3000),
-                                   dict(wg_halo=512, wg_fill_shift=3)])
+@pytest.mark.parametrize("knobs", [dict(wg_halo=512), dict(wg_bias=3000), dict(wg_bias=-600), dict(wg_fill_simd=0xFFF3),
+                                   dict(wg_fill_simd=0x6EEE), dict(wg_fill_simd=0x6EEE, wg_bias=3000),
+                                   dict(wg_halo=512, wg_fill_simd=0x11E0)])
 def test_wgrid_halo_and_forced_window_misses(knobs, gpu_device):
     """wg_bias shifts every step's predicted reset count (3000 resets = ~1500 draws, far beyond the 256-draw
     halo; -600 wraps to a huge count): each step's window is regenerated exactly after the exchange.
-    wg_fill_shift moves window rows between the env waves (every distribution fills the same words)."""
+    wg_fill_simd moves window rows between the SIMDs' env waves (every distribution fills the same words)."""
     from gym_po_amd._lib import debug_knobs
     B = 1 << 20
     with debug_knobs(**knobs):

@@ -51,11 +51,14 @@ for task in "${@:-tests ab bench floor}"; do
       run 400 $O/taxiprof.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/taxiprof -o p -- python3 -u tools/taxi_numpy_rate.py ${TAXI_B:-65536 4194304}
       grep numpy $O/taxiprof.log
       for f in $(find $O/taxiprof -name "*kernel_stats.csv"); do cp $f $O/taxi_kernel_stats.csv; head -12 $f | cut -c1-220; done ;;
-    fshift)  # windowed kernel: window rows moved onto SIMD 3's env waves (wg_fill_shift), latency_probe per value
+    fsimd)  # windowed kernel: per-SIMD window-row deltas (wg_fill_simd, 4 signed nibbles), LIB:CODE cases
       for rep in 1 2; do
-        for F in ${FSHIFTS:-0 1 2}; do
-          GP_KNOBS=wg_kmax=1000,wg_fill_shift=$F run 150 $O/fs_$F.log python -u tools/latency_probe.py ${FS_B:-1048576} ${ABK:-20 128}
-          echo "== $rep fill_shift $F"; grep "B=" $O/fs_$F.log
+        for c in ${FS_CASES:-base:0}; do
+          IFS=: read V F <<< "$c"
+          L=$LD/libgympo_amd_$V.so
+          [ "$V" = base ] && L=$LD/libgympo_amd.so
+          GYM_PO_AMD_LIB=$L GP_KNOBS=wg_kmax=1000,wg_fill_simd=$F run 150 $O/fs_${V}_$F.log python -u tools/latency_probe.py ${FS_B:-1048576} ${ABK:-20 128}
+          echo "== $rep $V fill_simd $F"; grep "B=" $O/fs_${V}_$F.log
         done
       done ;;
     strong)  # strong-scaling shard sizes: the fused kernel (wg_kmax 0) vs the windowed kernel (wg_kmax 1000)

@@ -10,7 +10,7 @@ per stamp was waited for by later vmcnt(0) waits and stretched the phases), per 
               9 all-gather done, 10 cells drawn (before B2), 11 after B2, 12 next state done
   store wave: 13 copy start (after B2), 14 copy issued
   every env wave w: 16 + w transitions done, 24 + w window filled (before B2), 32 + w step start
-  env wave 0: 40 loop top (next actions issued), 41 every wave's window part in (fill_done)
+  env wave 0: 41 loop top (before the next actions' loads), 40 after issuing them
 Launch stamps per block: 0 entry, 1 P1 passed (control), 2 env wave 0's first window filled, 3 control step loop
 done, 4 kernel end, 5 / 6 table staging done (control wave / store wave 0), 7 env wave 0 has the first
 window's offset.
@@ -133,9 +133,9 @@ sw = x[:, :, 32:40] - x[:, :, :1]
 print("  start: " + " ".join(f"w{w}:{np.median(sw[:, :, w]):5.0f}" for w in range(8)))
 nxt = a[:, 3:kk, 32:40] - a[:, 2:kk - 1, :1]  # every wave's NEXT step start, from wave 0's start of this step
 print("  next start: " + " ".join(f"w{w}:{np.median(nxt[:, :, w]):5.0f}" for w in range(8)))
-lt = a[:, 3:kk, 40] - a[:, 2:kk - 1, 0]
-fd = a[:, 3:kk, 41] - a[:, 2:kk - 1, 0]
-print("  wave 0 next loop top (actions issued) %.0f, fill_done seen %.0f, next start %.0f (median, from this step's start)" % (
+lt = a[:, 3:kk, 41] - a[:, 2:kk - 1, 0]
+fd = a[:, 3:kk, 40] - a[:, 2:kk - 1, 0]
+print("  wave 0 next loop top %.0f, next actions issued %.0f, next start %.0f (median, from this step's start)" % (
     np.median(lt), np.median(fd), np.median(step)))
 print("  which wave is slowest (transitions / fill), counts over blocks x steps:",
       np.bincount(tw.argmax(2).ravel(), minlength=8).tolist(), np.bincount(fw.argmax(2).ravel(), minlength=8).tolist())
