@@ -225,6 +225,7 @@ int gp_debug_set(const char* key, int64_t value) {
   else if (!strcmp(key, "fused_step")) g_dbg.fused_step = value;
   else if (!strcmp(key, "wg_block_envs")) g_dbg.wg_block_envs = (int)value;
   else if (!strcmp(key, "wg_fill_simd")) g_dbg.wg_fill_simd = (int)value;
+  else if (!strcmp(key, "wg_fill_wave")) g_dbg.wg_fill_wave = value;
   else if (!strcmp(key, "xg_ppt_min")) g_dbg.xg_ppt_min = (int)value;
   else if (!strcmp(key, "xg_spb_min")) g_dbg.xg_spb_min = (int)value;
   else if (!strcmp(key, "persist_bpc")) g_dbg.persist_bpc = (int)value;

@@ -42,6 +42,7 @@ struct GpDebugKnobs {
   int64_t fused_step = -1;  // GRID: the fused kernel's tag counter (GridCtl::step) set at every seed (-1 = kept)
   int wg_block_envs = 0;    // GRID windowed kernel: the smallest envs per block to use (0 = the smallest that fits)
   int wg_fill_simd = 0;     // GRID windowed kernel: per-SIMD window-row deltas, 4 signed nibbles (0 = WG_FILL_SIMD)
+  int64_t wg_fill_wave = 0; // GRID windowed kernel: per-wave deltas on top, 8 signed nibbles (wave 0 lowest)
   int persist_bpc = 0;      // TAXI / CROOMS / ANT-TAG streaming rollouts: blocks per CU (0 = every resident block, persistent_grid)
 };
 const GpDebugKnobs& gp_debug_knobs();

@@ -41,6 +41,11 @@ constexpr int MAX_TPB2 = 1024;  // max tiles per K2 block (B <= 256 * 1024 * EPB
 #define WG_KMAX 24
 #endif
 // Windowed kernel: window rows per env wave, per-SIMD deltas (wg_fill_simd's encoding; 0 = even rows).
+// Per-wave deltas on top (wg_fill_wave's encoding): the first env wave of each SIMD (the older one, issued first at
+// equal priority) +1 row, the second -1, so that the second does not fill alone at the end of the step.
+#ifndef WG_FILL_WAVE
+#define WG_FILL_WAVE 0xFFFF1111u
+#endif
 #ifndef WG_FILL_SIMD
 #define WG_FILL_SIMD 0x3FFF  // SIMD 3 (no control or store wave) +3 rows per env wave, SIMDs 0-2 -1 (profiles/r06_prologue_fill_rows_ab.txt)
 #endif
@@ -3049,10 +3054,21 @@ int GridBackend::build_wgrid(const std::vector<uint16_t>& move, const std::vecto
       ok = ok && base + dl[q] >= 1;
     }
     if (sum != 0 || !ok) dl[0] = dl[1] = dl[2] = dl[3] = 0;
+    int dv[8];  // knob wg_fill_wave: per-wave deltas (eight signed nibbles, wave 0 lowest) on top, summing to 0
+    int vsum = 0;
+    bool vok = true;
+    for (int v = 0; v < 8; ++v) {
+      const int n = (int)(((uint32_t)(dbg.wg_fill_wave != 0 ? dbg.wg_fill_wave : WG_FILL_WAVE) >> (4 * v)) & 15u);
+      dv[v] = n >= 8 ? n - 16 : n;
+      vsum += dv[v];
+      vok = vok && base + dl[v & 3] + dv[v] >= 1;
+    }
+    if (vsum != 0 || !vok)
+      for (int v = 0; v < 8; ++v) dv[v] = 0;
     int r = 0;
     for (int v = 0; v < 8; ++v) {
       w.fill_row0[v] = r;
-      w.fill_rows[v] = base + dl[v & 3];
+      w.fill_rows[v] = base + dl[v & 3] + dv[v];
       r += w.fill_rows[v];
     }
   }

@@ -633,7 +633,8 @@ __device__ __forceinline__ void wg_env_slow(const WgParams& P, WgShared& sh, con
 // Fill the window: env wave w writes rows fr0 .. fr0 + nrow - 1 of 64 words (word j = 64 r + lane): the lane's state
 // is the base jumped by 64 fr0 + lane (its jlane entry), then by 64 per row. The rows per wave (WgParams::fill_rows)
 // lean on the SIMD that hosts neither the control wave nor a store wave (round 6: its env waves finished their
-// fills ~0.7 us before the others).
+// fills ~0.7 us before the others). (Two independent chains per lane, for the ILP of a wave whose SIMD partner
+// has finished, measured no faster at 167 VGPRs: profiles/r06_fill_chains_ab.txt.)
 __device__ __forceinline__ void fill_window(uint64_t* RW, const PcgJump& jl, const PcgJump& jrow, int fr0, int nrow,
                                             u128 base, int lane) {
   u128 s = apply_jump(jl, base);

@@ -119,7 +119,8 @@ def test_wgrid_block_sizes_bit_exact(B, E, gpu_device):
 
 @pytest.mark.parametrize("knobs", [dict(wg_halo=512), dict(wg_bias=3000), dict(wg_bias=-600), dict(wg_fill_simd=0xFFF3),
                                    dict(wg_fill_simd=0x6EEE), dict(wg_fill_simd=0x6EEE, wg_bias=3000),
-                                   dict(wg_halo=512, wg_fill_simd=0x11E0)])
+                                   dict(wg_halo=512, wg_fill_simd=0x11E0), dict(wg_fill_wave=0xEEEE2222),
+                                   dict(wg_fill_wave=0x1E2F0E11, wg_bias=-600)])
 def test_wgrid_halo_and_forced_window_misses(knobs, gpu_device):
     """wg_bias shifts every step's predicted reset count (3000 resets = ~1500 draws, far beyond the 256-draw
     halo; -600 wraps to a huge count): each step's window is regenerated exactly after the exchange.
