@@ -10,7 +10,7 @@ independent, full-chip kernels); `"numpy"` draws the reference's own PCG64 strea
 ziggurat normals and buffered Lemire choices, seed-identical with the reference; up to 1,024 envs one
 workgroup resolves the data-dependent word counts, above that every draw call is resolved over all of its
 stream positions by grid-wide kernels, at any size: 7.0-7.3e9 env-steps/s at 2^21 envs (286-299 us per
-step), ~18x below philox, profiles/r05_crooms_numpy_rate.txt);
+step), ~20x below philox's 14 us, profiles/r05_crooms_numpy_rate.txt);
 `"replay"` takes the reference stream's values per env (bit-exact parity tests).
 
 Philox-mode normals are Box-Muller on float32 hardware log2 / sqrt / sin / cos (a 53-bit u1, so the radius
