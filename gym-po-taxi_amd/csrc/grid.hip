@@ -3772,10 +3772,12 @@ int GridBackend::build(const gp_grid_config* cfg) {
     for (int c = 0; c < nc; ++c)
       ocell[c] = cfg->obs_kind == GP_OBS_HANSEN ? ofix[c] : t1[c] + (t2.empty() ? 0 : t2[d.fixed_goal]);
     if (int e2 = build_wgrid(move, thr, ocell)) return e2;
-    // Blocks of <= 1,024 envs (<= 2^18 envs, e.g. the strong-scaling shards): the windowed kernel at every launch
-    // length (round 6, tools/r6_check.sh strong: 3.02 vs 3.69 us/step at 2^17 envs and 3.32 vs 3.60 at 2^18 in
-    // 128-step launches, 67 vs 82 us per 20-step launch at 2^17).
-    if (dbg.wg_kmax < 0 && wg_G && wg_NS <= 2) wg_kmax = 1 << 30;
+    // The windowed kernel at every launch length for blocks of <= 1,024 envs (<= 2^18 envs, e.g. the strong-scaling
+    // shards: 3.02 vs 3.69 us/step at 2^17 envs and 3.32 vs 3.60 at 2^18 in 128-step launches, 67 vs 82 us per
+    // 20-step launch at 2^17) and, since its round-6 window-row balance, for 4,096-env blocks (2^20 envs: 109.4-109.6
+    // vs 117.0-118.1 us at K = 20, 328.6-328.8 vs 334.8-343.1 at 64, 647.1-647.2 vs 647.3-655.3 at 128,
+    // profiles/r06_kernel_by_K.txt). 2,048-env blocks keep WG_KMAX (not re-measured).
+    if (dbg.wg_kmax < 0 && wg_G && (wg_NS <= 2 || wg_NS >= 8)) wg_kmax = 1 << 30;
   }
   wg_kmax_default = wg_kmax;
   nslots = std::max({d.nblk, grid_persist, fused_G, wg_G});

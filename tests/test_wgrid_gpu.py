@@ -97,9 +97,10 @@ def test_fused_tag_wrap_between_windowed_launches_bit_exact(fstep, gpu_device):
 
 
 def test_small_blocks_default_to_windowed_at_every_length(gpu_device):
-    """Blocks of <= 1,024 envs (2^17 / 2^18 envs: the strong-scaling shards) run the windowed kernel for every launch
-    length by default; 2048-env blocks hand launches of more than 24 steps to the fused kernel."""
-    for B, kmax in ((1 << 17, 1 << 30), (1 << 18, 1 << 30), (1 << 19, 24), (1 << 20, 24)):
+    """Blocks of <= 1,024 envs (2^17 / 2^18 envs: the strong-scaling shards) and of 4,096 envs (2^20, the headline)
+    run the windowed kernel for every launch length by default; 2048-env blocks hand launches of more than 24 steps
+    to the fused kernel."""
+    for B, kmax in ((1 << 17, 1 << 30), (1 << 18, 1 << 30), (1 << 19, 24), (1 << 20, 1 << 30)):
         env = _fourrooms(B, gpu_device)
         assert env.query("wgrid_kmax") == kmax, B
         env.close()
@@ -256,12 +257,13 @@ def test_wgrid_goal_crowd_bit_exact(B, frac, gpu_device):
     _check_chunks(env, ora, (6, 1, 9), action_seed=11, n_act=4)
 
 
-@pytest.mark.parametrize("tmode", [4, 64, 128, 32 | 512, 8 | 16])
+@pytest.mark.parametrize("tmode", [4, 64, 128, 32 | 512, 8 | 16, 4096, 8192])
 def test_wgrid_schedule_variants_bit_exact(tmode, gpu_device):
     """Test-only schedules of the windowed kernel (gp_debug_set wg_tmode, wgrid.hip TM_*): 4 = next actions loaded
     after the transitions, 64 = store waves copy a step as soon as it is final, 128 = no candidate cells (every
     resetter's word drawn after the exchange), 32|512 = env-wave priority off / always high, 8|16 = throttled
-    stores and busy polling. Results must not depend on the schedule."""
+    stores and busy polling, 4096 = next actions loaded at the step start, 8192 = round 5's prologue. Results must
+    not depend on the schedule."""
     from gym_po_amd._lib import debug_knobs
     B = 1 << 18
     with debug_knobs(wg_tmode=tmode):
