@@ -83,6 +83,7 @@ constexpr int TM_NOTABLES = 1024;  // no table staging at launch (stale LDS tabl
 constexpr int TM_NOFIRST = 2048;   // no first-window fill at launch (stale words: measurement only)
 constexpr int TM_ACTSTART = 4096;  // env waves issue the next step's action loads at the step's start (default: loop top)
 constexpr int TM_OLDPRO = 8192;    // round-5 prologue: the whole first window by rows, then the control wave's go-ahead
+constexpr int TM_CELLSWAP = 16384; // blocks of <= 1,024 envs: the control wave places the resetters' cells (round 5)
 
 constexpr int EW = 8;                 // env waves
 #ifndef WG_SW
@@ -116,7 +117,8 @@ struct WgShared {
   uint64_t rw[2][2];         // by parity of the step a window serves: its base state (hi, lo)
   int32_t rw_off[2];         // by step parity: env i of that step reads window word i + rw_off
   uint32_t fix[2];           // by step parity: bit 0 slow path, bit 1 window regeneration
-  uint32_t R, h, u, nrp;     // slow path: block prefix, has_uint32 / uinteger at the step start, # positions
+  uint32_t R, h, u, nrp;     // block prefix, has_uint32 / uinteger at the step start, # rejected positions (slow path)
+  uint32_t cbase;            // half-word of cand[0] (env-wave cells)
   uint32_t rp[MAXRP];        // slow path: rejected half-word positions, ascending
   uint16_t r2s[4096];        // resetter rank in the block -> env slot
   uint16_t cand[NCAND];      // the cells of choice() half-words cbase .. cbase + NCAND - 1 (predicted block prefix)
@@ -436,6 +438,9 @@ __device__ __forceinline__ void wg_ctrl(const WgParams& P, WgShared& sh, const T
   const uint32_t nag = (uint32_t)P.n_agent, thra = P.thr_agent;
   const int32_t H = P.halo;
   const uint32_t bias = (uint32_t)P.wg_bias;
+  // small blocks (<= 1,024 envs): the env waves place their resetters' cells (their SIMDs have room; the control
+  // wave's cells loop leaves the chain); 4,096-env blocks: the control wave (env waves' SIMD time bounds the step)
+  const bool envcells = NS <= 2 && !(P.tmode & TM_CELLSWAP);
   uint32_t* derr = &C->err;
   lds_barrier();  // P1: tables staged, counters zeroed
   // round 5's prologue (TM_OLDPRO): the first window's offset for the env waves, which filled the window by rows
@@ -527,7 +532,13 @@ __device__ __forceinline__ void wg_ctrl(const WgParams& P, WgShared& sh, const T
     lds_wait(&sh.r2s_done, (uint32_t)EW * (uint32_t)(k + 1), derr);
     if (!slow) {
       words_to_draws(b, h, used, h2);
-      if (cb) {  // this block's resetters' cells: rank q takes half-word R + q
+      if (envcells && lane == 0) {  // the env waves place their own resetters (rank q -> half-word R + q)
+        sh.R = R;
+        sh.h = h;
+        sh.u = u;
+        sh.cbase = cbase;
+      }
+      if (cb && !envcells) {  // this block's resetters' cells: rank q takes half-word R + q
         uint16_t* st = reinterpret_cast<uint16_t*>(L.stg(k, E));
         for (uint32_t q = (uint32_t)lane; q < cb; q += 64u) {
           const uint32_t hw = R + q;
@@ -630,6 +641,41 @@ __device__ __forceinline__ void wg_env_slow(const WgParams& P, WgShared& sh, con
   }
 }
 
+// Fast path (no rejection in the step's choice() words), blocks of <= 1,024 envs: this lane's resetters take
+// half-words R + rank, rank from the listing (pre + mbcnt); their cells are the control wave's candidates when inside
+// its window, else drawn from the coarse states (the control wave publishes R, h, u, cbase with cells_done and draws
+// nothing after the all-gather, so its cells loop is off the step's chain).
+template <int NS>
+__device__ __forceinline__ void wg_env_cells(const WgParams& P, WgShared& sh, const Tabs& tb, const uint64_t* CS,
+                                             char* stg, uint32_t dn, const uint32_t (&pre)[NS], const uint64_t (&bm)[NS],
+                                             uint32_t (&ae)[NS]) {
+  if (!dn) return;
+  const int lg = threadIdx.x;
+  const uint32_t R = sh.R, h = sh.h, u = sh.u, cbase = sh.cbase;
+  const bool nocand = (P.tmode & TM_NOCAND) != 0;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    if (!((dn >> s) & 1u)) continue;
+    const uint32_t hw = R + pre[s] + mbcnt(bm[s]);
+    uint32_t cell;
+    if (hw - cbase < (uint32_t)NCAND && !nocand) {  // (hw >= cbase >= h: never the buffered half)
+      cell = sh.cand[hw - cbase];
+    } else {
+      uint32_t word;
+      if (h && hw == 0) {
+        word = u;
+      } else {
+        const uint32_t hh = hw - h;
+        const uint64_t x = pcg_output(draw_state(tb, CS, hh >> 1));
+        word = (hh & 1u) ? (uint32_t)(x >> 32) : (uint32_t)x;
+      }
+      cell = tb.avalid(lemire_value(word, (uint32_t)P.n_agent));
+    }
+    reinterpret_cast<uint16_t*>(stg)[2 * (s * 512 + lg)] = (uint16_t)cell;
+    ae[s] = cell;
+  }
+}
+
 // Fill the window: env wave w writes rows fr0 .. fr0 + nrow - 1 of 64 words (word j = 64 r + lane): the lane's state
 // is the base jumped by 64 fr0 + lane (its jlane entry), then by 64 per row. The rows per wave (WgParams::fill_rows)
 // lean on the SIMD that hosts neither the control wave nor a store wave (round 6: its env waves finished their
@@ -660,6 +706,7 @@ __device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Ta
   const uint32_t goal = (uint32_t)P.goal, tlim = (uint32_t)P.time_limit;
   uint32_t* derr = &P.ctl->err;
   uint32_t* aeg = P.ae;
+  const bool envcells = NS <= 2 && !(P.tmode & TM_CELLSWAP);  // (as wg_ctrl)
   const int fr0 = P.fill_row0[w], nrow = P.fill_rows[w];  // this wave's window rows
   const int tmode = P.tmode;
   const PcgJump jrow = P.jrow;
@@ -823,6 +870,8 @@ __device__ __forceinline__ void wg_env(const WgParams& P, WgShared& sh, const Ta
     const uint32_t fix = sh.fix[k & 1];
     if (fix & 1u) {
       wg_env_slow<NS>(P, sh, tb, L.CS(k), k, stg, dn, pre, bm, ae);
+    } else if (envcells) {
+      wg_env_cells<NS>(P, sh, tb, L.CS(k), stg, dn, pre, bm, ae);
     } else {
 #pragma unroll
       for (int s = 0; s < NS; ++s)

@@ -257,13 +257,14 @@ def test_wgrid_goal_crowd_bit_exact(B, frac, gpu_device):
     _check_chunks(env, ora, (6, 1, 9), action_seed=11, n_act=4)
 
 
-@pytest.mark.parametrize("tmode", [4, 64, 128, 32 | 512, 8 | 16, 4096, 8192])
+@pytest.mark.parametrize("tmode", [4, 64, 128, 32 | 512, 8 | 16, 4096, 8192, 16384, 16384 | 128])
 def test_wgrid_schedule_variants_bit_exact(tmode, gpu_device):
     """Test-only schedules of the windowed kernel (gp_debug_set wg_tmode, wgrid.hip TM_*): 4 = next actions loaded
     after the transitions, 64 = store waves copy a step as soon as it is final, 128 = no candidate cells (every
     resetter's word drawn after the exchange), 32|512 = env-wave priority off / always high, 8|16 = throttled
-    stores and busy polling, 4096 = next actions loaded at the step start, 8192 = round 5's prologue. Results must
-    not depend on the schedule."""
+    stores and busy polling, 4096 = next actions loaded at the step start, 8192 = round 5's prologue, 16384 = the
+    control wave places the resetters' cells (at this size the env waves do by default). Results must not depend
+    on the schedule."""
     from gym_po_amd._lib import debug_knobs
     B = 1 << 18
     with debug_knobs(wg_tmode=tmode):
