@@ -44,6 +44,7 @@ const char* gp_derr_text(uint32_t flags) {
 
 static GpDebugKnobs g_dbg;
 const GpDebugKnobs& gp_debug_knobs() { return g_dbg; }
+extern int gp_xg_graph_knob;  // crooms.hip: exact mode's K-step launch sequence as a hipGraph (-1 / 0 / 1)
 
 int DevErr::clear() {
   if (!buf.p) return GP_OK;
@@ -229,13 +230,17 @@ int gp_debug_set(const char* key, int64_t value) {
   else if (!strcmp(key, "xg_ppt_min")) g_dbg.xg_ppt_min = (int)value;
   else if (!strcmp(key, "xg_spb_min")) g_dbg.xg_spb_min = (int)value;
   else if (!strcmp(key, "persist_bpc")) g_dbg.persist_bpc = (int)value;
+  else if (!strcmp(key, "xg_graph")) gp_xg_graph_knob = (int)value;  // (crooms.hip: read at create)
   else {
     gp_set_error("gp_debug_set: unknown key '%s'", key);
     return GP_E_INVALID;
   }
   return GP_OK;
 }
-void gp_debug_reset(void) { g_dbg = GpDebugKnobs{}; }
+void gp_debug_reset(void) {
+  g_dbg = GpDebugKnobs{};
+  gp_xg_graph_knob = -1;
+}
 int gp_abi_version(void) { return GP_ABI_VERSION; }
 
 // Makes the env's device current for one C-ABI call and gives the calling thread its own current device back on

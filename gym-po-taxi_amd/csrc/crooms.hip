@@ -34,6 +34,9 @@
 
 #pragma clang fp contract(off)
 
+// gp_debug_set("xg_graph"), read at create (CRoomsBackend::xg_graph_mode): -1 default, 0 never, 1 from the first call.
+int gp_xg_graph_knob = -1;
+
 namespace {
 
 constexpr int TPB = 256;
@@ -2350,6 +2353,49 @@ struct CRoomsBackend : EnvBackend {
   DevBuf xg_jt, xg_bits, xg_pbits, xg_bstate, xg_span, xg_val, xg_cnt, xg_ebits;
   DevBuf xg_tbc, xg_tgs, xg_tacc;  // the fused normal call's tagged counts (tacc zero between launches)
   uint32_t xg_tag = 0;
+  // Round 6: xg_rollout's K-step launch sequence (5-6 dependent launches per step, all sized on the host from B and
+  // K alone) captured once and replayed as a hipGraph: a dependent launch costs ~1 us less replayed than launched
+  // (tools/mb_graph.hip, profiles/r06_mb_graph.txt). A captured fused call's tag is fixed (bit 31 set; eager tags
+  // stay below it), and the graph ends by clearing the tagged slots, so no replay finds one of its tags already
+  // published. One graph is kept, keyed by K, the caller's buffers and the geometry knobs; by default it is
+  // captured on the second identical call (a one-off call stays eager), up to XG_GRAPH_MAX_ENVS envs: replayed vs
+  // launched, µs/step (profiles/r06_crooms_numpy_graph_ab.txt) 32.0 vs 36.5 at 4,096 envs, 49.7 vs 50.0 at 65,536,
+  // but 76.6 vs 74.2 at 2^18 (not explained) and 290-292 vs 289-303 at 2^21: eager launches above 65,536 envs.
+  static constexpr int64_t XG_GRAPH_MAX_ENVS = 65536;
+  struct XgGraphKey {
+    int K = -1;
+    const void *act = nullptr, *obs = nullptr, *rew = nullptr, *term = nullptr, *trunc = nullptr;
+    int spb = 0, ppt = 0;
+    bool operator==(const XgGraphKey& o) const {
+      return K == o.K && act == o.act && obs == o.obs && rew == o.rew && term == o.term && trunc == o.trunc &&
+             spb == o.spb && ppt == o.ppt;
+    }
+  };
+  int xg_graph_mode = -1;  // gp_debug_set("xg_graph") at create: -1 from the 2nd identical call, 0 never, 1 always
+  bool xg_graph_broken = false;  // a capture failed: eager launches from then on
+  XgGraphKey xg_gkey, xg_glast;  // the graph's key; the last eager call's
+  hipGraph_t xg_graph = nullptr;
+  hipGraphExec_t xg_gexec = nullptr;
+  hipStream_t xg_cap = nullptr;  // the capture stream (the caller's may be the null stream, which cannot capture)
+  bool xg_capturing = false;
+  uint32_t xg_gtag = 0;
+  uint32_t xg_next_tag() {
+    if (xg_capturing) return 0x80000000u | ++xg_gtag;
+    if (++xg_tag >= 0x80000000u) xg_tag = 1;  // (a wrapped tag could only meet slots 2^31 launches old)
+    return xg_tag;
+  }
+  void xg_graph_drop() {
+    if (xg_gexec) (void)hipGraphExecDestroy(xg_gexec);
+    if (xg_graph) (void)hipGraphDestroy(xg_graph);
+    xg_gexec = nullptr;
+    xg_graph = nullptr;
+    xg_gkey = XgGraphKey{};
+  }
+  ~CRoomsBackend() override {
+    xg_graph_drop();
+    if (xg_cap) (void)hipStreamDestroy(xg_cap);
+  }
+  int xg_graph_capture(const XgGraphKey& key, const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc);
 #ifdef GP_STAMPS
   DevBuf xg_dbg;  // [6 kinds][1024 blocks][8] stamps (tools/xstamps.py)
   int debug_stamps(unsigned long long* out, int cap) override {
@@ -2455,8 +2501,7 @@ struct CRoomsBackend : EnvBackend {
       a.tbc = xg_tbc.as<unsigned long long>();
       a.tgs = xg_tgs.as<unsigned long long>();
       a.tacc = xg_tacc.as<unsigned long long>();
-      if (++xg_tag == 0) xg_tag = 1;  // (a wrapped tag could only meet slots 2^32 launches old)
-      a.tag = xg_tag;
+      a.tag = xg_next_tag();
       if (ppt == 4) hipLaunchKernelGGL(xg_norm_fused<4>, dim3(nbp), dim3(XGT), 0, s, a);
       else hipLaunchKernelGGL(xg_norm_fused<1>, dim3(nbp), dim3(XGT), 0, s, a);
     }
@@ -2475,8 +2520,7 @@ struct CRoomsBackend : EnvBackend {
       a.tbc = xg_tbc.as<unsigned long long>();
       a.tgs = xg_tgs.as<unsigned long long>();
       a.tacc = xg_tacc.as<unsigned long long>();
-      if (++xg_tag == 0) xg_tag = 1;
-      a.tag = xg_tag;
+      a.tag = xg_next_tag();
       hipLaunchKernelGGL(xg_cho_fused, dim3(nbc), dim3(XGT), 0, s, a);
     }
     xg_slot ^= 1;
@@ -2493,6 +2537,7 @@ struct CRoomsBackend : EnvBackend {
   }
   int xg_reset(void* obs, hipStream_t s);
   int xg_rollout(int K, const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc, hipStream_t s);
+  int xg_launches(int K, const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc, hipStream_t s);
   const uint64_t* rp_u = nullptr;
   const int32_t* rp_goal = nullptr;
   const int32_t* rp_agent = nullptr;
@@ -2953,6 +2998,7 @@ int CRoomsBackend::build(const gp_crooms_config* cfg) {
   if ((e = derr.alloc())) return e;
   d.derr = derr.ptr();
   xg_split = gp_debug_knobs().disable_fused != 0;
+  xg_graph_mode = gp_xg_graph_knob;
   if (rng_mode == GP_RNG_NUMPY && (e = x_alloc())) return e;
   return GP_OK;
 }
@@ -3028,6 +3074,69 @@ int CRoomsBackend::xg_reset(void* obs, hipStream_t s) {  // crooms.py:251-266: g
 
 int CRoomsBackend::xg_rollout(int K, const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc,
                               hipStream_t s) {
+  if (xg_graph_mode == 0 || (xg_graph_mode < 0 && B > XG_GRAPH_MAX_ENVS) || xg_graph_broken || !xg_fused())
+    return xg_launches(K, act, obs, rew, term, trunc, s);
+  XgGraphKey key;
+  key.K = K;
+  key.act = act;
+  key.obs = obs;
+  key.rew = rew;
+  key.term = term;
+  key.trunc = trunc;
+  key.spb = gp_debug_knobs().xg_spb_min;
+  key.ppt = gp_debug_knobs().xg_ppt_min;
+  if (!(xg_gexec && key == xg_gkey)) {
+    const bool again = key == xg_glast;
+    xg_glast = key;
+    if (xg_graph_mode < 0 && !again) return xg_launches(K, act, obs, rew, term, trunc, s);
+    if (xg_graph_capture(key, act, obs, rew, term, trunc)) return xg_launches(K, act, obs, rew, term, trunc, s);
+  }
+  GP_HIP_CHECK(hipGraphLaunch(xg_gexec, s));
+  return GP_OK;
+}
+
+// Captures xg_launches(K, ...) plus the clearing of the tagged count slots into xg_gexec; nonzero (and eager
+// launches from then on) if the runtime refuses any of it.
+int CRoomsBackend::xg_graph_capture(const XgGraphKey& key, const void* act, void* obs, float* rew, uint8_t* term,
+                                    uint8_t* trunc) {
+  xg_graph_drop();
+  if (!xg_cap && hipStreamCreateWithFlags(&xg_cap, hipStreamNonBlocking) != hipSuccess) {
+    xg_cap = nullptr;
+    xg_graph_broken = true;
+    return 1;
+  }
+  if (hipStreamBeginCapture(xg_cap, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+    (void)hipGetLastError();
+    xg_graph_broken = true;
+    return 1;
+  }
+  xg_capturing = true;
+  xg_gtag = 0;
+  int e = xg_launches(key.K, act, obs, rew, term, trunc, xg_cap);
+  xg_capturing = false;
+  if (!e && (hipMemsetAsync(xg_tbc.p, 0, xg_tbc.n, xg_cap) != hipSuccess ||
+             hipMemsetAsync(xg_tgs.p, 0, xg_tgs.n, xg_cap) != hipSuccess))
+    e = 1;
+  hipGraph_t g = nullptr;
+  if (hipStreamEndCapture(xg_cap, &g) != hipSuccess || !g) e = 1;
+  if (!e && hipGraphInstantiate(&xg_gexec, g, nullptr, nullptr, 0) != hipSuccess) {
+    xg_gexec = nullptr;
+    e = 1;
+  }
+  xg_slot = 0;
+  if (e) {
+    if (g) (void)hipGraphDestroy(g);
+    (void)hipGetLastError();
+    xg_graph_broken = true;
+    return 1;
+  }
+  xg_graph = g;
+  xg_gkey = key;
+  return 0;
+}
+
+int CRoomsBackend::xg_launches(int K, const void* act, void* obs, float* rew, uint8_t* term, uint8_t* trunc,
+                               hipStream_t s) {
   xg_slot = 0;
   CrDev dd = dev_for_launch();
   dd.rp_u = xd.u;  // the per-env draws of the call sequence, consumed by the replay step

@@ -116,6 +116,58 @@ def test_numpy_mode_both_paths_across_crossover(case, xg_min, gpu_device):
         test_numpy_mode_vs_oracle(*case, gpu_device)
 
 
+# Round 6: the grid-wide K-step launch sequence replayed as a hipGraph (gp_debug_set xg_graph at create): 1 = from
+# the first call (every call above captures anew or replays), 0 = never (the eager launches).
+GRAPH_CASES = [(ORACLE_CASES[5], 1), (ORACLE_CASES[6], 1), (ORACLE_CASES[9], 1), (ORACLE_CASES[8], 0),
+               (ORACLE_CASES[5], 0)]
+
+
+@pytest.mark.parametrize("case,mode", GRAPH_CASES)
+def test_numpy_mode_graph_knob_vs_oracle(case, mode, gpu_device):
+    from gym_po_amd._lib import debug_knobs
+    with debug_knobs(xg_graph=mode):
+        test_numpy_mode_vs_oracle(*case, gpu_device)
+
+
+@pytest.mark.parametrize("mode", [-1, 1])
+@pytest.mark.parametrize("kw,B,K", [({"obs_type": "vector_goal_mdp", "goal_xy": None, "use_velocity": True,
+                                      "time_limit": 7}, 30001, 4),
+                                     ({"obs_type": "vector_mdp", "action_std": 0.5, "time_limit": 5}, 65536, 3)])
+def test_numpy_mode_graph_replay_vs_oracle(kw, B, K, mode, gpu_device):
+    """The same action / output buffers on every call (rollout_plan), so the graph is replayed: by default it is
+    captured on the 2nd call and replayed from the 3rd. Every step against the oracle, and the final PCG64 state."""
+    import torch
+    from gym_po_amd import CRoomsEnv
+    from gym_po_amd._lib import debug_knobs
+    calls = 6
+    acts = np.random.default_rng(5).uniform(-1, 1, (calls * K, B, 2))
+    ora = CRoomsOracle(B, **kw)
+    o_ref = ora.reset_seed(77)
+    with debug_knobs(xg_graph=mode):
+        env = CRoomsEnv(B, **kw, rng_mode="numpy", dtype=torch.float64)
+    o = env.reset(seed=77).cpu().numpy()
+    np.testing.assert_array_equal(o.astype(np.float64), np.asarray(o_ref).astype(np.float64))
+    a = torch.zeros((K, B, 2), dtype=torch.float64, device=env.device)
+    run, (obs, rew, term, trunc) = env.rollout_plan(a)
+    eps = 0
+    for c in range(calls):
+        a.copy_(torch.as_tensor(acts[c * K:(c + 1) * K]))
+        run()
+        got = [x.cpu().numpy() for x in (obs, rew, term, trunc)]
+        for j in range(K):
+            ro, rr, rd, rt = ora.step_seeded(acts[c * K + j])
+            tag = f"call {c} step {j}"
+            np.testing.assert_array_equal(got[0][j].astype(np.float64), np.asarray(ro).astype(np.float64),
+                                          err_msg="obs " + tag)
+            np.testing.assert_array_equal(got[1][j], rr, err_msg="rew " + tag)
+            np.testing.assert_array_equal(got[2][j].astype(bool), rd, err_msg="term " + tag)
+            np.testing.assert_array_equal(got[3][j].astype(bool), rt, err_msg="trunc " + tag)
+            eps += int((rd | rt).sum())
+        assert _dev_state(env) == _np_state(ora.gen), f"PCG64 state after call {c}"
+    m = env.metrics()
+    assert m["episodes"] == eps and m["env_steps"] == calls * K * B
+
+
 @pytest.mark.parametrize("kw,B,steps,K", ORACLE_CASES)
 def test_numpy_mode_vs_oracle(kw, B, steps, K, gpu_device):
     """Every step against the oracle on numpy's Generator; K-step launches; final PCG64 state."""
